@@ -1,0 +1,767 @@
+// msgpu.hip — libmsgpu: host orchestration and the C ABI (include/msgpu.h).
+//
+// One msg_render_batch call renders N independent presets (each one call of
+// the reference's render(), microsound_0.2.1/main_v2.py:588-792) on one
+// MI355X: device planner -> generator -> LDS spectral chain -> overlap-add x
+// ADSR -> partitioned FFT FIR (ER + IR) -> stereo/tanh/normalise.  All work is
+// batched across presets so every launch has thousands of workgroups.
+#include <hip/hip_runtime.h>
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "msg_common.h"
+#include "ziggurat_tables.h"
+#include "nprng.h"
+#include "plan.h"
+#include "fftplan.h"
+#include "fft_lds.h"
+#include "kernels.h"
+#include "../../include/msgpu.h"
+
+namespace {
+
+const nprng::Zig kHostZig = {zig_ki_double, zig_wi_double, zig_fi_double,
+                             zig_ke_double, zig_we_double, zig_fe_double};
+
+constexpr int SPEC_T_BIG = 1024, SPEC_C_BIG = 20480;    // 160 KiB LDS
+constexpr int SPEC_T_SMALL = 256, SPEC_C_SMALL = 8192;  // 64 KiB LDS
+constexpr int FIR_T = 1024, FIR_C = 16385;              // N <= 32768 real
+constexpr int FIR_NMAX = 32768;
+
+thread_local std::string g_err;   // errors before a context exists
+
+template <class T>
+struct DevBuf {
+    T* p = nullptr;
+    size_t cap = 0;   // elements
+    hipError_t ensure(size_t n) {
+        if (n <= cap && p) return hipSuccess;
+        if (p) { hipFree(p); p = nullptr; cap = 0; }
+        size_t want = std::max<size_t>(n, 1);
+        want = want + want / 4;
+        hipError_t e = hipMalloc(&p, want * sizeof(T));
+        if (e == hipSuccess) cap = want;
+        return e;
+    }
+    void release() { if (p) hipFree(p); p = nullptr; cap = 0; }
+};
+
+struct PlanStore {
+    std::vector<RealPlan> host;          // descriptors (device pointers inside)
+    std::vector<void*> allocs;
+    std::map<int, int> by_n;
+    bool dirty = false;
+    DevBuf<RealPlan> dev;
+};
+
+}  // namespace
+
+struct msg_ctx {
+    int device = 0;
+    std::string err;
+    bool profiling = false;
+    float stage_ms[8] = {0};
+    hipEvent_t ev[9] = {};
+    // constant tables
+    uint64_t* d_ki = nullptr; double* d_wi = nullptr; double* d_fi = nullptr;
+    uint64_t* d_ke = nullptr; double* d_we = nullptr; double* d_fe = nullptr;
+    JumpTab* d_jump = nullptr;
+    nprng::Zig dzig{};
+    PlanStore grain_plans, fir_plans;
+    // per-batch buffers
+    DevBuf<msg_preset> presets;
+    DevBuf<int64_t> frag_len;
+    DevBuf<msg_plan_info> info;
+    DevBuf<int32_t> slot_base, tap_base;
+    DevBuf<msg_event> events;
+    DevBuf<int32_t> er_off;
+    DevBuf<double> er_gain;
+    DevBuf<EventRt> ert;
+    DevBuf<PresetRt> prt;
+    DevBuf<int32_t> gen_list, spec_small, spec_big, tile_begin, fir_begin, h_begin, st_begin, fir_plan_of;
+    DevBuf<float> micro, grain, mono_a, mono_y;
+    DevBuf<float2> hspec;
+    DevBuf<double> irbank;
+    DevBuf<unsigned> maxbits;
+    // host mirrors of the last batch
+    std::vector<msg_plan_info> h_info;
+    std::vector<msg_event> h_events;
+    std::vector<PresetRt> h_prt;
+    std::vector<int32_t> h_slot_base;
+    int32_t last_n = 0;
+};
+
+#define HIPCHK(ctx, expr)                                                        \
+    do {                                                                         \
+        hipError_t _e = (expr);                                                  \
+        if (_e != hipSuccess) {                                                  \
+            (ctx)->err = std::string(#expr) + ": " + hipGetErrorString(_e);      \
+            return MSG_E_DEVICE;                                                 \
+        }                                                                        \
+    } while (0)
+
+static int fail(msg_ctx* ctx, int code, const std::string& msg) {
+    if (ctx) ctx->err = msg; else g_err = msg;
+    return code;
+}
+
+// ---------------------------------------------------------------------------
+// FFT plan creation
+// ---------------------------------------------------------------------------
+static hipError_t upload(PlanStore& ps, const std::vector<float>& v, const float2** out) {
+    void* d = nullptr;
+    hipError_t e = hipMalloc(&d, v.size() * sizeof(float));
+    if (e != hipSuccess) return e;
+    e = hipMemcpy(d, v.data(), v.size() * sizeof(float), hipMemcpyHostToDevice);
+    ps.allocs.push_back(d);
+    *out = reinterpret_cast<const float2*>(d);
+    return e;
+}
+
+static bool make_fftdesc(PlanStore& ps, int m, FftDesc& d, std::string& why) {
+    std::vector<int> rad;
+    memset(&d, 0, sizeof(d));
+    d.m = m;
+    if (fftplan::factor(m, rad)) {
+        d.blue = 0;
+        d.size = m;
+    } else {
+        d.blue = 1;
+        d.size = fftplan::next_pow2(2 * m - 1);
+        fftplan::factor(d.size, rad);
+        std::vector<float> chirp, bspec;
+        fftplan::bluestein(m, d.size, chirp, bspec);
+        if (upload(ps, chirp, &d.chirp) != hipSuccess || upload(ps, bspec, &d.bspec) != hipSuccess) {
+            why = "hip upload failed";
+            return false;
+        }
+    }
+    if ((int)rad.size() > 24) { why = "too many radix passes"; return false; }
+    d.nrad = (int)rad.size();
+    for (size_t i = 0; i < rad.size(); ++i) d.rad[i] = rad[i];
+    if (upload(ps, fftplan::twiddles(d.size), &d.tw) != hipSuccess) { why = "hip upload failed"; return false; }
+    return true;
+}
+
+// Real-FFT plan for n samples; returns index or -1.
+static int real_plan(PlanStore& ps, int n, std::string& why) {
+    auto it = ps.by_n.find(n);
+    if (it != ps.by_n.end()) return it->second;
+    RealPlan rp;
+    memset(&rp, 0, sizeof(rp));
+    rp.n = n;
+    rp.even = (n % 2 == 0);
+    const int m = rp.even ? n / 2 : n;
+    if (!make_fftdesc(ps, m, rp.c, why)) return -1;
+    rp.lds_c = std::max(rp.even ? m + 1 : m, rp.c.size);
+    if (rp.even) {
+        std::vector<float> t(2 * (size_t)(m + 1));
+        for (int k = 0; k <= m; ++k) {
+            const long double a = -2.0L * 3.14159265358979323846264338327950288L * k / (long double)n;
+            t[2 * k] = (float)std::cos(a);
+            t[2 * k + 1] = (float)std::sin(a);
+        }
+        if (upload(ps, t, &rp.rtw) != hipSuccess) { why = "hip upload failed"; return -1; }
+    }
+    const int idx = (int)ps.host.size();
+    ps.host.push_back(rp);
+    ps.by_n[n] = idx;
+    ps.dirty = true;
+    return idx;
+}
+
+static hipError_t sync_plans(PlanStore& ps, hipStream_t s) {
+    if (!ps.dirty) return hipSuccess;
+    hipError_t e = ps.dev.ensure(ps.host.size());
+    if (e != hipSuccess) return e;
+    e = hipMemcpyAsync(ps.dev.p, ps.host.data(), ps.host.size() * sizeof(RealPlan), hipMemcpyHostToDevice, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    ps.dirty = false;
+    return e;
+}
+
+// Bessel J_m(x), m >= 0, power series (x <= 0.9 here).
+static double bessel_j(int m, double x) {
+    double term = 1.0;
+    for (int k = 1; k <= m; ++k) term *= (x / 2.0) / k;
+    double sum = term;
+    for (int k = 1; k < 60; ++k) {
+        term *= -(x / 2.0) * (x / 2.0) / ((double)k * (double)(k + m));
+        sum += term;
+        if (std::fabs(term) < 1e-30) break;
+    }
+    return sum;
+}
+
+// Choose (N, P, Q) minimising FFT work for an M-tap FIR over n outputs.
+static void choose_fir(int64_t M, int64_t n, int& N, int& P, int& Q) {
+    double best = 1e300;
+    N = FIR_NMAX; P = (int)std::min<int64_t>(M, FIR_NMAX / 2); Q = (int)((M + P - 1) / P);
+    for (int lg = 10; lg <= 15; ++lg) {
+        const int NN = 1 << lg;
+        for (int q = 1; q <= 64; ++q) {
+            const int64_t pp = (M + q - 1) / q;
+            if (pp >= NN) continue;
+            const int64_t B = NN - pp + 1;
+            const int64_t blocks = (n + B - 1) / B;
+            const double cost = (double)blocks * (q + 1) * NN * lg + (double)blocks * NN * 4.0;
+            if (cost < best) { best = cost; N = NN; P = (int)pp; Q = q; }
+        }
+    }
+}
+
+static int spec_ops(const msg_preset& p, const msg_event& e) {
+    int ops = 0;
+    if (p.gen_mode == MSG_GEN_NOISE_BURST || p.gen_mode == MSG_GEN_FALLBACK) ops |= SPEC_TILT_NOISE;
+    if (p.gen_mode == MSG_GEN_SKEWED) ops |= SPEC_TILT_SKEW;
+    if ((p.flags & MSG_F_BANDLIMIT) && e.n >= 8) ops |= SPEC_LOWPASS;
+    if ((p.flags & MSG_F_NL_WARP) && e.n >= 16) ops |= SPEC_WARP;
+    if (!(p.flags & MSG_F_PARTIAL_LOCK) && e.n >= 16 && std::fabs(e.stretch - 1.0) >= 1e-9) ops |= SPEC_STRETCH;
+    return ops;
+}
+
+static bool supported(const msg_preset& p, std::string& why) {
+    const uint32_t unsupported = MSG_F_PARTIAL_LOCK | MSG_F_CEP_WARP | MSG_F_RES_BANK | MSG_F_WAVEGUIDE |
+                                 MSG_F_EVENT_FEEDBACK | MSG_F_IMPRINT | MSG_F_MULTIBAND;
+    if (p.flags & unsupported) { why = "preset uses a stage not yet on the GPU path (flags 0x" +
+                                       std::to_string(p.flags & unsupported) + ")"; return false; }
+    switch (p.gen_mode) {
+        case MSG_GEN_GAUSSIAN_CLICK: case MSG_GEN_NOISE_BURST: case MSG_GEN_SKEWED:
+        case MSG_GEN_RESONANT: case MSG_GEN_FALLBACK: break;
+        default: why = "generator mode " + std::to_string(p.gen_mode) + " not yet on the GPU path"; return false;
+    }
+    return true;
+}
+
+static void stage_mark(msg_ctx* ctx, int i, hipStream_t s) {
+    if (ctx->profiling) hipEventRecord(ctx->ev[i], s);
+}
+
+// ---------------------------------------------------------------------------
+// C ABI
+// ---------------------------------------------------------------------------
+extern "C" {
+
+int msg_abi_version(void) { return MSG_ABI_VERSION; }
+
+int64_t msg_sizeof(int32_t which) {
+    switch (which) {
+        case 0: return (int64_t)sizeof(msg_preset);
+        case 1: return (int64_t)sizeof(msg_event);
+        case 2: return (int64_t)sizeof(msg_plan_info);
+        default: return -1;
+    }
+}
+
+const char* msg_last_error(msg_ctx* ctx) { return ctx ? ctx->err.c_str() : g_err.c_str(); }
+
+msg_ctx* msg_create(int device_ordinal) {
+    int ndev = 0;
+    hipError_t e = hipGetDeviceCount(&ndev);
+    if (e != hipSuccess || ndev <= 0) { g_err = "no HIP device available"; return nullptr; }
+    if (device_ordinal < 0 || device_ordinal >= ndev) { g_err = "bad device ordinal"; return nullptr; }
+    if (hipSetDevice(device_ordinal) != hipSuccess) { g_err = "hipSetDevice failed"; return nullptr; }
+    std::unique_ptr<msg_ctx> ctx(new msg_ctx());
+    ctx->device = device_ordinal;
+    auto up = [&](auto*& dst, const auto* src, size_t n) {
+        using T = std::remove_pointer_t<std::remove_reference_t<decltype(dst)>>;
+        if (hipMalloc(&dst, n * sizeof(T)) != hipSuccess) return false;
+        return hipMemcpy(dst, src, n * sizeof(T), hipMemcpyHostToDevice) == hipSuccess;
+    };
+    if (!up(ctx->d_ki, zig_ki_double, 256) || !up(ctx->d_wi, zig_wi_double, 256) ||
+        !up(ctx->d_fi, zig_fi_double, 256) || !up(ctx->d_ke, zig_ke_double, 256) ||
+        !up(ctx->d_we, zig_we_double, 256) || !up(ctx->d_fe, zig_fe_double, 256)) {
+        g_err = "uploading ziggurat tables failed";
+        return nullptr;
+    }
+    ctx->dzig = nprng::Zig{ctx->d_ki, ctx->d_wi, ctx->d_fi, ctx->d_ke, ctx->d_we, ctx->d_fe};
+    JumpTab jt;
+    for (int l = 0; l < GEN_T; ++l) {
+        const nprng::Jump j = nprng::jump_of((uint64_t)l + 1);
+        jt.a[l] = j.a; jt.s[l] = j.s;
+    }
+    const nprng::Jump j64 = nprng::jump_of(GEN_T);
+    jt.a64 = j64.a; jt.s64 = j64.s;
+    if (!up(ctx->d_jump, &jt, 1)) { g_err = "uploading jump table failed"; return nullptr; }
+    for (auto& ev : ctx->ev) hipEventCreate(&ev);
+    hipFuncSetAttribute((const void*)k_spectral<SPEC_T_BIG, SPEC_C_BIG>,
+                        hipFuncAttributeMaxDynamicSharedMemorySize, SPEC_C_BIG * 8);
+    hipFuncSetAttribute((const void*)k_fir<FIR_T, FIR_C>, hipFuncAttributeMaxDynamicSharedMemorySize, FIR_C * 8);
+    hipFuncSetAttribute((const void*)k_fir_h<FIR_T, FIR_C>, hipFuncAttributeMaxDynamicSharedMemorySize, FIR_C * 8);
+    return ctx.release();
+}
+
+void msg_destroy(msg_ctx* ctx) {
+    if (!ctx) return;
+    hipSetDevice(ctx->device);
+    hipDeviceSynchronize();
+    for (PlanStore* ps : {&ctx->grain_plans, &ctx->fir_plans}) {
+        for (void* p : ps->allocs) hipFree(p);
+        ps->dev.release();
+    }
+    hipFree(ctx->d_ki); hipFree(ctx->d_wi); hipFree(ctx->d_fi);
+    hipFree(ctx->d_ke); hipFree(ctx->d_we); hipFree(ctx->d_fe); hipFree(ctx->d_jump);
+    for (auto& ev : ctx->ev) hipEventDestroy(ev);
+    ctx->presets.release(); ctx->frag_len.release(); ctx->info.release(); ctx->slot_base.release();
+    ctx->tap_base.release(); ctx->events.release(); ctx->er_off.release(); ctx->er_gain.release();
+    ctx->ert.release(); ctx->prt.release(); ctx->gen_list.release(); ctx->spec_small.release();
+    ctx->spec_big.release(); ctx->tile_begin.release(); ctx->fir_begin.release(); ctx->h_begin.release();
+    ctx->st_begin.release(); ctx->fir_plan_of.release(); ctx->micro.release(); ctx->grain.release();
+    ctx->mono_a.release(); ctx->mono_y.release(); ctx->hspec.release(); ctx->irbank.release();
+    ctx->maxbits.release();
+    delete ctx;
+}
+
+int msg_set_profiling(msg_ctx* ctx, int32_t on) {
+    if (!ctx) return MSG_E_ARG;
+    ctx->profiling = on != 0;
+    return MSG_OK;
+}
+
+int msg_stage_times(msg_ctx* ctx, float* ms, int32_t n) {
+    if (!ctx || !ms) return MSG_E_ARG;
+    for (int i = 0; i < n && i < 8; ++i) ms[i] = ctx->stage_ms[i];
+    return MSG_OK;
+}
+
+int msg_plan_host(const msg_preset* preset, const double* ir_frag, int64_t ir_frag_len,
+                  msg_plan_info* info, msg_event* events, int32_t max_events,
+                  int32_t* er_off, double* er_gain) {
+    (void)ir_frag;
+    if (!preset || !info) return fail(nullptr, MSG_E_ARG, "null argument");
+    msg_plan_info sz;
+    msgplan::plan_sizes(*preset, kHostZig, ir_frag_len, sz);
+    *info = sz;
+    if (!events) return MSG_OK;
+    if (sz.n_slots > max_events) return fail(nullptr, MSG_E_ARG, "event buffer too small");
+    const bool er = (preset->flags & MSG_F_ER_CLOUD) != 0;
+    msgplan::plan_events(*preset, kHostZig, ir_frag_len, 0, *info, events,
+                         er ? er_off : nullptr, er ? er_gain : nullptr);
+    return MSG_OK;
+}
+
+int msg_rng_raw(uint64_t seed, uint64_t* out, int64_t n) {
+    nprng::Pcg64 g = nprng::default_rng(seed);
+    for (int64_t i = 0; i < n; ++i) out[i] = nprng::next_u64(g);
+    return MSG_OK;
+}
+int msg_rng_normal(uint64_t seed, double* out, int64_t n) {
+    nprng::Pcg64 g = nprng::default_rng(seed);
+    for (int64_t i = 0; i < n; ++i) out[i] = nprng::standard_normal(g, kHostZig);
+    return MSG_OK;
+}
+int msg_rng_exponential(uint64_t seed, double* out, int64_t n) {
+    nprng::Pcg64 g = nprng::default_rng(seed);
+    for (int64_t i = 0; i < n; ++i) out[i] = nprng::standard_exponential(g, kHostZig);
+    return MSG_OK;
+}
+int msg_rng_integers(uint64_t seed, int64_t low, int64_t high, int64_t* out, int64_t n) {
+    if (high <= low) return fail(nullptr, MSG_E_VALUE, "low >= high");
+    nprng::Pcg64 g = nprng::default_rng(seed);
+    for (int64_t i = 0; i < n; ++i) out[i] = nprng::integers(g, low, high);
+    return MSG_OK;
+}
+
+// Host emulation of k_gen_normal's chunked walk (same decisions, sequential lanes).
+int msg_rng_normal_chunked(uint64_t seed, double* out, int64_t n) {
+    const nprng::Pcg64 g0 = nprng::default_rng(seed);
+    nprng::Jump ja[64];
+    for (int l = 0; l < 64; ++l) ja[l] = nprng::jump_of((uint64_t)l + 1);
+    const nprng::Jump j64 = nprng::jump_of(64);
+    nprng::u128 st[64];
+    for (int l = 0; l < 64; ++l) st[l] = ja[l].a * g0.state + g0.inc * ja[l].s;
+    int64_t produced = 0;
+    int local = 0;
+    while (produced < n) {
+        uint64_t rabs[64]; int idx[64]; double x[64]; uint64_t F = 0;
+        for (int l = 0; l < 64; ++l) {
+            const uint64_t raw = nprng::xsl_rr(st[l]);
+            idx[l] = (int)(raw & 0xff);
+            const uint64_t rr = raw >> 8;
+            rabs[l] = (rr >> 1) & 0x000fffffffffffffULL;
+            x[l] = (double)rabs[l] * zig_wi_double[idx[l]];
+            if (rr & 1) x[l] = -x[l];
+            if (rabs[l] < zig_ki_double[idx[l]]) F |= 1ULL << l;
+        }
+        while (local < 64 && produced < n) {
+            const uint64_t S = ~F & (~0ULL << local);
+            const int q = S ? __builtin_ctzll(S) : 64;
+            for (int l = local; l < q; ++l) {
+                const int64_t j = produced + l - local;
+                if (j < n) out[j] = x[l];
+            }
+            produced += q - local;
+            if (q == 64) { local = 64; break; }
+            nprng::Pcg64 g;
+            g.state = st[q]; g.inc = g0.inc; g.has_u32 = 0; g.u32 = 0;
+            // replicate slow_normal (host copy of the same control flow)
+            int c = 1;
+            uint64_t ra = rabs[q]; int id = idx[q]; double xv = x[q]; double v = 0.0;
+            for (;;) {
+                if (id == 0) {
+                    for (;;) {
+                        const double xx = -nprng::ZIG_NOR_INV_R * log1p(-nprng::next_double(g));
+                        const double yy = -log1p(-nprng::next_double(g));
+                        c += 2;
+                        if (yy + yy > xx * xx) { v = ((ra >> 8) & 1) ? -(nprng::ZIG_NOR_R + xx) : nprng::ZIG_NOR_R + xx; break; }
+                    }
+                    break;
+                }
+                const double u = nprng::next_double(g);
+                c += 1;
+                if (((zig_fi_double[id - 1] - zig_fi_double[id]) * u + zig_fi_double[id]) < exp(-0.5 * xv * xv)) { v = xv; break; }
+                uint64_t r = nprng::next_u64(g);
+                c += 1;
+                id = (int)(r & 0xff); r >>= 8;
+                const int sign = (int)(r & 1);
+                ra = (r >> 1) & 0x000fffffffffffffULL;
+                xv = (double)ra * zig_wi_double[id];
+                if (sign) xv = -xv;
+                if (ra < zig_ki_double[id]) { v = xv; break; }
+            }
+            if (produced < n) out[produced] = v;
+            ++produced;
+            local = q + c;
+        }
+        do {
+            for (int l = 0; l < 64; ++l) st[l] = j64.a * st[l] + g0.inc * j64.s;
+            local -= 64;
+        } while (local >= 64);
+    }
+    return MSG_OK;
+}
+
+int msg_last_plan(msg_ctx* ctx, msg_plan_info* info, int32_t n_presets) {
+    if (!ctx || !info) return MSG_E_ARG;
+    if (n_presets > ctx->last_n) return fail(ctx, MSG_E_ARG, "n_presets exceeds last batch");
+    std::memcpy(info, ctx->h_info.data(), sizeof(msg_plan_info) * n_presets);
+    return MSG_OK;
+}
+
+int msg_last_events(msg_ctx* ctx, int32_t preset, msg_event* events, int32_t cap, int32_t* n) {
+    if (!ctx || !n) return MSG_E_ARG;
+    if (preset < 0 || preset >= ctx->last_n) return fail(ctx, MSG_E_ARG, "bad preset index");
+    const int32_t k = ctx->h_info[preset].n_events;
+    *n = k;
+    if (!events) return MSG_OK;
+    if (k > cap) return fail(ctx, MSG_E_ARG, "event buffer too small");
+    std::memcpy(events, ctx->h_events.data() + ctx->h_slot_base[preset], sizeof(msg_event) * k);
+    return MSG_OK;
+}
+
+int msg_last_meta(msg_ctx* ctx, int32_t preset, double* micro, double* grain, int64_t cap, int64_t* n) {
+    if (!ctx || !n) return MSG_E_ARG;
+    if (preset < 0 || preset >= ctx->last_n) return fail(ctx, MSG_E_ARG, "bad preset index");
+    hipSetDevice(ctx->device);
+    const msg_plan_info& inf = ctx->h_info[preset];
+    *n = 0;
+    if (inf.n_events <= 0) return MSG_OK;
+    const msg_event& e = ctx->h_events[ctx->h_slot_base[preset] + inf.n_events - 1];
+    if (e.n > cap) return fail(ctx, MSG_E_ARG, "meta buffer too small");
+    std::vector<float> tmp(e.n);
+    const int64_t off = ctx->h_prt[preset].pool_base + e.pool_off;
+    HIPCHK(ctx, hipDeviceSynchronize());
+    if (micro) {
+        HIPCHK(ctx, hipMemcpy(tmp.data(), ctx->micro.p + off, e.n * sizeof(float), hipMemcpyDeviceToHost));
+        for (int i = 0; i < e.n; ++i) micro[i] = tmp[i];
+    }
+    if (grain) {
+        HIPCHK(ctx, hipMemcpy(tmp.data(), ctx->grain.p + off, e.n * sizeof(float), hipMemcpyDeviceToHost));
+        for (int i = 0; i < e.n; ++i) grain[i] = tmp[i];
+    }
+    *n = e.n;
+    return MSG_OK;
+}
+
+int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
+                     const double* const* irs, const int64_t* ir_lens, int32_t n_irs,
+                     const uint8_t* const* images, const int32_t* img_h, const int32_t* img_w,
+                     int32_t n_images, float* out_dev, const int64_t* out_offsets, void* stream) {
+    (void)images; (void)img_h; (void)img_w; (void)n_images;
+    if (!ctx || !presets || P <= 0 || !out_dev || !out_offsets) return fail(ctx, MSG_E_ARG, "bad arguments");
+    hipStream_t s = (hipStream_t)stream;
+    HIPCHK(ctx, hipSetDevice(ctx->device));
+    for (int p = 0; p < P; ++p) {
+        std::string why;
+        if (!supported(presets[p], why)) return fail(ctx, MSG_E_UNSUPPORTED, "preset " + std::to_string(p) + ": " + why);
+        if (presets[p].n_bp[0] > MSG_MAX_BP || presets[p].n_bp[1] > MSG_MAX_BP ||
+            presets[p].n_bp[2] > MSG_MAX_BP || presets[p].n_bp[3] > MSG_MAX_BP)
+            return fail(ctx, MSG_E_ARG, "too many breakpoints");
+        const int ic = presets[p].ir_conv;
+        if (ic >= n_irs || (ic >= 0 && !irs)) return fail(ctx, MSG_E_ARG, "bad IR index");
+    }
+    stage_mark(ctx, 0, s);
+    // ---- phase 1: sizes ----
+    std::vector<int64_t> flen(P, 0);
+    for (int p = 0; p < P; ++p) {
+        const int f = presets[p].ir_frag;
+        flen[p] = (f >= 0 && f < n_irs) ? ir_lens[f] : 0;
+    }
+    HIPCHK(ctx, ctx->presets.ensure(P));
+    HIPCHK(ctx, ctx->frag_len.ensure(P));
+    HIPCHK(ctx, ctx->info.ensure(P));
+    HIPCHK(ctx, hipMemcpyAsync(ctx->presets.p, presets, sizeof(msg_preset) * P, hipMemcpyHostToDevice, s));
+    HIPCHK(ctx, hipMemcpyAsync(ctx->frag_len.p, flen.data(), sizeof(int64_t) * P, hipMemcpyHostToDevice, s));
+    const int pb = 64;
+    hipLaunchKernelGGL(k_plan_sizes, dim3((P + pb - 1) / pb), dim3(pb), 0, s,
+                       ctx->presets.p, P, ctx->frag_len.p, ctx->dzig, ctx->info.p);
+    HIPCHK(ctx, hipGetLastError());
+    std::vector<msg_plan_info> info(P);
+    HIPCHK(ctx, hipMemcpyAsync(info.data(), ctx->info.p, sizeof(msg_plan_info) * P, hipMemcpyDeviceToHost, s));
+    HIPCHK(ctx, hipStreamSynchronize(s));
+    // ---- phase 2: events + ER taps ----
+    std::vector<int32_t> slot_base(P), tap_base(P);
+    int64_t nslots = 0, ntaps = 0;
+    for (int p = 0; p < P; ++p) {
+        slot_base[p] = (int32_t)nslots;
+        tap_base[p] = (int32_t)ntaps;
+        nslots += info[p].n_slots;
+        if (presets[p].flags & MSG_F_ER_CLOUD) ntaps += std::max(1, presets[p].er_taps);
+    }
+    if (nslots > INT32_MAX / 2) return fail(ctx, MSG_E_UNSUPPORTED, "too many events in one batch");
+    HIPCHK(ctx, ctx->slot_base.ensure(P));
+    HIPCHK(ctx, ctx->tap_base.ensure(P));
+    HIPCHK(ctx, ctx->events.ensure(nslots));
+    HIPCHK(ctx, ctx->er_off.ensure(ntaps));
+    HIPCHK(ctx, ctx->er_gain.ensure(ntaps));
+    HIPCHK(ctx, hipMemcpyAsync(ctx->slot_base.p, slot_base.data(), sizeof(int32_t) * P, hipMemcpyHostToDevice, s));
+    HIPCHK(ctx, hipMemcpyAsync(ctx->tap_base.p, tap_base.data(), sizeof(int32_t) * P, hipMemcpyHostToDevice, s));
+    hipLaunchKernelGGL(k_plan_events, dim3((P + pb - 1) / pb), dim3(pb), 0, s,
+                       ctx->presets.p, P, ctx->frag_len.p, ctx->dzig, ctx->slot_base.p, ctx->tap_base.p,
+                       ctx->events.p, ctx->er_off.p, ctx->er_gain.p, ctx->info.p);
+    HIPCHK(ctx, hipGetLastError());
+    ctx->h_events.resize(nslots);
+    HIPCHK(ctx, hipMemcpyAsync(info.data(), ctx->info.p, sizeof(msg_plan_info) * P, hipMemcpyDeviceToHost, s));
+    if (nslots)
+        HIPCHK(ctx, hipMemcpyAsync(ctx->h_events.data(), ctx->events.p, sizeof(msg_event) * nslots,
+                                   hipMemcpyDeviceToHost, s));
+    HIPCHK(ctx, hipStreamSynchronize(s));
+    stage_mark(ctx, 1, s);
+
+    // ---- host: runtime records ----
+    std::vector<PresetRt> prt(P);
+    std::vector<EventRt> ert(nslots);
+    std::vector<int32_t> gen_list, spec_small, spec_big, tile_begin(P), fir_begin(P), h_begin(P), st_begin(P),
+        fir_plan_of(P, 0);
+    std::vector<double> irbank;
+    std::vector<int64_t> ir_off(std::max(n_irs, 1), 0);
+    for (int i = 0; i < n_irs; ++i) {
+        ir_off[i] = (int64_t)irbank.size();
+        irbank.insert(irbank.end(), irs[i], irs[i] + ir_lens[i]);
+    }
+    int64_t pool = 0, ysum = 0, hsum = 0;
+    int32_t tiles = 0, fblocks = 0, hblocks = 0, stiles = 0;
+    for (int p = 0; p < P; ++p) {
+        const msg_preset& pr = presets[p];
+        const msg_plan_info& inf = info[p];
+        PresetRt& r = prt[p];
+        memset(&r, 0, sizeof(r));
+        r.out_n = inf.out_n;
+        r.out_off = out_offsets[p];
+        r.pool_base = pool;
+        r.y_off = ysum;
+        r.ev_begin = slot_base[p];
+        r.n_events = inf.n_events;
+        r.er_base = tap_base[p];
+        r.n_taps = (pr.flags & MSG_F_ER_CLOUD) ? std::max(1, pr.er_taps) : 0;
+        r.tile_begin = tiles;
+        r.max_n = inf.max_n;
+        // ADSR (MS:173-177); A > n raises ValueError in the reference (MS:182)
+        const double sr = (double)pr.base_sr;
+        const int64_t A = std::max<int64_t>(0, (int64_t)std::nearbyint(sr * pr.env_a / 1000.0));
+        const int64_t D = std::max<int64_t>(0, (int64_t)std::nearbyint(sr * pr.env_d / 1000.0));
+        const int64_t R = std::max<int64_t>(0, (int64_t)std::nearbyint(sr * pr.env_r / 1000.0));
+        if (A > inf.out_n)
+            return fail(ctx, MSG_E_VALUE, "could not broadcast input array from shape (" + std::to_string(A) +
+                                              ",) into shape (" + std::to_string(inf.out_n) + ",)");
+        r.envA = (int32_t)A; r.envD = (int32_t)std::min<int64_t>(D, INT32_MAX);
+        r.envR = (int32_t)std::min<int64_t>(R, INT32_MAX);
+        r.envS = (float)std::min(std::max(pr.env_s, 0.0), 1.0);
+        r.envC = (float)std::max(1e-6, pr.env_curve);
+        // space FIR
+        const bool er = (pr.flags & MSG_F_ER_CLOUD) != 0;
+        const int ic = pr.ir_conv;
+        const bool ir = (pr.flags & MSG_F_SPACE_IR) && ic >= 0 && ir_lens[ic] > 0;   // size<8 check: caller
+        r.ir_len = ir ? (int32_t)std::min<int64_t>(ir_lens[ic], 8192) : 0;
+        r.ir_off = ir ? ir_off[ic] : 0;
+        r.fir_on = (er || ir) ? 1 : 0;
+        if (r.fir_on) {
+            const int64_t er_span = er ? (int64_t)std::nearbyint(pr.er_max_ms / 1000.0 * sr) + 1 : 0;
+            const int64_t M = (ir ? r.ir_len : 1) + er_span;
+            int N, Pp, Q;
+            choose_fir(M, inf.out_n, N, Pp, Q);
+            std::string why;
+            const int fp = real_plan(ctx->fir_plans, N, why);
+            if (fp < 0) return fail(ctx, MSG_E_DEVICE, "FIR plan: " + why);
+            fir_plan_of[p] = fp;
+            r.fir_N = N; r.fir_P = Pp; r.fir_Q = Q; r.fir_B = N - Pp + 1;
+            r.fir_block_begin = fblocks;
+            r.h_block_begin = hblocks;
+            r.h_off = hsum;
+            fblocks += (int32_t)((inf.out_n + r.fir_B - 1) / r.fir_B);
+            hblocks += Q;
+            hsum += (int64_t)Q * (N / 2 + 1);
+        }
+        fir_begin[p] = r.fir_block_begin;
+        h_begin[p] = r.h_block_begin;
+        // stereo (MS:423-436)
+        const double w = std::min(std::max(pr.stereo_width, 0.0), 1.0);
+        const bool stereo = (pr.flags & MSG_F_STEREO) && inf.out_n >= 64;
+        if (stereo && (inf.out_n % 2))
+            return fail(ctx, MSG_E_UNSUPPORTED, "stereo diffusion of an odd-length output is not yet on the GPU path");
+        r.stereo_fir = stereo ? 1 : 0;
+        r.dl = (int32_t)std::nearbyint((1 + 7 * w) * 0.0005 * sr);
+        r.dr = (int32_t)std::nearbyint((1 + 9 * w) * 0.0007 * sr);
+        for (int m = -12; m <= 12; ++m) {
+            const double j = bessel_j(std::abs(m), w * 0.9);
+            r.bess[m + 12] = (float)((m < 0 && (m & 1)) ? -j : j);
+        }
+        r.drive = (float)pr.sat_drive;
+        r.peak = (float)pr.peak;
+        st_begin[p] = stiles;
+        stiles += (int32_t)((inf.out_n + ST_TILE - 1) / ST_TILE);
+        tiles += (int32_t)((inf.out_n + OLA_TILE - 1) / OLA_TILE);
+        pool += inf.pool_len;
+        ysum += inf.out_n;
+        // events
+        for (int k = 0; k < inf.n_events; ++k) {
+            const int ei = slot_base[p] + k;
+            const msg_event& e = ctx->h_events[ei];
+            EventRt& x = ert[ei];
+            memset(&x, 0, sizeof(x));
+            x.n = e.n;
+            x.gen_sr = e.gen_sr;
+            x.ops = spec_ops(pr, e);
+            x.cutoff_gen = e.cutoff_out * e.ufac;
+            x.roll = pr.bandlimit_roll_hz;
+            x.stretch = e.stretch;
+            const double tilt = pr.gen_mode == MSG_GEN_FALLBACK ? -3.0 : pr.noise_tilt;
+            x.tilt_alpha = std::log(std::pow(10.0, tilt / 20.0)) / std::log(2.0);
+            x.env_tau = std::max(1e-6, (pr.micro_ms / 1000.0) * (pr.gen_mode == MSG_GEN_SKEWED ? 0.2 : 0.25));
+            x.warp_power = pr.nl_warp_power;
+            gen_list.push_back(ei);
+            if (x.ops) {
+                std::string why;
+                const int pi = real_plan(ctx->grain_plans, e.n, why);
+                if (pi < 0) return fail(ctx, MSG_E_DEVICE, "grain plan: " + why);
+                x.plan = pi;
+                const int lc = ctx->grain_plans.host[pi].lds_c;
+                if (lc <= SPEC_C_SMALL) spec_small.push_back(ei);
+                else if (lc <= SPEC_C_BIG) spec_big.push_back(ei);
+                else return fail(ctx, MSG_E_UNSUPPORTED, "grain of " + std::to_string(e.n) +
+                                 " samples exceeds the LDS-resident FFT (max ~40958 even / 20479 odd)");
+            } else {
+                spec_small.push_back(ei);
+            }
+        }
+    }
+    HIPCHK(ctx, sync_plans(ctx->grain_plans, s));
+    HIPCHK(ctx, sync_plans(ctx->fir_plans, s));
+    HIPCHK(ctx, ctx->ert.ensure(nslots));
+    HIPCHK(ctx, ctx->prt.ensure(P));
+    HIPCHK(ctx, ctx->gen_list.ensure(gen_list.size()));
+    HIPCHK(ctx, ctx->spec_small.ensure(spec_small.size()));
+    HIPCHK(ctx, ctx->spec_big.ensure(spec_big.size()));
+    HIPCHK(ctx, ctx->tile_begin.ensure(P));
+    HIPCHK(ctx, ctx->fir_begin.ensure(P));
+    HIPCHK(ctx, ctx->h_begin.ensure(P));
+    HIPCHK(ctx, ctx->st_begin.ensure(P));
+    HIPCHK(ctx, ctx->fir_plan_of.ensure(P));
+    HIPCHK(ctx, ctx->micro.ensure(pool));
+    HIPCHK(ctx, ctx->grain.ensure(pool));
+    HIPCHK(ctx, ctx->mono_a.ensure(ysum));
+    HIPCHK(ctx, ctx->mono_y.ensure(ysum));
+    HIPCHK(ctx, ctx->hspec.ensure(hsum));
+    HIPCHK(ctx, ctx->irbank.ensure(irbank.size()));
+    HIPCHK(ctx, ctx->maxbits.ensure(P));
+    auto h2d = [&](void* dst, const void* src, size_t bytes) -> hipError_t {
+        return bytes ? hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, s) : hipSuccess;
+    };
+    for (int p = 0; p < P; ++p) tile_begin[p] = prt[p].tile_begin;
+    HIPCHK(ctx, h2d(ctx->ert.p, ert.data(), sizeof(EventRt) * nslots));
+    HIPCHK(ctx, h2d(ctx->prt.p, prt.data(), sizeof(PresetRt) * P));
+    HIPCHK(ctx, h2d(ctx->gen_list.p, gen_list.data(), sizeof(int32_t) * gen_list.size()));
+    HIPCHK(ctx, h2d(ctx->spec_small.p, spec_small.data(), sizeof(int32_t) * spec_small.size()));
+    HIPCHK(ctx, h2d(ctx->spec_big.p, spec_big.data(), sizeof(int32_t) * spec_big.size()));
+    HIPCHK(ctx, h2d(ctx->tile_begin.p, tile_begin.data(), sizeof(int32_t) * P));
+    HIPCHK(ctx, h2d(ctx->fir_begin.p, fir_begin.data(), sizeof(int32_t) * P));
+    HIPCHK(ctx, h2d(ctx->h_begin.p, h_begin.data(), sizeof(int32_t) * P));
+    HIPCHK(ctx, h2d(ctx->st_begin.p, st_begin.data(), sizeof(int32_t) * P));
+    HIPCHK(ctx, h2d(ctx->fir_plan_of.p, fir_plan_of.data(), sizeof(int32_t) * P));
+    HIPCHK(ctx, h2d(ctx->irbank.p, irbank.data(), sizeof(double) * irbank.size()));
+    HIPCHK(ctx, hipMemsetAsync(ctx->maxbits.p, 0, sizeof(unsigned) * P, s));
+
+    // ---- generate ----
+    stage_mark(ctx, 2, s);
+    if (!gen_list.empty())
+        hipLaunchKernelGGL(k_gen_normal, dim3((unsigned)gen_list.size()), dim3(GEN_T), 0, s,
+                           ctx->presets.p, ctx->events.p, ctx->prt.p, ctx->gen_list.p, (int)gen_list.size(),
+                           ctx->dzig, ctx->d_jump, ctx->micro.p);
+    HIPCHK(ctx, hipGetLastError());
+    // ---- spectral chain ----
+    stage_mark(ctx, 3, s);
+    if (!spec_small.empty())
+        hipLaunchKernelGGL((k_spectral<SPEC_T_SMALL, SPEC_C_SMALL>), dim3((unsigned)spec_small.size()),
+                           dim3(SPEC_T_SMALL), SPEC_C_SMALL * 8, s, ctx->presets.p, ctx->events.p, ctx->ert.p,
+                           ctx->prt.p, ctx->grain_plans.dev.p, ctx->spec_small.p, (int)spec_small.size(),
+                           ctx->micro.p, ctx->grain.p);
+    HIPCHK(ctx, hipGetLastError());
+    if (!spec_big.empty())
+        hipLaunchKernelGGL((k_spectral<SPEC_T_BIG, SPEC_C_BIG>), dim3((unsigned)spec_big.size()),
+                           dim3(SPEC_T_BIG), SPEC_C_BIG * 8, s, ctx->presets.p, ctx->events.p, ctx->ert.p,
+                           ctx->prt.p, ctx->grain_plans.dev.p, ctx->spec_big.p, (int)spec_big.size(),
+                           ctx->micro.p, ctx->grain.p);
+    HIPCHK(ctx, hipGetLastError());
+    // ---- overlap-add x ADSR ----
+    stage_mark(ctx, 4, s);
+    hipLaunchKernelGGL(k_ola_env, dim3((unsigned)tiles), dim3(OLA_T), 0, s, ctx->events.p, ctx->prt.p,
+                       ctx->tile_begin.p, P, ctx->grain.p, ctx->mono_a.p);
+    HIPCHK(ctx, hipGetLastError());
+    // ---- FIR (presets without ER/IR pass a through) ----
+    stage_mark(ctx, 5, s);
+    float* yb = ctx->mono_a.p;
+    if (hblocks > 0) {
+        hipLaunchKernelGGL((k_fir_h<FIR_T, FIR_C>), dim3((unsigned)hblocks), dim3(FIR_T), FIR_C * 8, s,
+                           ctx->prt.p, ctx->h_begin.p, P, ctx->fir_plans.dev.p, ctx->fir_plan_of.p,
+                           ctx->er_off.p, ctx->er_gain.p, ctx->irbank.p, ctx->hspec.p);
+        HIPCHK(ctx, hipGetLastError());
+        hipLaunchKernelGGL((k_fir<FIR_T, FIR_C>), dim3((unsigned)fblocks), dim3(FIR_T), FIR_C * 8, s,
+                           ctx->prt.p, ctx->fir_begin.p, P, ctx->fir_plans.dev.p, ctx->fir_plan_of.p,
+                           ctx->hspec.p, ctx->mono_a.p, ctx->mono_y.p);
+        HIPCHK(ctx, hipGetLastError());
+        // presets with fir_on == 0 in a mixed batch: copy a -> y
+        for (int p = 0; p < P; ++p)
+            if (!prt[p].fir_on)
+                HIPCHK(ctx, hipMemcpyAsync(ctx->mono_y.p + prt[p].y_off, ctx->mono_a.p + prt[p].y_off,
+                                           sizeof(float) * prt[p].out_n, hipMemcpyDeviceToDevice, s));
+        yb = ctx->mono_y.p;
+    }
+    // ---- stereo, tanh, normalise ----
+    stage_mark(ctx, 6, s);
+    hipLaunchKernelGGL(k_stereo_max, dim3((unsigned)stiles), dim3(ST_T), 0, s, ctx->prt.p, ctx->st_begin.p, P,
+                       yb, ctx->maxbits.p);
+    HIPCHK(ctx, hipGetLastError());
+    hipLaunchKernelGGL(k_stereo_out, dim3((unsigned)stiles), dim3(ST_T), 0, s, ctx->prt.p, ctx->st_begin.p, P,
+                       yb, ctx->maxbits.p, out_dev);
+    HIPCHK(ctx, hipGetLastError());
+    stage_mark(ctx, 7, s);
+    ctx->h_info = info;
+    ctx->h_prt = prt;
+    ctx->h_slot_base = slot_base;
+    ctx->last_n = P;
+    if (ctx->profiling) {
+        HIPCHK(ctx, hipEventSynchronize(ctx->ev[7]));
+        for (int i = 0; i < 7; ++i) hipEventElapsedTime(&ctx->stage_ms[i], ctx->ev[i], ctx->ev[i + 1]);
+        hipEventElapsedTime(&ctx->stage_ms[7], ctx->ev[0], ctx->ev[7]);
+    }
+    return MSG_OK;
+}
+
+}  // extern "C"

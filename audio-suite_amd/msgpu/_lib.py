@@ -1,0 +1,148 @@
+"""ctypes binding of libmsgpu (include/msgpu.h).
+
+The library is built in-tree (``audio-suite_amd/build.py`` -> ``msgpu/libmsgpu.so``)
+and is the only compute path: there is no CPU fallback.  If the shared object is
+missing or cannot be loaded, :func:`lib` raises ``RuntimeError``.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import threading
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("MSGPU_LIB", os.path.join(HERE, "libmsgpu.so"))
+MAX_BP = 32
+ABI_VERSION = 1
+
+# status codes (msg_status)
+MSG_OK, MSG_E_VALUE, MSG_E_UNSUPPORTED, MSG_E_DEVICE, MSG_E_ARG = 0, 1, 2, 3, 4
+
+# enums (msg_gen_mode, msg_process, msg_flag)
+GEN_MODE = {"Gaussian click": 0, "Dust impulses": 1, "Noise burst": 2, "Skewed transient": 3,
+            "Resonant strike": 4, "Crackle / corona": 5, "Stick–slip friction": 6,
+            "Micro-chaos": 7, "Wavelet atoms": 8, "IR fragment": 9, "Image scanline": 10}
+GEN_FALLBACK = 11
+PROCESS = {"Single": 0, "Poisson": 1, "Clustered": 2, "Hawkes": 3}
+PROC_NONE = 4
+F_STEREO, F_BANDLIMIT, F_PARTIAL_LOCK, F_NL_WARP, F_CEP_WARP, F_GRAIN_OFFSET = (1 << i for i in range(6))
+F_RES_BANK, F_WAVEGUIDE, F_EVENT_FEEDBACK, F_IMPRINT, F_ER_CLOUD, F_SPACE_IR, F_MULTIBAND = \
+    (1 << i for i in range(6, 13))
+
+
+class MsgPreset(C.Structure):
+    _fields_ = [
+        ("seed", C.c_int64),
+        ("base_sr", C.c_int32), ("gen_mode", C.c_int32), ("process", C.c_int32), ("max_grains", C.c_int32),
+        ("cluster_size", C.c_int32), ("crackle_kernel", C.c_int32), ("wav_count", C.c_int32),
+        ("pl_top_n", C.c_int32),
+        ("pl_neigh", C.c_int32), ("res_modes", C.c_int32), ("wg_lines", C.c_int32), ("er_taps", C.c_int32),
+        ("flags", C.c_uint32),
+        ("ir_conv", C.c_int32), ("ir_frag", C.c_int32), ("image", C.c_int32),
+        ("n_bp", C.c_int32 * 4),
+        ("out_dur_s", C.c_double), ("time_unfold", C.c_double), ("peak", C.c_double),
+        ("sat_drive", C.c_double), ("stereo_width", C.c_double),
+        ("micro_ms", C.c_double), ("dust_density", C.c_double), ("noise_tilt", C.c_double),
+        ("ring_hz", C.c_double), ("ring_decay_ms", C.c_double),
+        ("crackle_alpha", C.c_double), ("crackle_density", C.c_double),
+        ("ss_threshold", C.c_double), ("ss_build", C.c_double), ("ss_decay", C.c_double),
+        ("ss_noise", C.c_double),
+        ("chaos_r", C.c_double), ("chaos_gate", C.c_double), ("wav_base_hz", C.c_double),
+        ("wav_spread", C.c_double),
+        ("partial_stretch", C.c_double), ("nl_warp_power", C.c_double), ("cep_factor", C.c_double),
+        ("mb_b", C.c_double * 3), ("mb_u", C.c_double * 3), ("mb_roll", C.c_double),
+        ("bandlimit_out_hz", C.c_double), ("bandlimit_roll_hz", C.c_double),
+        ("grains_per_sec", C.c_double), ("grain_amp_rand", C.c_double),
+        ("grain_offset_max_ms", C.c_double),
+        ("cluster_spread_ms", C.c_double), ("hawkes_gain", C.c_double), ("hawkes_decay_s", C.c_double),
+        ("res_fmin", C.c_double), ("res_fmax", C.c_double), ("res_decay_ms", C.c_double),
+        ("wg_max_ms", C.c_double), ("wg_fb", C.c_double),
+        ("event_feedback_amt", C.c_double), ("spectral_imprint_amt", C.c_double),
+        ("spectral_imprint_smooth", C.c_double),
+        ("er_max_ms", C.c_double),
+        ("env_a", C.c_double), ("env_d", C.c_double), ("env_s", C.c_double), ("env_r", C.c_double),
+        ("env_curve", C.c_double),
+        ("bp_t", (C.c_double * MAX_BP) * 4),
+        ("bp_v", (C.c_double * MAX_BP) * 4),
+    ]
+
+
+class MsgEvent(C.Structure):
+    _fields_ = [("t0", C.c_double), ("amp", C.c_double), ("ufac", C.c_double),
+                ("cutoff_out", C.c_double), ("stretch", C.c_double), ("pool_off", C.c_int64),
+                ("index", C.c_int32), ("preset", C.c_int32), ("gen_sr", C.c_int32), ("n", C.c_int32),
+                ("start", C.c_int32), ("offset", C.c_int32), ("len", C.c_int32), ("pad", C.c_int32)]
+
+
+class MsgPlanInfo(C.Structure):
+    _fields_ = [("out_n", C.c_int64), ("design_sr", C.c_int32), ("n_events", C.c_int32),
+                ("n_slots", C.c_int32), ("max_n", C.c_int32), ("pool_len", C.c_int64)]
+
+
+# name -> (restype, argtypes)
+_PROTOS = {
+    "msg_abi_version": (C.c_int, []),
+    "msg_sizeof": (C.c_int64, [C.c_int32]),
+    "msg_create": (C.c_void_p, [C.c_int]),
+    "msg_destroy": (None, [C.c_void_p]),
+    "msg_last_error": (C.c_char_p, [C.c_void_p]),
+    "msg_plan_host": (C.c_int, [C.POINTER(MsgPreset), C.POINTER(C.c_double), C.c_int64,
+                                C.POINTER(MsgPlanInfo), C.POINTER(MsgEvent), C.c_int32,
+                                C.POINTER(C.c_int32), C.POINTER(C.c_double)]),
+    "msg_render_batch": (C.c_int, [C.c_void_p, C.POINTER(MsgPreset), C.c_int32,
+                                   C.POINTER(C.POINTER(C.c_double)), C.POINTER(C.c_int64), C.c_int32,
+                                   C.POINTER(C.POINTER(C.c_uint8)), C.POINTER(C.c_int32),
+                                   C.POINTER(C.c_int32), C.c_int32,
+                                   C.c_void_p, C.POINTER(C.c_int64), C.c_void_p]),
+    "msg_last_plan": (C.c_int, [C.c_void_p, C.POINTER(MsgPlanInfo), C.c_int32]),
+    "msg_last_events": (C.c_int, [C.c_void_p, C.c_int32, C.POINTER(MsgEvent), C.c_int32,
+                                  C.POINTER(C.c_int32)]),
+    "msg_last_meta": (C.c_int, [C.c_void_p, C.c_int32, C.POINTER(C.c_double), C.POINTER(C.c_double),
+                                C.c_int64, C.POINTER(C.c_int64)]),
+    "msg_set_profiling": (C.c_int, [C.c_void_p, C.c_int32]),
+    "msg_stage_times": (C.c_int, [C.c_void_p, C.POINTER(C.c_float), C.c_int32]),
+    "msg_rng_raw": (C.c_int, [C.c_uint64, C.POINTER(C.c_uint64), C.c_int64]),
+    "msg_rng_normal": (C.c_int, [C.c_uint64, C.POINTER(C.c_double), C.c_int64]),
+    "msg_rng_exponential": (C.c_int, [C.c_uint64, C.POINTER(C.c_double), C.c_int64]),
+    "msg_rng_integers": (C.c_int, [C.c_uint64, C.c_int64, C.c_int64, C.POINTER(C.c_int64), C.c_int64]),
+    "msg_rng_normal_chunked": (C.c_int, [C.c_uint64, C.POINTER(C.c_double), C.c_int64]),
+}
+EXPORTS = tuple(_PROTOS)
+
+_lib = None
+_lock = threading.Lock()
+
+
+def lib() -> C.CDLL:
+    """Load libmsgpu once; raise RuntimeError (no fallback) if it is missing."""
+    global _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(LIB_PATH):
+                raise RuntimeError(f"libmsgpu not built: {LIB_PATH} is missing "
+                                   "(run `python -c 'import __graft_entry__ as g; g.build()'`)")
+            L = C.CDLL(LIB_PATH)
+            for name, (res, args) in _PROTOS.items():
+                f = getattr(L, name)
+                f.restype = res
+                f.argtypes = args
+            if L.msg_abi_version() != ABI_VERSION:
+                raise RuntimeError("libmsgpu ABI version mismatch")
+            for which, st in enumerate((MsgPreset, MsgEvent, MsgPlanInfo)):
+                if L.msg_sizeof(which) != C.sizeof(st):
+                    raise RuntimeError(f"libmsgpu struct {st.__name__} size mismatch: "
+                                       f"{L.msg_sizeof(which)} != {C.sizeof(st)}")
+            _lib = L
+    return _lib
+
+
+def check(status: int, ctx=None) -> None:
+    """Map a msg_status to the exception type the reference would raise."""
+    if status == MSG_OK:
+        return
+    msg = lib().msg_last_error(ctx).decode("utf-8", "replace")
+    if status == MSG_E_VALUE:
+        raise ValueError(msg)
+    if status == MSG_E_UNSUPPORTED:
+        raise NotImplementedError(msg)
+    raise RuntimeError(f"libmsgpu: {msg}")

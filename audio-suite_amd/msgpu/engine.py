@@ -1,0 +1,118 @@
+"""Device engine: one libmsgpu context per (process, device).
+
+``Engine.render_packed`` enqueues one batched render on the current torch
+stream and returns the device output tensor (frames x 2, float32,
+interleaved L/R).  PyTorch-ROCm is used only as the device-buffer container
+and for its stream handle.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import threading
+
+import numpy as np
+
+from . import _lib as L
+from .pack import PackedBatch
+
+
+class Engine:
+    def __init__(self, device: int = 0):
+        import torch  # device buffers only
+
+        if not torch.cuda.is_available():
+            raise RuntimeError("msgpu needs a HIP device (torch.cuda.is_available() is False)")
+        self.torch = torch
+        self.device = int(device)
+        lib = L.lib()
+        with torch.cuda.device(self.device):
+            torch.cuda.current_stream()  # initialise the runtime on this device first
+            ctx = lib.msg_create(self.device)
+        if not ctx:
+            raise RuntimeError("msg_create failed: " + lib.msg_last_error(None).decode())
+        self._ctx = C.c_void_p(ctx)
+        self._lock = threading.Lock()
+        self._last_n = 0
+
+    def close(self):
+        if getattr(self, "_ctx", None):
+            L.lib().msg_destroy(self._ctx)
+            self._ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ------------------------------------------------------------------
+    def set_profiling(self, on: bool):
+        L.check(L.lib().msg_set_profiling(self._ctx, 1 if on else 0), self._ctx)
+
+    def stage_times(self):
+        arr = (C.c_float * 8)()
+        L.check(L.lib().msg_stage_times(self._ctx, arr, 8), self._ctx)
+        return list(arr)
+
+    def alloc_output(self, packed: PackedBatch):
+        return self.torch.empty((packed.total_frames, 2), dtype=self.torch.float32,
+                                device=f"cuda:{self.device}")
+
+    def render_packed(self, packed: PackedBatch, out=None, stream=None):
+        """Enqueue the batch; returns the output tensor (not yet synchronised)."""
+        torch = self.torch
+        if out is None:
+            out = self.alloc_output(packed)
+        if out.dtype != torch.float32 or not out.is_contiguous() or out.numel() < 2 * packed.total_frames:
+            raise ValueError("output tensor must be contiguous float32 with 2*frames elements")
+        if stream is None:
+            stream = torch.cuda.current_stream(self.device)
+        with self._lock:
+            st = L.lib().msg_render_batch(
+                self._ctx, packed.presets, packed.n, packed.ir_ptrs, packed.ir_lens, packed.n_irs,
+                packed.img_ptrs, packed.img_h, packed.img_w, packed.n_images,
+                C.c_void_p(out.data_ptr()), packed._offsets_c, C.c_void_p(stream.cuda_stream))
+            L.check(st, self._ctx)
+            self._last_n = packed.n
+        return out
+
+    def render_batch(self, params_list, out=None):
+        packed = PackedBatch(params_list)
+        return self.render_packed(packed, out), packed
+
+    # ---- last-batch inspection -----------------------------------------
+    def last_plan(self):
+        arr = (L.MsgPlanInfo * self._last_n)()
+        L.check(L.lib().msg_last_plan(self._ctx, arr, self._last_n), self._ctx)
+        return list(arr)
+
+    def last_events(self, preset: int):
+        n = C.c_int32(0)
+        L.check(L.lib().msg_last_events(self._ctx, preset, None, 0, C.byref(n)), self._ctx)
+        arr = (L.MsgEvent * max(n.value, 1))()
+        L.check(L.lib().msg_last_events(self._ctx, preset, arr, n.value, C.byref(n)), self._ctx)
+        return list(arr)[:n.value]
+
+    def last_meta(self, preset: int, cap: int):
+        micro = np.zeros(max(cap, 1), dtype=np.float64)
+        grain = np.zeros(max(cap, 1), dtype=np.float64)
+        n = C.c_int64(0)
+        L.check(L.lib().msg_last_meta(self._ctx, preset, micro.ctypes.data_as(C.POINTER(C.c_double)),
+                                      grain.ctypes.data_as(C.POINTER(C.c_double)), cap, C.byref(n)),
+                self._ctx)
+        if n.value == 0:
+            return None, None
+        return micro[:n.value].copy(), grain[:n.value].copy()
+
+
+_engines: dict = {}
+_engines_lock = threading.Lock()
+
+
+def default_engine(device: int = 0) -> Engine:
+    with _engines_lock:
+        eng = _engines.get(device)
+        if eng is None:
+            eng = Engine(device)
+            _engines[device] = eng
+        return eng

@@ -1,0 +1,70 @@
+"""Drop-in ``render(params, progress=None)`` for microsound_0.2.1/main_v2.py:588.
+
+Usage from the unchanged PyQt6 front-end::
+
+    import main_v2, msgpu
+    main_v2.render = msgpu.render      # RenderWorker.run (MS:811) and on_batch (MS:1585)
+
+Returns ``(audio, meta)`` like the reference: ``audio`` is a C-contiguous
+(out_n, 2) float32 array (the consumers only read its shape/columns and cast
+with ``astype(np.float32)`` before ``sf.write``, MS:1473-1519, 1589), ``meta``
+has ``out_sr``, ``design_sr_base``, ``micro_last``, ``grain_last`` (MS:786-791).
+The ``progress`` callback gets the reference's messages: 0 with the SR line,
+every 50th placed event, and 100 "Done." (MS:599-600, 757-758, 783-784).
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from .engine import default_engine
+from .pack import PackedBatch, design_sr
+from .params import merged
+
+_NOTE = {"IR fragment": "IR fragment", "Image scanline": ""}
+
+
+def render(params, progress=None, device: int = 0):
+    p = merged(params)
+    base_sr = int(p["base_sr"])
+    if progress:
+        progress(0, f"Output SR {base_sr} Hz | Design SR {design_sr(p)} Hz")
+    eng = default_engine(device)
+    packed = PackedBatch([p])
+    out = eng.render_packed(packed)
+    eng.torch.cuda.synchronize(eng.device)
+    audio = out.cpu().numpy().reshape(packed.total_frames, 2)
+    info = eng.last_plan()[0]
+    if progress:
+        events = eng.last_events(0)
+        n = len(events)
+        note = _fragment_note(p)
+        for e in events:
+            if e.len > 0 and e.index % 50 == 0:
+                progress(int(5 + 70 * (e.index / max(1, n))), f"Events {e.index}/{n}  {note}".strip())
+        progress(100, "Done.")
+    micro = grain = None
+    if info.n_events > 0:
+        micro, grain = eng.last_meta(0, int(info.max_n))
+    meta = {"out_sr": base_sr, "design_sr_base": int(info.design_sr),
+            "micro_last": micro, "grain_last": grain}
+    return np.ascontiguousarray(audio), meta
+
+
+def _fragment_note(p):
+    mode = p["gen_mode"]
+    if mode == "IR fragment":
+        ir = p.get("_ir_audio")
+        return "No IR loaded" if (ir is None or ir.size < 32) else "IR fragment"
+    if mode == "Image scanline" and p.get("_img_gray") is None:
+        return "No image loaded"
+    return ""
+
+
+def render_batch(params_list, device: int = 0):
+    """Render many presets in one device batch; returns a list of (out_n, 2) float32 arrays."""
+    eng = default_engine(device)
+    packed = PackedBatch(list(params_list))
+    out = eng.render_packed(packed)
+    eng.torch.cuda.synchronize(eng.device)
+    host = out.cpu().numpy()
+    return [host[o:o + n].copy() for o, n in zip(packed.offsets, packed.out_n)]

@@ -1,0 +1,175 @@
+#!/usr/bin/env python3
+"""Benchmark: Msamples/s rendered by the MI355X Microsound render path.
+
+Workload (BASELINE.json configs[2], SURVEY.md section 8 "C3"): 384 kHz output,
+unfold x100 (design SR clamps to 30 MHz), spectral stretch x2, resonant
+transient, Poisson events, 16 k-tap IR request (8192-tap cap, MS:443),
+early reflections, stereo diffusion — a batch of 1024 presets per GPU, seeds
+1000 + rank*batch + b.  One step = one full render of the batch (device plan ->
+generate -> spectral -> overlap-add -> FIR -> stereo/normalise) with inputs
+(packed presets + IR) resident.  Weak scaling: every rank renders its own batch.
+
+    python bench.py [--gpus N --steps K --warmup W --config C3 --batch 1024]
+
+Multi-GPU: launched by torch.distributed.run, one process per GPU, no
+data-path collective (presets are independent); barrier + max-over-ranks timing.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "audio-suite_amd"))
+sys.path.insert(0, REPO)
+
+import numpy as np  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: 8.0 TB/s spec
+
+
+def load_irs():
+    z = np.load(os.path.join(REPO, "tests", "golden", "irs.npz"))
+    return {k: z[k] for k in z.files}
+
+
+def stage_bytes(infos, packed, params):
+    """Algorithmic (compulsory) HBM bytes per stage for one step."""
+    sum_n = sum(int(i.pool_len) for i in infos)
+    out_n = sum(int(i.out_n) for i in infos)
+    return {
+        "generate": 4 * sum_n,                 # grain samples written once
+        "spectral": 8 * sum_n,                 # grain read + grain written (one LDS round trip)
+        "overlap_add": 4 * sum_n + 4 * out_n,  # placed grains read + mono written (upper bound)
+        "fir": 8 * out_n,                      # mono read + mono written
+        "stereo": 16 * out_n,                  # max pass reads y; output pass reads y, writes L/R
+    }
+
+
+def cpu_baseline(cfg, irs, budget_s):
+    from oracle import msound_oracle as O   # CPU baseline only
+    import msgpu
+    done = 0
+    frames = 0
+    t0 = time.perf_counter()
+    while True:
+        p = msgpu.config_params(cfg, seed=1000 + done, irs=irs)
+        a, _ = O.render(p)
+        frames += a.shape[0]
+        done += 1
+        if time.perf_counter() - t0 >= budget_s or done >= 256:
+            break
+    dt = time.perf_counter() - t0
+    return {"value": frames / dt / 1e6, "unit": "Msamples/s", "cores": 1, "kind": "port",
+            "sample": f"{done} {cfg} presets (seeds 1000..{999 + done}) rendered sequentially by "
+                      f"oracle/msound_oracle.py (NumPy restatement of main_v2.render) on 1 host core "
+                      f"in {dt:.1f} s"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="C3")
+    ap.add_argument("--batch", type=int, default=1024)
+    ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of CPU-baseline work")
+    ap.add_argument("--no-cpu", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+    dev = local if world > 1 else 0
+
+    import msgpu
+    from msgpu.engine import Engine
+    from msgpu.pack import PackedBatch
+
+    irs = load_irs()
+    seeds = [1000 + rank * args.batch + b for b in range(args.batch)]
+    params = [msgpu.config_params(args.config, seed=s, irs=irs) for s in seeds]
+    packed = PackedBatch(params)
+    eng = Engine(dev)
+    out = eng.alloc_output(packed)
+    stream = torch.cuda.current_stream(dev)
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    for _ in range(args.warmup):
+        eng.render_packed(packed, out, stream)
+    torch.cuda.synchronize(dev)
+    infos = eng.last_plan()
+
+    eng.set_profiling(True)
+    stage_sum = np.zeros(8)
+    barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        eng.render_packed(packed, out, stream)
+        stage_sum += np.array(eng.stage_times())
+    torch.cuda.synchronize(dev)
+    barrier()
+    elapsed = time.perf_counter() - t0
+    eng.set_profiling(False)
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{dev}")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    frames_rank = packed.total_frames
+    total_frames = frames_rank * world * args.steps
+    value = total_frames / elapsed / 1e6
+    ms_step = elapsed / args.steps * 1e3
+    stage_ms = stage_sum / args.steps
+    names = ["plan", "host_prep", "generate", "spectral", "overlap_add", "fir", "stereo", "total"]
+    stages = {n: round(float(v), 4) for n, v in zip(names, stage_ms)}
+    sb = stage_bytes(infos, packed, params)
+    stage_gbs = {k: round(sb[k] / (stages[k] * 1e-3) / 1e9, 1) for k in sb if stages.get(k, 0) > 0}
+    kernel_stages = ["generate", "spectral", "overlap_add", "fir", "stereo"]
+    dom = max(kernel_stages, key=lambda k: stages[k])
+    achieved = sb[dom] / (stages[dom] * 1e-3) / 1e9
+    sum_n = sum(int(i.pool_len) for i in infos)
+    n_ev = sum(int(i.n_events) for i in infos)
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        cpu = cpu_baseline(args.config, irs, args.cpu_budget)
+
+    if rank == 0:
+        line = {
+            "metric": "Msamples/sec rendered (microsound full pipe, 384 kHz->48 kHz) at 1/2/4/8 GPUs",
+            "value": round(value, 3), "unit": "Msamples/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(ms_step, 3), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
+            "data": "synthetic presets (reference param dicts, seeds per rank), IR ir_tiny_room_250ms",
+            "config": {"workload": f"{args.config}: 384 kHz out, unfold x100 (30 MHz design SR), stretch x2, "
+                                   f"Poisson 18/s, 1 s, 16k-tap IR request (8192 cap), ER 320 taps, stereo",
+                       "presets_per_gpu": args.batch, "frames_per_gpu_step": frames_rank,
+                       "events_per_gpu_step": n_ev, "design_samples_per_gpu_step": sum_n,
+                       "parallelism": f"preset-sharded x{world}"},
+            "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1),
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                         "traffic": None, "algorithmic_bytes": sb[dom]},
+            "stage_ms": stages, "stage_algorithmic_GBs": stage_gbs,
+            "design_msamples_per_s": round(sum_n * world * args.steps / elapsed / 1e6, 1),
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

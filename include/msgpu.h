@@ -1,0 +1,170 @@
+/*
+ * msgpu.h — C ABI of libmsgpu, the MI355X (gfx950) Microsound render engine.
+ *
+ * Drop-in boundary: the reference's only interface on this path is the Python
+ * function  render(params: dict, progress=None) -> (audio[out_n, 2], meta)
+ * (microsound_0.2.1/main_v2.py:588-792, "MS").  The Python shim
+ * audio-suite_amd/msgpu/render.py keeps that signature and binds this library
+ * with ctypes (INTEGRATION.md shows the binding).  Every entry point takes plain
+ * pointers and sizes, never throws, and reports failure as a non-zero status
+ * with the text in msg_last_error().
+ *
+ *   msg_preset       one params dict (MS:1166-1266) flattened to POD
+ *   msg_render_batch render(params) for N presets at once      (replaces MS:588)
+ *   msg_plan_host    the render's scalar/RNG plan, host-side    (MS:589-646, 742-751)
+ *   msg_rng_*        NumPy PCG64 stream primitives, host-side   (np.random.default_rng)
+ */
+#ifndef MSGPU_H
+#define MSGPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MSG_ABI_VERSION 1
+#define MSG_MAX_BP 32          /* breakpoints per lane (MS:452-467) */
+
+/* gen_mode (MS:919-923) */
+enum msg_gen_mode {
+    MSG_GEN_GAUSSIAN_CLICK = 0, MSG_GEN_DUST = 1, MSG_GEN_NOISE_BURST = 2,
+    MSG_GEN_SKEWED = 3, MSG_GEN_RESONANT = 4, MSG_GEN_CRACKLE = 5,
+    MSG_GEN_STICK_SLIP = 6, MSG_GEN_MICRO_CHAOS = 7, MSG_GEN_WAVELET = 8,
+    MSG_GEN_IR_FRAGMENT = 9, MSG_GEN_IMAGE = 10,
+    MSG_GEN_FALLBACK = 11      /* unknown name -> "Noise burst" fallback, MS:686 */
+};
+/* event_process (MS:1039); unknown names give no events (MS:558) */
+enum msg_process { MSG_PROC_SINGLE = 0, MSG_PROC_POISSON = 1, MSG_PROC_CLUSTERED = 2,
+                   MSG_PROC_HAWKES = 3, MSG_PROC_NONE = 4 };
+/* boolean switches, msg_preset.flags */
+enum msg_flag {
+    MSG_F_STEREO = 1u << 0, MSG_F_BANDLIMIT = 1u << 1, MSG_F_PARTIAL_LOCK = 1u << 2,
+    MSG_F_NL_WARP = 1u << 3, MSG_F_CEP_WARP = 1u << 4, MSG_F_GRAIN_OFFSET = 1u << 5,
+    MSG_F_RES_BANK = 1u << 6, MSG_F_WAVEGUIDE = 1u << 7, MSG_F_EVENT_FEEDBACK = 1u << 8,
+    MSG_F_IMPRINT = 1u << 9, MSG_F_ER_CLOUD = 1u << 10, MSG_F_SPACE_IR = 1u << 11,
+    MSG_F_MULTIBAND = 1u << 12
+};
+
+/* One render's parameters: the params dict of MS:1166-1266, flattened. */
+typedef struct msg_preset {
+    int64_t seed;
+    int32_t base_sr, gen_mode, process, max_grains;
+    int32_t cluster_size, crackle_kernel, wav_count, pl_top_n;
+    int32_t pl_neigh, res_modes, wg_lines, er_taps;
+    uint32_t flags;
+    int32_t ir_conv;           /* index into the IR bank for the space FIR, -1 = none   */
+    int32_t ir_frag;           /* index into the IR bank for the "IR fragment" source   */
+    int32_t image;             /* index into the image bank, -1 = none                  */
+    int32_t n_bp[4];           /* points in lanes density, unfold, cutoff, stretch      */
+    double out_dur_s, time_unfold, peak, sat_drive, stereo_width;
+    double micro_ms, dust_density, noise_tilt, ring_hz, ring_decay_ms;
+    double crackle_alpha, crackle_density;
+    double ss_threshold, ss_build, ss_decay, ss_noise;
+    double chaos_r, chaos_gate, wav_base_hz, wav_spread;
+    double partial_stretch, nl_warp_power, cep_factor;
+    double mb_b[3], mb_u[3], mb_roll;
+    double bandlimit_out_hz, bandlimit_roll_hz;
+    double grains_per_sec, grain_amp_rand, grain_offset_max_ms;
+    double cluster_spread_ms, hawkes_gain, hawkes_decay_s;
+    double res_fmin, res_fmax, res_decay_ms, wg_max_ms, wg_fb;
+    double event_feedback_amt, spectral_imprint_amt, spectral_imprint_smooth;
+    double er_max_ms;
+    double env_a, env_d, env_s, env_r, env_curve;
+    double bp_t[4][MSG_MAX_BP];
+    double bp_v[4][MSG_MAX_BP];
+} msg_preset;
+
+/* One micro event after planning (MS:633-755). */
+typedef struct msg_event {
+    double t0, amp, ufac, cutoff_out, stretch;
+    int64_t pool_off;          /* grain offset inside the preset's grain pool           */
+    int32_t index;             /* i of the reference loop (generator seed = seed + i)   */
+    int32_t preset;            /* preset index in the batch                             */
+    int32_t gen_sr, n;         /* design SR of the event, grain length                  */
+    int32_t start, offset;     /* output sample, read offset into the grain             */
+    int32_t len;               /* samples overlap-added (0 = not placed)                */
+    int32_t pad;
+} msg_event;
+
+/* Per-preset plan summary. */
+typedef struct msg_plan_info {
+    int64_t out_n;             /* output frames (MS:591)                                */
+    int32_t design_sr;         /* meta["design_sr_base"] (MS:596-597)                   */
+    int32_t n_events;          /* events after max_grains truncation (MS:617-618)       */
+    int32_t n_slots;           /* event slots needed before truncation                  */
+    int32_t max_n;             /* longest grain                                         */
+    int64_t pool_len;          /* sum of grain lengths                                  */
+} msg_plan_info;
+
+/* status codes; the Python shim maps them to the reference's exception types */
+enum msg_status { MSG_OK = 0, MSG_E_VALUE = 1 /* ValueError */, MSG_E_UNSUPPORTED = 2 /* NotImplementedError */,
+                  MSG_E_DEVICE = 3 /* RuntimeError: HIP failure */, MSG_E_ARG = 4 /* RuntimeError: bad call */ };
+
+typedef struct msg_ctx msg_ctx;
+
+int         msg_abi_version(void);
+/* sizeof of the ABI structs (0 msg_preset, 1 msg_event, 2 msg_plan_info) for binding checks */
+int64_t     msg_sizeof(int32_t which);
+msg_ctx*    msg_create(int device_ordinal);
+void        msg_destroy(msg_ctx* ctx);
+const char* msg_last_error(msg_ctx* ctx);   /* ctx may be NULL (creation errors) */
+
+/* Host-side plan of one preset (the same code the device planner runs).
+ * events: capacity max_events; *n_events receives the event count.
+ * er_off / er_gain: capacity preset->er_taps (MS:410-417).               */
+int msg_plan_host(const msg_preset* preset, const double* ir_frag, int64_t ir_frag_len,
+                  msg_plan_info* info, msg_event* events, int32_t max_events,
+                  int32_t* er_off, double* er_gain);
+
+/* Render a batch of presets on the context's device.
+ * irs: host pointers to IR bank entries (float64 mono), ir_lens their lengths.
+ *      The conv kernel of a preset uses irs[ir_conv] (already cut to
+ *      space_ir_max_samps and <= 8192 taps by the caller, MS:443, 773).
+ * images: host uint8 grey images (h*w each), img_h/img_w dims.
+ * out_dev: device buffer of sum(out_n)*2 floats, interleaved L/R per frame;
+ *      out_offsets[i] = first frame of preset i (host array, n_presets entries).
+ * stream: hipStream_t (NULL = default stream).  The call returns after the
+ *      work is enqueued; synchronise the stream before reading out_dev.      */
+int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t n_presets,
+                     const double* const* irs, const int64_t* ir_lens, int32_t n_irs,
+                     const uint8_t* const* images, const int32_t* img_h, const int32_t* img_w,
+                     int32_t n_images,
+                     float* out_dev, const int64_t* out_offsets, void* stream);
+
+/* Plan summaries of the last msg_render_batch (host copy, n_presets entries). */
+int msg_last_plan(msg_ctx* ctx, msg_plan_info* info, int32_t n_presets);
+
+/* Planned events of preset i of the last batch (host copy); *n receives the count. */
+int msg_last_events(msg_ctx* ctx, int32_t preset, msg_event* events, int32_t cap, int32_t* n);
+
+/* Copy the last event's generator output (micro_last) and final grain
+ * (grain_last, before feedback/imprint) of preset i of the last batch to host
+ * float64 buffers of capacity cap; *n receives the length (0 if no events). */
+int msg_last_meta(msg_ctx* ctx, int32_t preset, double* micro, double* grain,
+                  int64_t cap, int64_t* n);
+
+/* Device time of each stage of the last batch in ms (HIP events):
+ * [0] device plan + read-back, [1] host prep + uploads, [2] generate,
+ * [3] spectral, [4] overlap-add x ADSR, [5] FIR (h build + FIR),
+ * [6] stereo+clip+normalise, [7] total.  Needs msg_set_profiling(ctx, 1).  */
+int msg_set_profiling(msg_ctx* ctx, int32_t on);
+int msg_stage_times(msg_ctx* ctx, float* ms, int32_t n);
+
+/* ---- NumPy stream primitives on the host (tests pin them against NumPy) ---- */
+/* Raw PCG64 outputs of np.random.default_rng(seed).bit_generator.random_raw(n). */
+int msg_rng_raw(uint64_t seed, uint64_t* out, int64_t n);
+/* standard_normal(n) / standard_exponential(n) / random(n) of default_rng(seed). */
+int msg_rng_normal(uint64_t seed, double* out, int64_t n);
+int msg_rng_exponential(uint64_t seed, double* out, int64_t n);
+/* integers(low, high, size=n) of default_rng(seed). */
+int msg_rng_integers(uint64_t seed, int64_t low, int64_t high, int64_t* out, int64_t n);
+/* The same walk the device uses to generate normals in parallel chunks of 64
+ * (host emulation of the wave algorithm, for testing). */
+int msg_rng_normal_chunked(uint64_t seed, double* out, int64_t n);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MSGPU_H */
