@@ -1,29 +1,52 @@
 #!/usr/bin/env python3
-"""Build libmsgpu.so in-tree for gfx950 (hipcc).  Usage: python audio-suite_amd/build.py [--force]"""
+"""Build libmsgpu.so in-tree for gfx950 with hipcc (translation units in parallel).
+
+    python audio-suite_amd/build.py [--force]
+"""
+import concurrent.futures as cf
 import os
 import subprocess
 import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-SRC = os.path.join(HERE, "csrc", "msgpu.hip")
+CSRC = os.path.join(HERE, "csrc")
+OBJ = os.path.join(HERE, "build")
 OUT = os.path.join(HERE, "msgpu", "libmsgpu.so")
-DEPS = [os.path.join(HERE, "csrc", f) for f in os.listdir(os.path.join(HERE, "csrc"))] + \
-       [os.path.join(os.path.dirname(HERE), "include", "msgpu.h")]
+TUS = ["msgpu.hip", "k_spectral.hip", "k_fir.hip"]
+HEADERS = [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".h")] + \
+          [os.path.join(os.path.dirname(HERE), "include", "msgpu.h")]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
+FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC",
          "-Wall", "-Wno-unused-function", "-Wno-unused-value", "-Wno-unused-result"]
 
 
-def stale() -> bool:
-    if not os.path.exists(OUT):
-        return True
-    t = os.path.getmtime(OUT)
-    return any(os.path.getmtime(d) > t for d in DEPS)
+def _newest_header():
+    return max(os.path.getmtime(h) for h in HEADERS)
+
+
+def _compile(tu):
+    src = os.path.join(CSRC, tu)
+    obj = os.path.join(OBJ, tu.replace(".hip", ".o"))
+    if os.path.exists(obj) and os.path.getmtime(obj) >= max(os.path.getmtime(src), _newest_header()):
+        return obj
+    cmd = [HIPCC, *FLAGS, "-c", "-o", obj + ".tmp", src]
+    print("[msgpu build]", " ".join(cmd), flush=True)
+    subprocess.check_call(cmd)
+    os.replace(obj + ".tmp", obj)
+    return obj
 
 
 def build(force: bool = False) -> str:
-    if force or stale():
-        cmd = [HIPCC, *FLAGS, "-o", OUT + ".tmp", SRC]
+    os.makedirs(OBJ, exist_ok=True)
+    if force:
+        for tu in TUS:
+            o = os.path.join(OBJ, tu.replace(".hip", ".o"))
+            if os.path.exists(o):
+                os.remove(o)
+    with cf.ThreadPoolExecutor(max_workers=len(TUS)) as ex:
+        objs = list(ex.map(_compile, TUS))
+    if not os.path.exists(OUT) or any(os.path.getmtime(o) > os.path.getmtime(OUT) for o in objs):
+        cmd = [HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", OUT + ".tmp", *objs]
         print("[msgpu build]", " ".join(cmd), flush=True)
         subprocess.check_call(cmd)
         os.replace(OUT + ".tmp", OUT)

@@ -4,31 +4,57 @@
 #include <cmath>
 #include <complex>
 #include <vector>
+#include <algorithm>
 #include <stdint.h>
 
 namespace fftplan {
 
-// Radix sequence for a Stockham FFT of length m using {8,4,2,5,3,7}; returns
-// false when m has another prime factor (-> Bluestein).
+// Radix sequence for a Stockham FFT of length m over the register DFTs of
+// fft_lds.h {2,3,4,5,6,7,8,9,10,12,15,16,20,25}; false when m has a prime
+// factor > 7 (-> Bluestein).  Few passes = few LDS round trips.
 inline bool factor(int m, std::vector<int>& rad) {
     rad.clear();
-    int r = m;
-    while (r % 8 == 0 && r >= 8) { rad.push_back(8); r /= 8; }
-    if (r % 4 == 0) { rad.push_back(4); r /= 4; }
-    if (r % 2 == 0) { rad.push_back(2); r /= 2; }
-    for (int p : {5, 3, 7}) {
-        while (r % p == 0) { rad.push_back(p); r /= p; }
+    int r = m, a2 = 0, a3 = 0, a5 = 0, a7 = 0;
+    while (r % 2 == 0) { r /= 2; ++a2; }
+    while (r % 3 == 0) { r /= 3; ++a3; }
+    while (r % 5 == 0) { r /= 5; ++a5; }
+    while (r % 7 == 0) { r /= 7; ++a7; }
+    if (r != 1) return false;
+    for (; a5 >= 2; a5 -= 2) rad.push_back(25);
+    if (a5) rad.push_back(5);
+    for (; a3 >= 2; a3 -= 2) rad.push_back(9);
+    if (a3) rad.push_back(3);
+    for (; a7; --a7) rad.push_back(7);
+    for (; a2 >= 4; a2 -= 4) rad.push_back(16);
+    if (a2 == 3) rad.push_back(8);
+    else if (a2 == 2) rad.push_back(4);
+    else if (a2 == 1) rad.push_back(2);
+    auto ok = [](int x) {
+        for (int v : {2, 3, 4, 5, 6, 7, 8, 9, 10, 12, 15, 16, 20, 25}) if (v == x) return true;
+        return false;
+    };
+    for (bool merged = true; merged;) {   // merge the smallest mergeable pair
+        merged = false;
+        std::sort(rad.begin(), rad.end());
+        for (size_t i = 0; i < rad.size() && !merged; ++i)
+            for (size_t j = i + 1; j < rad.size() && !merged; ++j)
+                if (ok(rad[i] * rad[j])) {
+                    rad[i] *= rad[j];
+                    rad.erase(rad.begin() + j);
+                    merged = true;
+                }
     }
-    return r == 1;
+    return true;
 }
 
 inline int next_pow2(int x) { int p = 1; while (p < x) p <<= 1; return p; }
 
-inline std::vector<float> twiddles(int size) {   // interleaved re,im of exp(-2 pi i j / size)
-    std::vector<float> t(2 * (size_t)size);
-    for (int j = 0; j < size; ++j) {
-        // exact octant symmetry keeps the float64 values symmetric
-        const long double a = -2.0L * 3.14159265358979323846264338327950288L * (long double)j / (long double)size;
+// interleaved re,im of exp(-2 pi i j * step / size), j < count
+inline std::vector<float> twiddles(int size, int count, int step) {
+    std::vector<float> t(2 * (size_t)count);
+    for (int j = 0; j < count; ++j) {
+        const long long e = ((long long)j * step) % size;
+        const long double a = -2.0L * 3.14159265358979323846264338327950288L * (long double)e / (long double)size;
         t[2 * j] = (float)std::cos(a);
         t[2 * j + 1] = (float)std::sin(a);
     }

@@ -1,0 +1,23 @@
+// k_spectral.hip — translation unit of the per-event spectral chain kernels.
+#include "kernels_spectral.h"
+#include "launch.h"
+
+void spectral_init_attrs() {
+    (void)hipFuncSetAttribute((const void*)k_spectral<SPEC_T_BIG, SPEC_M_BIG>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
+    (void)hipFuncSetAttribute((const void*)k_spectral<SPEC_T_SMALL, SPEC_M_SMALL>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, SPEC_SMALL_BYTES);
+}
+
+hipError_t launch_spectral(bool big, unsigned grid, int lds_bytes, hipStream_t s,
+                           const msg_preset* presets, const msg_event* events, const EventRt* ert,
+                           const PresetRt* rt, const RealPlan* plans, const int32_t* ev_list, int n_list,
+                           float* micro_pool, float* grain_pool) {
+    if (big)
+        hipLaunchKernelGGL((k_spectral<SPEC_T_BIG, SPEC_M_BIG>), dim3(grid), dim3(SPEC_T_BIG), lds_bytes, s,
+                           presets, events, ert, rt, plans, ev_list, n_list, micro_pool, grain_pool);
+    else
+        hipLaunchKernelGGL((k_spectral<SPEC_T_SMALL, SPEC_M_SMALL>), dim3(grid), dim3(SPEC_T_SMALL), lds_bytes, s,
+                           presets, events, ert, rt, plans, ev_list, n_list, micro_pool, grain_pool);
+    return hipGetLastError();
+}

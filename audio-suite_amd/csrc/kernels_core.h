@@ -1,0 +1,314 @@
+// kernels_core.h — planner, generator, overlap-add and stereo kernels (TU: msgpu.hip).
+#pragma once
+#include "rt.h"
+
+// ---------------------------------------------------------------------------
+// Planner (one thread per preset).
+// ---------------------------------------------------------------------------
+__global__ void k_plan_sizes(const msg_preset* __restrict__ presets, int n_presets,
+                             const int64_t* __restrict__ frag_len, nprng::Zig z,
+                             msg_plan_info* __restrict__ info) {
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= n_presets) return;
+    msg_plan_info inf;
+    msgplan::plan_sizes(presets[p], z, frag_len[p], inf);
+    info[p] = inf;
+}
+
+__global__ void k_plan_events(const msg_preset* __restrict__ presets, int n_presets,
+                              const int64_t* __restrict__ frag_len, nprng::Zig z,
+                              const int32_t* __restrict__ slot_base, const int32_t* __restrict__ tap_base,
+                              msg_event* __restrict__ events, int32_t* __restrict__ er_off,
+                              double* __restrict__ er_gain, msg_plan_info* __restrict__ info) {
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= n_presets) return;
+    msg_plan_info inf;
+    const msg_preset& pr = presets[p];
+    const bool er = (pr.flags & MSG_F_ER_CLOUD) != 0;
+    msgplan::plan_events(pr, z, frag_len[p], p, inf, events + slot_base[p],
+                         er ? er_off + tap_base[p] : nullptr, er ? er_gain + tap_base[p] : nullptr);
+    info[p] = inf;
+}
+
+// ---------------------------------------------------------------------------
+// Generators driven by standard_normal(n): parallel ziggurat walk.
+//
+// The stream of raw PCG64 draws is consumed 64 at a time: lane l holds the
+// state of draw base+l (jump-ahead), classifies it as a fast ziggurat accept,
+// and a wave ballot locates the rare draws that start a slow (rejection)
+// normal.  That lane finishes the slow normal sequentially from its own
+// state and reports how many draws it consumed, which moves the parse
+// position.  The emitted sequence is exactly NumPy's standard_normal(n).
+// ---------------------------------------------------------------------------
+struct JumpTab { nprng::u128 a[GEN_T]; nprng::u128 s[GEN_T]; nprng::u128 a64, s64; };
+
+MSG_DEV double slow_normal(nprng::u128 st, nprng::u128 inc, uint64_t rabs, int idx, double x,
+                           const nprng::Zig& z, int& consumed) {
+    nprng::Pcg64 g;
+    g.state = st; g.inc = inc; g.has_u32 = 0; g.u32 = 0;
+    int c = 1;
+    for (;;) {
+        if (idx == 0) {
+            for (;;) {
+                const double xx = -nprng::ZIG_NOR_INV_R * log1p(-nprng::next_double(g));
+                const double yy = -log1p(-nprng::next_double(g));
+                c += 2;
+                if (yy + yy > xx * xx) {
+                    consumed = c;
+                    return ((rabs >> 8) & 1) ? -(nprng::ZIG_NOR_R + xx) : nprng::ZIG_NOR_R + xx;
+                }
+            }
+        }
+        const double u = nprng::next_double(g);
+        c += 1;
+        if (((z.fi[idx - 1] - z.fi[idx]) * u + z.fi[idx]) < exp(-0.5 * x * x)) { consumed = c; return x; }
+        uint64_t r = nprng::next_u64(g);
+        c += 1;
+        idx = (int)(r & 0xff);
+        r >>= 8;
+        const int sign = (int)(r & 1);
+        rabs = (r >> 1) & 0x000fffffffffffffULL;
+        x = (double)rabs * z.wi[idx];
+        if (sign) x = -x;
+        if (rabs < z.ki[idx]) { consumed = c; return x; }
+    }
+}
+
+// Closed-form part of gen_basic for sample j given its normal N_j (MS:235-268).
+struct GenBasicConst {
+    int mode;            // MSG_GEN_*
+    int n, fade;
+    double inv_sr;
+    double f_ring, inv_tau, inv_tau_exc;   // resonant
+    double inv_sigma;                       // gaussian
+};
+MSG_DEV float gen_basic_sample(const GenBasicConst& c, int j, double nrm) {
+    float x;
+    if (c.mode == MSG_GEN_RESONANT) {
+        const double t = (double)j * c.inv_sr;
+        const double cyc = c.f_ring * t;                      // sin(2 pi f t), reduced in float64
+        const float ph = (float)(cyc - floor(cyc));
+        const float ring = sinpif(2.0f * ph) * expf((float)(-t * c.inv_tau));
+        const float exc = (float)nrm * expf((float)(-t * c.inv_tau_exc));
+        x = 0.9f * ring + 0.25f * exc;
+    } else if (c.mode == MSG_GEN_GAUSSIAN_CLICK) {
+        const double u = (double)j * c.inv_sigma;
+        x = (float)(exp(-0.5 * (u * u)) * (nrm * 0.12 + 1.0));
+    } else if (c.mode == MSG_GEN_NOISE_BURST || c.mode == MSG_GEN_SKEWED) {
+        return (float)nrm;                                    // raw normals; tilt/env in k_spectral
+    } else {
+        x = (float)(nrm * 0.1);                               // fallback (MS:263)
+    }
+    return x * fade_w(j, c.n, c.fade);
+}
+
+__global__ void __launch_bounds__(GEN_T)
+k_gen_normal(const msg_preset* __restrict__ presets, const msg_event* __restrict__ events,
+             const PresetRt* __restrict__ rt, const int32_t* __restrict__ ev_list, int n_list,
+             nprng::Zig z, const JumpTab* __restrict__ jt, float* __restrict__ pool) {
+    const int li = blockIdx.x;
+    if (li >= n_list) return;
+    const msg_event& e = events[ev_list[li]];
+    const msg_preset& pr = presets[e.preset];
+    const PresetRt& r = rt[e.preset];
+    const int lane = threadIdx.x;
+    const int n = e.n;
+    float* out = pool + r.pool_base + e.pool_off;
+
+    GenBasicConst c;
+    c.mode = pr.gen_mode == MSG_GEN_FALLBACK ? MSG_GEN_NOISE_BURST : pr.gen_mode;   // MS:686
+    c.n = n;
+    c.fade = (int)(0.01 * n) > 8 ? (int)(0.01 * n) : 8;
+    c.inv_sr = 1.0 / (double)e.gen_sr;
+    c.f_ring = fmax(10.0, pr.ring_hz);
+    c.inv_tau = 1.0 / fmax(1e-6, pr.ring_decay_ms / 1000.0);
+    c.inv_tau_exc = 1.0 / fmax(1e-6, (pr.micro_ms / 1000.0) * 0.15);
+    const int sigma = (int)(0.0025 * n) > 1 ? (int)(0.0025 * n) : 1;
+    c.inv_sigma = 1.0 / (double)sigma;
+
+    // default_rng(seed + i): every lane computes the (uniform) seed state.
+    const nprng::Pcg64 g0 = nprng::default_rng((uint64_t)(pr.seed + e.index));
+    const nprng::u128 inc = g0.inc;
+    const nprng::u128 c64 = inc * jt->s64;
+    nprng::u128 st = jt->a[lane] * g0.state + inc * jt->s[lane];   // state after lane+1 steps
+
+    int produced = 0;
+    int local = 0;   // parse position within the current chunk
+    while (produced < n) {
+        const uint64_t raw = nprng::xsl_rr(st);
+        const int idx = (int)(raw & 0xff);
+        const uint64_t rr = raw >> 8;
+        const uint64_t rabs = (rr >> 1) & 0x000fffffffffffffULL;
+        double x = (double)rabs * z.wi[idx];
+        if (rr & 1) x = -x;
+        const bool fast = rabs < z.ki[idx];
+        const uint64_t F = __ballot(fast);
+        while (local < 64 && produced < n) {
+            const uint64_t S = ~F & (~0ULL << local);
+            const int q = S ? __builtin_ctzll(S) : 64;
+            if (lane >= local && lane < q) {
+                const int j = produced + lane - local;
+                if (j < n) out[j] = gen_basic_sample(c, j, x);
+            }
+            produced += q - local;
+            if (q == 64) { local = 64; break; }
+            int consumed = 1;
+            double v = 0.0;
+            if (lane == q) v = slow_normal(st, inc, rabs, idx, x, z, consumed);
+            v = __shfl(v, q);
+            consumed = __shfl(consumed, q);
+            if (produced < n && lane == 0) out[produced] = gen_basic_sample(c, produced, v);
+            ++produced;
+            local = q + consumed;
+        }
+        do {   // advance all lanes by one chunk; skip chunks a slow normal consumed
+            st = jt->a64 * st + c64;
+            local -= 64;
+        } while (local >= 64);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Overlap-add of placed grains (event order) x ADSR -> mono a[t].
+// ---------------------------------------------------------------------------
+MSG_DEV float adsr_at(const PresetRt& r, int64_t t) {
+    const int64_t n = r.out_n;
+    const int64_t A = r.envA, D = r.envD, R = r.envR;
+    const int64_t i = A;
+    const int64_t j = n < i + D ? n : i + D;
+    const int64_t s1 = (j > n - R) ? j : n - R;
+    const float c = r.envC, S = r.envS;
+    if (A > 0 && t < A) return powf((float)((double)t * (1.0 / (double)A)), c);
+    if (D > 0 && j > i && t >= i && t < j) {
+        const float d = (float)((double)(t - i) * (1.0 / (double)(j - i)));
+        return 1.0f - (1.0f - S) * powf(d, c);
+    }
+    if (t >= j && t < s1) return S;
+    if (R > 0 && n > s1 && t >= s1) {
+        const int64_t num = n - s1;
+        float u;
+        if (num == 1) u = 0.f;
+        else if (t == n - 1) u = 1.f;
+        else u = (float)((double)(t - s1) * (1.0 / (double)(num - 1)));
+        return S * (1.0f - powf(u, c));
+    }
+    return 1.0f;
+}
+
+__global__ void __launch_bounds__(OLA_T)
+k_ola_env(const msg_event* __restrict__ events, const PresetRt* __restrict__ rt,
+          const int32_t* __restrict__ tile_begin, int n_presets,
+          const float* __restrict__ grain_pool, float* __restrict__ mono) {
+    const int b = blockIdx.x;
+    const int p = find_preset(tile_begin, n_presets, b);
+    const PresetRt& r = rt[p];
+    const int64_t t0 = (int64_t)(b - r.tile_begin) * OLA_TILE;
+    const int64_t t1 = t0 + OLA_TILE < r.out_n ? t0 + OLA_TILE : r.out_n;
+    constexpr int PER = OLA_TILE / OLA_T;
+    float acc[PER];
+#pragma unroll
+    for (int u = 0; u < PER; ++u) acc[u] = 0.f;
+    // events sorted by start: first event whose start > t0 - max_n
+    const msg_event* ev = events + r.ev_begin;
+    int lo = 0, hi = r.n_events;
+    const int64_t lim = t0 - (int64_t)r.max_n;
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if ((int64_t)ev[mid].start <= lim) lo = mid + 1; else hi = mid;
+    }
+    for (int k = lo; k < r.n_events; ++k) {
+        const msg_event& e = ev[k];
+        if ((int64_t)e.start >= t1) break;
+        if (e.len <= 0) continue;
+        const int64_t s = e.start, L = e.len;
+        if (s + L <= t0) continue;
+        const float amp = (float)e.amp;
+        const float* g = grain_pool + r.pool_base + e.pool_off + e.offset;
+#pragma unroll
+        for (int u = 0; u < PER; ++u) {
+            const int64_t t = t0 + threadIdx.x + u * OLA_T;
+            const int64_t q = t - s;
+            if (t < t1 && q >= 0 && q < L) acc[u] += amp * g[q];
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+        const int64_t t = t0 + threadIdx.x + u * OLA_T;
+        if (t < t1) mono[r.y_off + t] = acc[u] * adsr_at(r, t);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Stereo (even n: exact 25-tap Bessel FIR form of the spectral rotation),
+// tanh saturation and peak normalisation.
+// ---------------------------------------------------------------------------
+MSG_DEV void stereo_pair(const PresetRt& r, const float* __restrict__ y, int64_t t, float& L, float& R) {
+    const int64_t n = r.out_n;
+    if (!r.stereo_fir) { L = R = y[t]; return; }
+    int64_t il = t - r.dl;
+    il %= n; if (il < 0) il += n;
+    L = y[il];
+    float acc = 0.f;
+    int64_t base = (t + r.dr - 24) % n;
+    if (base < 0) base += n;
+#pragma unroll
+    for (int m = 0; m < 25; ++m) {
+        int64_t idx = base + 2 * m;
+        if (idx >= n) idx -= n;
+        if (idx >= n) idx -= n;
+        acc = fmaf(r.bess[m], y[idx], acc);
+    }
+    R = acc;
+}
+
+__global__ void __launch_bounds__(ST_T)
+k_stereo_max(const PresetRt* __restrict__ rt, const int32_t* __restrict__ st_begin, int n_presets,
+             const float* __restrict__ ybuf, unsigned* __restrict__ maxbits) {
+    const int b = blockIdx.x;
+    const int p = find_preset(st_begin, n_presets, b);
+    const PresetRt& r = rt[p];
+    const int64_t t0 = (int64_t)(b - st_begin[p]) * ST_TILE;
+    const float* y = ybuf + r.y_off;
+    float m = 0.f;
+    for (int u = threadIdx.x; u < ST_TILE; u += ST_T) {
+        const int64_t t = t0 + u;
+        if (t >= r.out_n) break;
+        float L, R;
+        stereo_pair(r, y, t, L, R);
+        m = fmaxf(m, fmaxf(fabsf(L), fabsf(R)));
+    }
+    for (int off = 32; off > 0; off >>= 1) m = fmaxf(m, __shfl_xor(m, off));
+    __shared__ float wm[ST_T / 64];
+    if ((threadIdx.x & 63) == 0) wm[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        float v = wm[0];
+        for (int w = 1; w < ST_T / 64; ++w) v = fmaxf(v, wm[w]);
+        atomicMax(maxbits + p, __float_as_uint(v));
+    }
+}
+
+MSG_DEV float sat(float v, float d, float inv_td) { return d > 0.f ? tanhf(v * d) * inv_td : v; }
+
+__global__ void __launch_bounds__(ST_T)
+k_stereo_out(const PresetRt* __restrict__ rt, const int32_t* __restrict__ st_begin, int n_presets,
+             const float* __restrict__ ybuf, const unsigned* __restrict__ maxbits, float* __restrict__ out) {
+    const int b = blockIdx.x;
+    const int p = find_preset(st_begin, n_presets, b);
+    const PresetRt& r = rt[p];
+    const int64_t t0 = (int64_t)(b - st_begin[p]) * ST_TILE;
+    const float* y = ybuf + r.y_off;
+    const float d = r.drive;
+    const float inv_td = d > 0.f ? 1.0f / tanhf(d) : 1.f;
+    const float M = __uint_as_float(maxbits[p]);
+    const float mc = sat(M, d, inv_td);
+    const float scale = mc > 0.f ? r.peak / mc : 1.f;
+    float2* o = reinterpret_cast<float2*>(out) + r.out_off;
+    for (int u = threadIdx.x; u < ST_TILE; u += ST_T) {
+        const int64_t t = t0 + u;
+        if (t >= r.out_n) break;
+        float L, R;
+        stereo_pair(r, y, t, L, R);
+        o[t] = make_float2(sat(L, d, inv_td) * scale, sat(R, d, inv_td) * scale);
+    }
+}

@@ -1,0 +1,30 @@
+// launch.h — host-side launchers of the kernels compiled in their own
+// translation units (k_spectral.hip, k_fir.hip), so the FFT-heavy kernels
+// build in parallel.
+#pragma once
+#include <hip/hip_runtime.h>
+#include "rt.h"
+
+constexpr int LDS_MAX = 163840;                              // 160 KiB per CU
+constexpr int SPEC_T_BIG = 1024, SPEC_M_BIG = 20480;          // up to 160 KiB LDS
+constexpr int SPEC_T_SMALL = 256, SPEC_M_SMALL = 8192;        // up to 64 KiB LDS
+constexpr int SPEC_SMALL_BYTES = 65536;
+constexpr int FIR_T = 1024, FIR_M = 16384;                    // N <= 32768 real
+constexpr int FIR_NMAX = 32768;
+
+void spectral_init_attrs();
+hipError_t launch_spectral(bool big, unsigned grid, int lds_bytes, hipStream_t s,
+                           const msg_preset* presets, const msg_event* events, const EventRt* ert,
+                           const PresetRt* rt, const RealPlan* plans, const int32_t* ev_list, int n_list,
+                           float* micro_pool, float* grain_pool);
+
+void fir_init_attrs();
+hipError_t launch_ir_spec(unsigned grid, int lds_bytes, hipStream_t s, const int64_t* jobs, int n_jobs,
+                          const RealPlan* fir_plans, const double* ir_bank, float2* ir_spec);
+hipError_t launch_fir_h(unsigned grid, int lds_bytes, hipStream_t s, const PresetRt* rt, const int32_t* hblk_begin,
+                        int n_presets, const RealPlan* fir_plans, const int32_t* fir_plan_of,
+                        const int32_t* er_off, const double* er_gain, const double* ir_bank,
+                        const float2* ir_spec, float2* hspec);
+hipError_t launch_fir(unsigned grid, int lds_bytes, hipStream_t s, const PresetRt* rt, const int32_t* fblk_begin,
+                      int n_presets, const RealPlan* fir_plans, const int32_t* fir_plan_of,
+                      const float2* hspec, const float* x_in, float* y_out);

@@ -22,7 +22,8 @@
 #include "plan.h"
 #include "fftplan.h"
 #include "fft_lds.h"
-#include "kernels.h"
+#include "kernels_core.h"
+#include "launch.h"
 #include "../../include/msgpu.h"
 
 namespace {
@@ -30,10 +31,6 @@ namespace {
 const nprng::Zig kHostZig = {zig_ki_double, zig_wi_double, zig_fi_double,
                              zig_ke_double, zig_we_double, zig_fe_double};
 
-constexpr int SPEC_T_BIG = 1024, SPEC_C_BIG = 20480;    // 160 KiB LDS
-constexpr int SPEC_T_SMALL = 256, SPEC_C_SMALL = 8192;  // 64 KiB LDS
-constexpr int FIR_T = 1024, FIR_C = 16385;              // N <= 32768 real
-constexpr int FIR_NMAX = 32768;
 
 thread_local std::string g_err;   // errors before a context exists
 
@@ -87,7 +84,8 @@ struct msg_ctx {
     DevBuf<PresetRt> prt;
     DevBuf<int32_t> gen_list, spec_small, spec_big, tile_begin, fir_begin, h_begin, st_begin, fir_plan_of;
     DevBuf<float> micro, grain, mono_a, mono_y;
-    DevBuf<float2> hspec;
+    DevBuf<float2> hspec, irspec;
+    DevBuf<int64_t> irjobs;
     DevBuf<double> irbank;
     DevBuf<unsigned> maxbits;
     // host mirrors of the last batch
@@ -143,10 +141,15 @@ static bool make_fftdesc(PlanStore& ps, int m, FftDesc& d, std::string& why) {
             return false;
         }
     }
-    if ((int)rad.size() > 24) { why = "too many radix passes"; return false; }
+    if ((int)rad.size() > FFT_MAXRAD) { why = "too many radix passes"; return false; }
     d.nrad = (int)rad.size();
     for (size_t i = 0; i < rad.size(); ++i) d.rad[i] = rad[i];
-    if (upload(ps, fftplan::twiddles(d.size), &d.tw) != hipSuccess) { why = "hip upload failed"; return false; }
+    d.tw_hi_n = (d.size + TW_LO - 1) / TW_LO;
+    if (upload(ps, fftplan::twiddles(d.size, TW_LO, 1), &d.tw0) != hipSuccess ||
+        upload(ps, fftplan::twiddles(d.size, d.tw_hi_n, TW_LO), &d.tw1) != hipSuccess) {
+        why = "hip upload failed";
+        return false;
+    }
     return true;
 }
 
@@ -161,6 +164,7 @@ static int real_plan(PlanStore& ps, int n, std::string& why) {
     const int m = rp.even ? n / 2 : n;
     if (!make_fftdesc(ps, m, rp.c, why)) return -1;
     rp.lds_c = std::max(rp.even ? m + 1 : m, rp.c.size);
+    rp.lds_bytes = (rp.lds_c + TW_LO + rp.c.tw_hi_n) * 8;
     if (rp.even) {
         std::vector<float> t(2 * (size_t)(m + 1));
         for (int k = 0; k <= m; ++k) {
@@ -291,10 +295,8 @@ msg_ctx* msg_create(int device_ordinal) {
     jt.a64 = j64.a; jt.s64 = j64.s;
     if (!up(ctx->d_jump, &jt, 1)) { g_err = "uploading jump table failed"; return nullptr; }
     for (auto& ev : ctx->ev) hipEventCreate(&ev);
-    hipFuncSetAttribute((const void*)k_spectral<SPEC_T_BIG, SPEC_C_BIG>,
-                        hipFuncAttributeMaxDynamicSharedMemorySize, SPEC_C_BIG * 8);
-    hipFuncSetAttribute((const void*)k_fir<FIR_T, FIR_C>, hipFuncAttributeMaxDynamicSharedMemorySize, FIR_C * 8);
-    hipFuncSetAttribute((const void*)k_fir_h<FIR_T, FIR_C>, hipFuncAttributeMaxDynamicSharedMemorySize, FIR_C * 8);
+    spectral_init_attrs();
+    fir_init_attrs();
     return ctx.release();
 }
 
@@ -314,7 +316,8 @@ void msg_destroy(msg_ctx* ctx) {
     ctx->ert.release(); ctx->prt.release(); ctx->gen_list.release(); ctx->spec_small.release();
     ctx->spec_big.release(); ctx->tile_begin.release(); ctx->fir_begin.release(); ctx->h_begin.release();
     ctx->st_begin.release(); ctx->fir_plan_of.release(); ctx->micro.release(); ctx->grain.release();
-    ctx->mono_a.release(); ctx->mono_y.release(); ctx->hspec.release(); ctx->irbank.release();
+    ctx->mono_a.release(); ctx->mono_y.release(); ctx->hspec.release(); ctx->irspec.release();
+    ctx->irjobs.release(); ctx->irbank.release();
     ctx->maxbits.release();
     delete ctx;
 }
@@ -556,8 +559,11 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
         ir_off[i] = (int64_t)irbank.size();
         irbank.insert(irbank.end(), irs[i], irs[i] + ir_lens[i]);
     }
-    int64_t pool = 0, ysum = 0, hsum = 0;
+    int64_t pool = 0, ysum = 0, hsum = 0, irs_sum = 0;
     int32_t tiles = 0, fblocks = 0, hblocks = 0, stiles = 0;
+    int spec_small_lds = 0, spec_big_lds = 0, fir_lds = 0;
+    std::map<std::pair<int, int>, int64_t> ir_spec_of;   // (IR index, N) -> offset
+    std::vector<int64_t> ir_jobs;                         // [ir_off, ir_len, plan, out_off] per job
     for (int p = 0; p < P; ++p) {
         const msg_preset& pr = presets[p];
         const msg_plan_info& inf = info[p];
@@ -592,6 +598,8 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
         r.ir_len = ir ? (int32_t)std::min<int64_t>(ir_lens[ic], 8192) : 0;
         r.ir_off = ir ? ir_off[ic] : 0;
         r.fir_on = (er || ir) ? 1 : 0;
+        r.fir_block_begin = fblocks;   // prefix arrays must stay monotone for find_preset
+        r.h_block_begin = hblocks;
         if (r.fir_on) {
             const int64_t er_span = er ? (int64_t)std::nearbyint(pr.er_max_ms / 1000.0 * sr) + 1 : 0;
             const int64_t M = (ir ? r.ir_len : 1) + er_span;
@@ -601,10 +609,24 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
             const int fp = real_plan(ctx->fir_plans, N, why);
             if (fp < 0) return fail(ctx, MSG_E_DEVICE, "FIR plan: " + why);
             fir_plan_of[p] = fp;
+            fir_lds = std::max(fir_lds, ctx->fir_plans.host[fp].lds_bytes);
             r.fir_N = N; r.fir_P = Pp; r.fir_Q = Q; r.fir_B = N - Pp + 1;
-            r.fir_block_begin = fblocks;
-            r.h_block_begin = hblocks;
             r.h_off = hsum;
+            if (er && ir) {
+                if (M - 1 > N)
+                    return fail(ctx, MSG_E_UNSUPPORTED, "early-reflection span + IR exceed the 32768-sample FIR "
+                                                        "transform (er_max_ms too long for this rate)");
+                auto key = std::make_pair(ic, N);
+                auto it = ir_spec_of.find(key);
+                if (it == ir_spec_of.end()) {
+                    it = ir_spec_of.emplace(key, irs_sum).first;
+                    ir_jobs.insert(ir_jobs.end(), {r.ir_off, (int64_t)r.ir_len, (int64_t)fp, irs_sum});
+                    irs_sum += N / 2 + 1;
+                }
+                r.irs_off = it->second;
+            } else if (er && M > N) {
+                return fail(ctx, MSG_E_UNSUPPORTED, "early-reflection span exceeds the FIR transform");
+            }
             fblocks += (int32_t)((inf.out_n + r.fir_B - 1) / r.fir_B);
             hblocks += Q;
             hsum += (int64_t)Q * (N / 2 + 1);
@@ -652,11 +674,17 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
                 const int pi = real_plan(ctx->grain_plans, e.n, why);
                 if (pi < 0) return fail(ctx, MSG_E_DEVICE, "grain plan: " + why);
                 x.plan = pi;
-                const int lc = ctx->grain_plans.host[pi].lds_c;
-                if (lc <= SPEC_C_SMALL) spec_small.push_back(ei);
-                else if (lc <= SPEC_C_BIG) spec_big.push_back(ei);
-                else return fail(ctx, MSG_E_UNSUPPORTED, "grain of " + std::to_string(e.n) +
-                                 " samples exceeds the LDS-resident FFT (max ~40958 even / 20479 odd)");
+                const RealPlan& gp = ctx->grain_plans.host[pi];
+                if (gp.lds_bytes <= SPEC_SMALL_BYTES && gp.c.size <= SPEC_M_SMALL) {
+                    spec_small.push_back(ei);
+                    spec_small_lds = std::max(spec_small_lds, gp.lds_bytes);
+                } else if (gp.lds_bytes <= LDS_MAX && gp.c.size <= SPEC_M_BIG) {
+                    spec_big.push_back(ei);
+                    spec_big_lds = std::max(spec_big_lds, gp.lds_bytes);
+                } else {
+                    return fail(ctx, MSG_E_UNSUPPORTED, "grain of " + std::to_string(e.n) +
+                                " samples exceeds the LDS-resident FFT (even n <= ~39900)");
+                }
             } else {
                 spec_small.push_back(ei);
             }
@@ -679,6 +707,8 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
     HIPCHK(ctx, ctx->mono_a.ensure(ysum));
     HIPCHK(ctx, ctx->mono_y.ensure(ysum));
     HIPCHK(ctx, ctx->hspec.ensure(hsum));
+    HIPCHK(ctx, ctx->irspec.ensure(irs_sum));
+    HIPCHK(ctx, ctx->irjobs.ensure(ir_jobs.size()));
     HIPCHK(ctx, ctx->irbank.ensure(irbank.size()));
     HIPCHK(ctx, ctx->maxbits.ensure(P));
     auto h2d = [&](void* dst, const void* src, size_t bytes) -> hipError_t {
@@ -696,6 +726,7 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
     HIPCHK(ctx, h2d(ctx->st_begin.p, st_begin.data(), sizeof(int32_t) * P));
     HIPCHK(ctx, h2d(ctx->fir_plan_of.p, fir_plan_of.data(), sizeof(int32_t) * P));
     HIPCHK(ctx, h2d(ctx->irbank.p, irbank.data(), sizeof(double) * irbank.size()));
+    HIPCHK(ctx, h2d(ctx->irjobs.p, ir_jobs.data(), sizeof(int64_t) * ir_jobs.size()));
     HIPCHK(ctx, hipMemsetAsync(ctx->maxbits.p, 0, sizeof(unsigned) * P, s));
 
     // ---- generate ----
@@ -708,17 +739,13 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
     // ---- spectral chain ----
     stage_mark(ctx, 3, s);
     if (!spec_small.empty())
-        hipLaunchKernelGGL((k_spectral<SPEC_T_SMALL, SPEC_C_SMALL>), dim3((unsigned)spec_small.size()),
-                           dim3(SPEC_T_SMALL), SPEC_C_SMALL * 8, s, ctx->presets.p, ctx->events.p, ctx->ert.p,
-                           ctx->prt.p, ctx->grain_plans.dev.p, ctx->spec_small.p, (int)spec_small.size(),
-                           ctx->micro.p, ctx->grain.p);
-    HIPCHK(ctx, hipGetLastError());
+        HIPCHK(ctx, launch_spectral(false, (unsigned)spec_small.size(), spec_small_lds, s, ctx->presets.p,
+                                    ctx->events.p, ctx->ert.p, ctx->prt.p, ctx->grain_plans.dev.p, ctx->spec_small.p,
+                                    (int)spec_small.size(), ctx->micro.p, ctx->grain.p));
     if (!spec_big.empty())
-        hipLaunchKernelGGL((k_spectral<SPEC_T_BIG, SPEC_C_BIG>), dim3((unsigned)spec_big.size()),
-                           dim3(SPEC_T_BIG), SPEC_C_BIG * 8, s, ctx->presets.p, ctx->events.p, ctx->ert.p,
-                           ctx->prt.p, ctx->grain_plans.dev.p, ctx->spec_big.p, (int)spec_big.size(),
-                           ctx->micro.p, ctx->grain.p);
-    HIPCHK(ctx, hipGetLastError());
+        HIPCHK(ctx, launch_spectral(true, (unsigned)spec_big.size(), spec_big_lds, s, ctx->presets.p,
+                                    ctx->events.p, ctx->ert.p, ctx->prt.p, ctx->grain_plans.dev.p, ctx->spec_big.p,
+                                    (int)spec_big.size(), ctx->micro.p, ctx->grain.p));
     // ---- overlap-add x ADSR ----
     stage_mark(ctx, 4, s);
     hipLaunchKernelGGL(k_ola_env, dim3((unsigned)tiles), dim3(OLA_T), 0, s, ctx->events.p, ctx->prt.p,
@@ -728,14 +755,15 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
     stage_mark(ctx, 5, s);
     float* yb = ctx->mono_a.p;
     if (hblocks > 0) {
-        hipLaunchKernelGGL((k_fir_h<FIR_T, FIR_C>), dim3((unsigned)hblocks), dim3(FIR_T), FIR_C * 8, s,
-                           ctx->prt.p, ctx->h_begin.p, P, ctx->fir_plans.dev.p, ctx->fir_plan_of.p,
-                           ctx->er_off.p, ctx->er_gain.p, ctx->irbank.p, ctx->hspec.p);
-        HIPCHK(ctx, hipGetLastError());
-        hipLaunchKernelGGL((k_fir<FIR_T, FIR_C>), dim3((unsigned)fblocks), dim3(FIR_T), FIR_C * 8, s,
-                           ctx->prt.p, ctx->fir_begin.p, P, ctx->fir_plans.dev.p, ctx->fir_plan_of.p,
-                           ctx->hspec.p, ctx->mono_a.p, ctx->mono_y.p);
-        HIPCHK(ctx, hipGetLastError());
+        if (!ir_jobs.empty()) {
+            HIPCHK(ctx, launch_ir_spec((unsigned)(ir_jobs.size() / 4), fir_lds, s, ctx->irjobs.p,
+                                       (int)(ir_jobs.size() / 4), ctx->fir_plans.dev.p, ctx->irbank.p, ctx->irspec.p));
+        }
+        HIPCHK(ctx, launch_fir_h((unsigned)hblocks, fir_lds, s, ctx->prt.p, ctx->h_begin.p, P,
+                                 ctx->fir_plans.dev.p, ctx->fir_plan_of.p, ctx->er_off.p, ctx->er_gain.p,
+                                 ctx->irbank.p, ctx->irspec.p, ctx->hspec.p));
+        HIPCHK(ctx, launch_fir((unsigned)fblocks, fir_lds, s, ctx->prt.p, ctx->fir_begin.p, P, ctx->fir_plans.dev.p,
+                               ctx->fir_plan_of.p, ctx->hspec.p, ctx->mono_a.p, ctx->mono_y.p));
         // presets with fir_on == 0 in a mixed batch: copy a -> y
         for (int p = 0; p < P; ++p)
             if (!prt[p].fir_on)

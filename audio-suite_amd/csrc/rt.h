@@ -1,0 +1,83 @@
+// rt.h — runtime records and helpers shared by the libmsgpu kernels.
+//
+//   k_plan_sizes / k_plan_events   per-preset planner (one thread per preset)      MS:589-646, 409-417
+//   k_gen_normal                   grain generator, one wave per event              MS:219-269
+//   k_spectral<T>                  LDS-resident spectral chain, one WG per event    MS:39-128, 224-233, 690-702
+//   k_ola_env                      grain overlap-add x ADSR, one WG per tile        MS:742-764
+//   k_fir_h                        (delta + ER) * IR kernel spectra per partition   MS:409-445
+//   k_fir                          partitioned FFT overlap-save FIR                 MS:766-773
+//   k_stereo_max / k_stereo_out    25-tap Bessel stereo, tanh, peak normalise       MS:423-436, 775-781
+#pragma once
+#include "msg_common.h"
+#include "nprng.h"
+#include "plan.h"
+#include "fft_lds.h"
+
+// Per-preset runtime record, built on the host after planning.
+struct PresetRt {
+    int64_t out_n;
+    int64_t out_off;       // first output frame of this preset
+    int64_t pool_base;     // grain pool offset (floats)
+    int64_t y_off;         // mono buffers offset (floats)
+    int32_t ev_begin;      // first event slot
+    int32_t n_events;
+    int32_t er_base;       // first ER tap
+    int32_t n_taps;        // ER taps (0 when ER off)
+    int32_t tile_begin;    // first overlap-add tile
+    int32_t max_n;
+    // ADSR (MS:172-195), in samples
+    int32_t envA, envD, envR;
+    float envS, envC;
+    // FIR (combined ER + IR), 0 = identity
+    int32_t fir_on, fir_N, fir_P, fir_Q, fir_B;
+    int32_t fir_block_begin;
+    int32_t h_block_begin;
+    int32_t ir_len;        // taps of the IR (0 -> delta)
+    int64_t ir_off;        // offset of the IR in the device IR bank (float64)
+    int64_t h_off;         // offset of the Q partition spectra (float2)
+    int64_t irs_off;       // offset of the IR spectrum at size fir_N (float2)
+    // stereo / saturation / normalisation
+    int32_t stereo_fir;    // 1: 25-tap Bessel FIR, 0: L = R = y
+    int32_t dl, dr;
+    float bess[25];        // J_m(0.9 w), m = -12..12
+    float drive, peak;
+    int32_t pad2;
+};
+
+// Per-event spectral work descriptor (host-built after planning).
+struct EventRt {
+    int32_t plan;          // RealPlan index for n
+    int32_t ops;           // bit mask of SPEC_* below
+    int32_t n, gen_sr;
+    double cutoff_gen, roll;
+    double stretch;
+    double tilt_alpha;     // log2 of the per-octave gain (MS:229-230)
+    double env_tau;        // noise/skewed envelope time constant (s)
+    double warp_power;     // fft_warp_power exponent (MS:103-115)
+};
+enum : int32_t {
+    SPEC_TILT_NOISE = 1, SPEC_TILT_SKEW = 2, SPEC_LOWPASS = 4, SPEC_STRETCH = 8, SPEC_WARP = 16,
+};
+
+constexpr int GEN_T = 64;          // one wave per event
+constexpr int OLA_T = 256;
+constexpr int OLA_TILE = 2048;
+constexpr int ST_T = 256;
+constexpr int ST_TILE = 4096;
+
+// shared helpers
+__device__ __forceinline__ int find_preset(const int32_t* __restrict__ begin, int n_presets, int b) {
+    int lo = 0, hi = n_presets - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (begin[mid] <= b) lo = mid; else hi = mid - 1;
+    }
+    return lo;
+}
+
+MSG_DEV float fade_w(int j, int n, int fade) {
+    double w = 1.0;
+    if (j < fade) w *= (double)j * (1.0 / (double)fade);
+    if (j >= n - fade) w *= (double)(j - (n - fade)) * (-1.0 / (double)fade) + 1.0;
+    return (float)w;
+}

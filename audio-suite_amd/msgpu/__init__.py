@@ -12,10 +12,10 @@ from .params import DEFAULTS, CONFIGS, config_params, merged  # noqa: F401
 
 
 def render(params, progress=None, device: int = 0):
-    from .render import render as _render
+    from .dropin import render as _render
     return _render(params, progress, device)
 
 
 def render_batch(params_list, device: int = 0):
-    from .render import render_batch as _rb
+    from .dropin import render_batch as _rb
     return _rb(params_list, device)

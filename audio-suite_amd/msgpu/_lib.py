@@ -121,6 +121,13 @@ def lib() -> C.CDLL:
             if not os.path.exists(LIB_PATH):
                 raise RuntimeError(f"libmsgpu not built: {LIB_PATH} is missing "
                                    "(run `python -c 'import __graft_entry__ as g; g.build()'`)")
+            # torch bundles its own HIP runtime and resolves it by file name; load it
+            # first so libmsgpu binds to that same libamdhip64.so.7 (by SONAME)
+            # instead of a second copy from /opt/rocm.
+            try:
+                import torch  # noqa: F401
+            except ImportError:
+                pass
             L = C.CDLL(LIB_PATH)
             for name, (res, args) in _PROTOS.items():
                 f = getattr(L, name)

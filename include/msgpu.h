@@ -4,7 +4,7 @@
  * Drop-in boundary: the reference's only interface on this path is the Python
  * function  render(params: dict, progress=None) -> (audio[out_n, 2], meta)
  * (microsound_0.2.1/main_v2.py:588-792, "MS").  The Python shim
- * audio-suite_amd/msgpu/render.py keeps that signature and binds this library
+ * audio-suite_amd/msgpu/dropin.py keeps that signature and binds this library
  * with ctypes (INTEGRATION.md shows the binding).  Every entry point takes plain
  * pointers and sizes, never throws, and reports failure as a non-zero status
  * with the text in msg_last_error().
