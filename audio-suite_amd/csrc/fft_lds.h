@@ -40,7 +40,7 @@ struct FftDesc {
 struct RealPlan {
     int32_t n;
     int32_t even;
-    int32_t lds_c;        // complex slots of LDS for data
+    int32_t lds_c;        // physical complex slots of LDS for data (padded, lds_phys)
     int32_t lds_bytes;    // data + staged twiddle tables
     FftDesc c;
     const float2* rtw;    // even: exp(-2 pi i k / n), k <= n/2
@@ -146,6 +146,14 @@ template <bool INV> struct Dft<16, INV> { static MSG_DEV void run(float2* v) { D
 template <bool INV> struct Dft<20, INV> { static MSG_DEV void run(float2* v) { DftComp<4, 5, INV>::run(v); } };
 template <bool INV> struct Dft<25, INV> { static MSG_DEV void run(float2* v) { DftComp<5, 5, INV>::run(v); } };
 
+// LDS data layout: logical complex element i lives at lp(i) = i ^ ((i>>4)&15),
+// an XOR swizzle inside each aligned 16-element (128-byte) block.  Contiguous
+// runs stay conflict-free (each block is permuted in place) and the strided
+// Stockham stores of the early passes (element stride R*8 bytes) spread over
+// all banks of a ds_write_b64 16-lane group.
+MSG_DEV int lp(int i) { return i ^ ((i >> 4) & 15); }
+MSG_HD constexpr int lds_phys(int logical) { return (logical + 15) & ~15; }
+
 // Staged twiddle tables in LDS.
 struct TwLds { const float2* t0; const float2* t1; };
 MSG_DEV float2 tw_at(const TwLds& tw, int i) { return cmul(tw.t1[i >> 7], tw.t0[i & (TW_LO - 1)]); }
@@ -158,67 +166,110 @@ MSG_DEV int fdiv(int j, int d, float inv_d) {
     return q;
 }
 
-template <int R, int T, int MAXM, bool INV>
+// Opaque copy of a wave-uniform int: values derived from it are not hoisted
+// out of the enclosing loop by LICM (register-pressure guard).
+MSG_DEV int opaque(int v) {
+    int o = __builtin_amdgcn_readfirstlane(v);
+    asm volatile("" : "+s"(o));
+    return o;
+}
+
+// Opaque thread index: per-thread LDS addresses derived from it are rebuilt
+// inside each pass/step instead of being hoisted (and spilled) by LICM.
+MSG_DEV int otid() {
+    int t = (int)threadIdx.x;
+    asm volatile("" : "+v"(t));
+    return t;
+}
+
+// One forward Stockham pass of radix R over buf[0..size), Ns = product of the
+// earlier radices.  Twiddles w^r for r < R come from w, w^2, w^3, w^4 and a
+// running power of w^4 (five live values, product depth <= R/4 + 2).
+template <int R, int T, int MAXM>
 MSG_DEV void stockham_pass(float2* buf, int size, int Ns, const TwLds& tw) {
     constexpr int BMAX = (MAXM + R * T - 1) / (R * T);
     const int nb = size / R;
     const int stride = size / (Ns * R);
     const float inv_ns = 1.0f / (float)Ns;
+    const int tid = otid();
     float2 v[BMAX][R];
 #pragma unroll
     for (int b = 0; b < BMAX; ++b) {
-        const int j = (int)threadIdx.x + b * T;
+        const int j = tid + b * T;
         if (j < nb) {
 #pragma unroll
-            for (int r = 0; r < R; ++r) v[b][r] = buf[j + r * nb];
+            for (int r = 0; r < R; ++r) v[b][r] = buf[lp(j + r * nb)];
         }
     }
     __syncthreads();
 #pragma unroll
     for (int b = 0; b < BMAX; ++b) {
-        const int j = (int)threadIdx.x + b * T;
+        const int j = tid + b * T;
         if (j < nb) {
             const int q = fdiv(j, Ns, inv_ns);
             const int k = j - q * Ns;
             if (k != 0) {
-                float2 p[R];
-                p[1] = tw_at(tw, k * stride);
+                const float2 w1 = tw_at(tw, k * stride);
+                const float2 w2 = cmul(w1, w1);
+                const float2 w3 = cmul(w2, w1);
+                const float2 w4 = cmul(w2, w2);
+                float2 pw = make_float2(1.f, 0.f);   // w^(4a)
 #pragma unroll
-                for (int r = 2; r < R; ++r) p[r] = cmul(p[r >> 1], p[r - (r >> 1)]);
-#pragma unroll
-                for (int r = 1; r < R; ++r) v[b][r] = INV ? cmulc(v[b][r], p[r]) : cmul(v[b][r], p[r]);
+                for (int r = 1; r < R; ++r) {
+                    if (r % 4 == 0) pw = (r == 4) ? w4 : cmul(pw, w4);
+                    const int e = r % 4;
+                    const float2 wr = e == 0 ? pw : (r < 4 ? (e == 1 ? w1 : e == 2 ? w2 : w3)
+                                                           : cmul(pw, e == 1 ? w1 : e == 2 ? w2 : w3));
+                    v[b][r] = cmul(v[b][r], wr);
+                }
             }
-            Dft<R, INV>::run(v[b]);
+            Dft<R, false>::run(v[b]);
             const int base = q * Ns * R + k;
 #pragma unroll
-            for (int r = 0; r < R; ++r) buf[base + r * Ns] = v[b][r];
+            for (int r = 0; r < R; ++r) buf[lp(base + r * Ns)] = v[b][r];
         }
     }
     __syncthreads();
 }
 
-// Unnormalised complex DFT of buf[0..size) by the plan's radix sequence.
-// Not inlined: one copy per (T, MAXM, INV) keeps code size and build time sane.
-template <int T, int MAXM, bool INV>
-MSG_NOINL void stockham(float2* buf, int size, const int32_t* rad, int nrad, const TwLds& tw) {
+// Radix sets compiled into a kernel: all (arbitrary grain lengths) or powers
+// of two only (FIR transforms).
+enum { RSET_ALL = 0, RSET_PO2 = 1 };
+
+// Unnormalised forward complex DFT of buf[0..size) by the plan's radix sequence.
+template <int T, int MAXM, int RSET>
+MSG_DEV void stockham_fwd(float2* buf, int size, const int32_t* rad, int nrad, const TwLds& tw) {
     int Ns = 1;
     for (int p = 0; p < nrad; ++p) {
         const int R = rad[p];
-        switch (R) {
-            case 2: stockham_pass<2, T, MAXM, INV>(buf, size, Ns, tw); break;
-            case 3: stockham_pass<3, T, MAXM, INV>(buf, size, Ns, tw); break;
-            case 4: stockham_pass<4, T, MAXM, INV>(buf, size, Ns, tw); break;
-            case 5: stockham_pass<5, T, MAXM, INV>(buf, size, Ns, tw); break;
-            case 6: stockham_pass<6, T, MAXM, INV>(buf, size, Ns, tw); break;
-            case 7: stockham_pass<7, T, MAXM, INV>(buf, size, Ns, tw); break;
-            case 8: stockham_pass<8, T, MAXM, INV>(buf, size, Ns, tw); break;
-            case 9: stockham_pass<9, T, MAXM, INV>(buf, size, Ns, tw); break;
-            case 10: stockham_pass<10, T, MAXM, INV>(buf, size, Ns, tw); break;
-            case 12: stockham_pass<12, T, MAXM, INV>(buf, size, Ns, tw); break;
-            case 15: stockham_pass<15, T, MAXM, INV>(buf, size, Ns, tw); break;
-            case 16: stockham_pass<16, T, MAXM, INV>(buf, size, Ns, tw); break;
-            case 20: stockham_pass<20, T, MAXM, INV>(buf, size, Ns, tw); break;
-            default: stockham_pass<25, T, MAXM, INV>(buf, size, Ns, tw); break;
+        // Opaque per-pass copy of the length: stops LICM from hoisting the
+        // address arithmetic of every switch case out of the pass loop (which
+        // kept hundreds of values live and spilled them to scratch).
+        size = opaque(size);
+        if (RSET == RSET_PO2) {
+            switch (R) {
+                case 2: stockham_pass<2, T, MAXM>(buf, size, Ns, tw); break;
+                case 4: stockham_pass<4, T, MAXM>(buf, size, Ns, tw); break;
+                case 8: stockham_pass<8, T, MAXM>(buf, size, Ns, tw); break;
+                default: stockham_pass<16, T, MAXM>(buf, size, Ns, tw); break;
+            }
+        } else {
+            switch (R) {
+                case 2: stockham_pass<2, T, MAXM>(buf, size, Ns, tw); break;
+                case 3: stockham_pass<3, T, MAXM>(buf, size, Ns, tw); break;
+                case 4: stockham_pass<4, T, MAXM>(buf, size, Ns, tw); break;
+                case 5: stockham_pass<5, T, MAXM>(buf, size, Ns, tw); break;
+                case 6: stockham_pass<6, T, MAXM>(buf, size, Ns, tw); break;
+                case 7: stockham_pass<7, T, MAXM>(buf, size, Ns, tw); break;
+                case 8: stockham_pass<8, T, MAXM>(buf, size, Ns, tw); break;
+                case 9: stockham_pass<9, T, MAXM>(buf, size, Ns, tw); break;
+                case 10: stockham_pass<10, T, MAXM>(buf, size, Ns, tw); break;
+                case 12: stockham_pass<12, T, MAXM>(buf, size, Ns, tw); break;
+                case 15: stockham_pass<15, T, MAXM>(buf, size, Ns, tw); break;
+                case 16: stockham_pass<16, T, MAXM>(buf, size, Ns, tw); break;
+                case 20: stockham_pass<20, T, MAXM>(buf, size, Ns, tw); break;
+                default: stockham_pass<25, T, MAXM>(buf, size, Ns, tw); break;
+            }
         }
         Ns *= R;
     }
@@ -233,107 +284,114 @@ MSG_DEV TwLds stage_twiddles(float2* dst, const FftDesc& d) {
     return TwLds{dst, dst + TW_LO};
 }
 
-// Complex DFT of length d.m in buf (Bluestein-aware).  Forward: exp(-2 pi i jk/m).
-template <int T, int MAXM, bool INV>
-MSG_DEV void cfft(float2* buf, const FftDesc& d, const TwLds& tw) {
-    if (!d.blue) {
-        stockham<T, MAXM, INV>(buf, d.size, d.rad, d.nrad, tw);
-        return;
-    }
-    // Bluestein: X = chirp . IFFT_M( FFT_M(x . chirp) . B ) / M ; inverse via conjugation.
+// Forward complex DFT of length d.m in buf (Bluestein-aware, exp(-2 pi i jk/m)).
+// Bluestein: X = chirp . IFFT_M( FFT_M(x . chirp) . B ) / M, the inner inverse
+// as conj(FFT_M(conj(.))).  One call site of the Stockham engine.
+template <int T, int MAXM, int RSET>
+MSG_DEV void cfft_fwd(float2* buf, const FftDesc& d, const TwLds& tw) {
     const int m = d.m, M = d.size;
-    for (int j = (int)threadIdx.x; j < M; j += T) {
-        float2 x = j < m ? buf[j] : make_float2(0.f, 0.f);
-        if (INV) x = cconj(x);
-        buf[j] = j < m ? cmul(x, d.chirp[j]) : x;
+    const int rounds = d.blue ? 2 : 1;
+    const int tid = otid();
+    for (int round = 0; round < rounds; ++round) {
+        if (d.blue) {
+            for (int j = tid; j < M; j += T) {
+                float2 x;
+                if (round == 0) x = j < m ? cmul(buf[lp(j)], d.chirp[j]) : make_float2(0.f, 0.f);
+                else x = cconj(cmul(buf[lp(j)], d.bspec[j]));
+                buf[lp(j)] = x;
+            }
+            __syncthreads();
+        }
+        stockham_fwd<T, MAXM, RSET>(buf, d.size, d.rad, d.nrad, tw);
     }
-    __syncthreads();
-    stockham<T, MAXM, false>(buf, M, d.rad, d.nrad, tw);
-    for (int j = (int)threadIdx.x; j < M; j += T) buf[j] = cmul(buf[j], d.bspec[j]);
-    __syncthreads();
-    stockham<T, MAXM, true>(buf, M, d.rad, d.nrad, tw);
-    const float s = 1.0f / (float)M;
-    for (int j = (int)threadIdx.x; j < m; j += T) {
-        const float2 y = cscale(cmul(buf[j], d.chirp[j]), s);
-        buf[j] = INV ? cconj(y) : y;
+    if (d.blue) {
+        const float s = 1.0f / (float)M;
+        for (int j = tid; j < m; j += T) buf[lp(j)] = cscale(cmul(cconj(buf[lp(j)]), d.chirp[j]), s);
+        __syncthreads();
     }
-    __syncthreads();
 }
 
 // ---- real transforms over the LDS buffer ----
-// After rfft: X[k] at buf[k], k = 0 .. n/2 (even n) or (n-1)/2 (odd n).
-// Real samples x[t]: ((float*)buf)[t] for even n, buf[t].x for odd n.
+// Spectrum bin / complex element k lives at cx(buf, k) (swizzled).  Real
+// samples x[t] are the packed pairs of element t/2 (even n) or element t's
+// real part (odd n): rx_get / rx_set.
 MSG_DEV float rx_get(const float2* buf, const RealPlan& rp, int t) {
-    return rp.even ? reinterpret_cast<const float*>(buf)[t] : buf[t].x;
+    if (rp.even) { const float2 c = buf[lp(t >> 1)]; return (t & 1) ? c.y : c.x; }
+    return buf[lp(t)].x;
 }
 MSG_DEV void rx_set(float2* buf, const RealPlan& rp, int t, float v) {
-    if (rp.even) reinterpret_cast<float*>(buf)[t] = v;
-    else buf[t] = make_float2(v, 0.f);
+    if (rp.even) reinterpret_cast<float*>(buf)[2 * lp(t >> 1) + (t & 1)] = v;
+    else buf[lp(t)] = make_float2(v, 0.f);
 }
+MSG_DEV float2& cx(float2* buf, int k) { return buf[lp(k)]; }
 
-template <int T, int MAXM>
-MSG_DEV void rfft_lds(float2* buf, const RealPlan& rp, const TwLds& tw) {
-    cfft<T, MAXM, false>(buf, rp.c, tw);
-    if (!rp.even) return;
-    const int m = rp.n / 2;
-    // X[k] = E + W^k O ; E = (Z[k] + conj Z[m-k])/2 ; O = -i (Z[k] - conj Z[m-k])/2
-    for (int k = (int)threadIdx.x; k <= m / 2; k += T) {
-        if (k == 0) {
-            const float2 z0 = buf[0];
-            buf[0] = make_float2(z0.x + z0.y, 0.f);
-            buf[m] = make_float2(z0.x - z0.y, 0.f);
-            continue;
-        }
-        const float2 zk = buf[k], zm = buf[m - k];
-        const float2 e1 = cscale(cadd(zk, cconj(zm)), 0.5f);
-        const float2 d1 = csub(zk, cconj(zm));
-        const float2 o1 = make_float2(0.5f * d1.y, -0.5f * d1.x);
-        const float2 e2 = cscale(cadd(zm, cconj(zk)), 0.5f);
-        const float2 d2 = csub(zm, cconj(zk));
-        const float2 o2 = make_float2(0.5f * d2.y, -0.5f * d2.x);
-        buf[k] = cadd(e1, cmul(rp.rtw[k], o1));
-        buf[m - k] = cadd(e2, cmul(rp.rtw[m - k], o2));
-    }
-    __syncthreads();
-}
-
-// Inverse of rfft_lds with numpy.fft.irfft normalisation; the imaginary parts of
-// the DC and (even n) Nyquist bins are ignored, as irfft does.
-template <int T, int MAXM>
-MSG_DEV void irfft_lds(float2* buf, const RealPlan& rp, const TwLds& tw) {
+// Real transform in place: forward (rfft: x -> X[0..n/2]) or inverse
+// (irfft, numpy normalisation; imaginary parts of the DC and even-n Nyquist
+// bins ignored as irfft does).  The inverse runs the forward engine on the
+// conjugated half-spectrum, so each kernel inlines the engine once.
+template <int T, int MAXM, int RSET>
+MSG_DEV void rtransform(float2* buf, const RealPlan& rp, const TwLds& tw, bool inverse) {
     const int n = rp.n;
-    if (rp.even) {
-        const int m = n / 2;
-        for (int k = (int)threadIdx.x; k <= m / 2; k += T) {
+    const int m = n / 2;
+    const int tid = otid();
+    if (inverse) {   // pre: Z = E + i O from Y, stored conjugated
+        if (rp.even) {
+            for (int k = tid; k <= m / 2; k += T) {
+                if (k == 0) {
+                    const float y0 = cx(buf, 0).x, ym = cx(buf, m).x;
+                    cx(buf, 0) = make_float2(0.5f * (y0 + ym), -0.5f * (y0 - ym));
+                    continue;
+                }
+                const float2 yk = cx(buf, k), ym = cx(buf, m - k);
+                const float2 e1 = cscale(cadd(yk, cconj(ym)), 0.5f);
+                const float2 o1 = cscale(cmulc(csub(yk, cconj(ym)), rp.rtw[k]), 0.5f);
+                const float2 e2 = cscale(cadd(ym, cconj(yk)), 0.5f);
+                const float2 o2 = cscale(cmulc(csub(ym, cconj(yk)), rp.rtw[m - k]), 0.5f);
+                cx(buf, k) = make_float2(e1.x - o1.y, -(e1.y + o1.x));
+                cx(buf, m - k) = make_float2(e2.x - o2.y, -(e2.y + o2.x));
+            }
+        } else {
+            const int K = (n + 1) / 2;
+            for (int k = tid; k < K; k += T) {
+                const float2 y = cx(buf, k);
+                if (k == 0) { cx(buf, 0) = make_float2(y.x, 0.f); continue; }
+                cx(buf, n - k) = y;          // conj of the mirrored conj(Y[k])
+                cx(buf, k) = cconj(y);
+            }
+        }
+        __syncthreads();
+    }
+    cfft_fwd<T, MAXM, RSET>(buf, rp.c, tw);
+    if (!inverse) {
+        if (!rp.even) return;
+        // X[k] = E + W^k O ; E = (Z[k] + conj Z[m-k])/2 ; O = -i (Z[k] - conj Z[m-k])/2
+        for (int k = tid; k <= m / 2; k += T) {
             if (k == 0) {
-                const float y0 = buf[0].x, ym = buf[m].x;
-                buf[0] = make_float2(0.5f * (y0 + ym), 0.5f * (y0 - ym));
+                const float2 z0 = cx(buf, 0);
+                cx(buf, 0) = make_float2(z0.x + z0.y, 0.f);
+                cx(buf, m) = make_float2(z0.x - z0.y, 0.f);
                 continue;
             }
-            const float2 yk = buf[k], ym = buf[m - k];
-            // E = (Y[k] + conj Y[m-k])/2 ; O = conj(W^k) (Y[k] - conj Y[m-k])/2 ; Z = E + i O
-            const float2 e1 = cscale(cadd(yk, cconj(ym)), 0.5f);
-            const float2 o1 = cscale(cmulc(csub(yk, cconj(ym)), rp.rtw[k]), 0.5f);
-            const float2 e2 = cscale(cadd(ym, cconj(yk)), 0.5f);
-            const float2 o2 = cscale(cmulc(csub(ym, cconj(yk)), rp.rtw[m - k]), 0.5f);
-            buf[k] = make_float2(e1.x - o1.y, e1.y + o1.x);
-            buf[m - k] = make_float2(e2.x - o2.y, e2.y + o2.x);
+            const float2 zk = cx(buf, k), zm = cx(buf, m - k);
+            const float2 e1 = cscale(cadd(zk, cconj(zm)), 0.5f);
+            const float2 d1 = csub(zk, cconj(zm));
+            const float2 o1 = make_float2(0.5f * d1.y, -0.5f * d1.x);
+            const float2 e2 = cscale(cadd(zm, cconj(zk)), 0.5f);
+            const float2 d2 = csub(zm, cconj(zk));
+            const float2 o2 = make_float2(0.5f * d2.y, -0.5f * d2.x);
+            cx(buf, k) = cadd(e1, cmul(rp.rtw[k], o1));
+            cx(buf, m - k) = cadd(e2, cmul(rp.rtw[m - k], o2));
         }
-        __syncthreads();
-        cfft<T, MAXM, true>(buf, rp.c, tw);
-        const float s = 1.0f / (float)m;
-        for (int j = (int)threadIdx.x; j < m; j += T) buf[j] = cscale(buf[j], s);
         __syncthreads();
     } else {
-        const int K = (n + 1) / 2;
-        for (int k = (int)threadIdx.x; k < K; k += T) {
-            if (k == 0) { buf[0].y = 0.f; continue; }
-            buf[n - k] = cconj(buf[k]);
+        // post: x = conj(result) / (m or n)
+        if (rp.even) {
+            const float s = 1.0f / (float)m;
+            for (int j = tid; j < m; j += T) { const float2 z = cx(buf, j); cx(buf, j) = make_float2(z.x * s, -z.y * s); }
+        } else {
+            const float s = 1.0f / (float)n;
+            for (int j = tid; j < n; j += T) cx(buf, j) = make_float2(cx(buf, j).x * s, 0.f);
         }
-        __syncthreads();
-        cfft<T, MAXM, true>(buf, rp.c, tw);
-        const float s = 1.0f / (float)n;
-        for (int j = (int)threadIdx.x; j < n; j += T) buf[j] = make_float2(buf[j].x * s, 0.f);
         __syncthreads();
     }
 }

@@ -75,43 +75,49 @@ MSG_DEV double slow_normal(nprng::u128 st, nprng::u128 inc, uint64_t rabs, int i
 }
 
 // Closed-form part of gen_basic for sample j given its normal N_j (MS:235-268).
+// The ring phase is reduced in float64 (f*t reaches ~150 cycles at 30 MHz);
+// the decays are exp2f of j times a float64-built coefficient.
 struct GenBasicConst {
     int mode;            // MSG_GEN_*
     int n, fade;
-    double inv_sr;
-    double f_ring, inv_tau, inv_tau_exc;   // resonant
-    double inv_sigma;                       // gaussian
+    float inv_fade;
+    double f_over_sr;    // resonant: cycles per sample
+    float k_ring, k_exc; // resonant: log2 decay per sample
+    float inv_sigma;     // gaussian click
 };
 MSG_DEV float gen_basic_sample(const GenBasicConst& c, int j, double nrm) {
     float x;
+    const float jf = (float)j;
     if (c.mode == MSG_GEN_RESONANT) {
-        const double t = (double)j * c.inv_sr;
-        const double cyc = c.f_ring * t;                      // sin(2 pi f t), reduced in float64
+        const double cyc = (double)j * c.f_over_sr;
         const float ph = (float)(cyc - floor(cyc));
-        const float ring = sinpif(2.0f * ph) * expf((float)(-t * c.inv_tau));
-        const float exc = (float)nrm * expf((float)(-t * c.inv_tau_exc));
-        x = 0.9f * ring + 0.25f * exc;
+        x = 0.9f * sinpif(2.0f * ph) * exp2f(jf * c.k_ring) + 0.25f * (float)nrm * exp2f(jf * c.k_exc);
     } else if (c.mode == MSG_GEN_GAUSSIAN_CLICK) {
-        const double u = (double)j * c.inv_sigma;
-        x = (float)(exp(-0.5 * (u * u)) * (nrm * 0.12 + 1.0));
+        const float u = jf * c.inv_sigma;
+        x = expf(-0.5f * (u * u)) * ((float)nrm * 0.12f + 1.0f);
     } else if (c.mode == MSG_GEN_NOISE_BURST || c.mode == MSG_GEN_SKEWED) {
         return (float)nrm;                                    // raw normals; tilt/env in k_spectral
     } else {
-        x = (float)(nrm * 0.1);                               // fallback (MS:263)
+        x = (float)nrm * 0.1f;                                // gen_basic's last branch (MS:263)
     }
-    return x * fade_w(j, c.n, c.fade);
+    if (j < c.fade) x *= jf * c.inv_fade;
+    if (j >= c.n - c.fade) x *= (float)(j - (c.n - c.fade)) * -c.inv_fade + 1.0f;
+    return x;
 }
 
 __global__ void __launch_bounds__(GEN_T)
 k_gen_normal(const msg_preset* __restrict__ presets, const msg_event* __restrict__ events,
              const PresetRt* __restrict__ rt, const int32_t* __restrict__ ev_list, int n_list,
              nprng::Zig z, const JumpTab* __restrict__ jt, float* __restrict__ pool) {
+    __shared__ uint64_t s_ki[256];
+    __shared__ double s_wi[256];
     const int li = blockIdx.x;
     if (li >= n_list) return;
+    const int lane = threadIdx.x;
+    for (int i = lane; i < 256; i += GEN_T) { s_ki[i] = z.ki[i]; s_wi[i] = z.wi[i]; }
     const msg_event& e = events[ev_list[li]];
     const msg_preset& pr = presets[e.preset];
     const PresetRt& r = rt[e.preset];
-    const int lane = threadIdx.x;
     const int n = e.n;
     float* out = pool + r.pool_base + e.pool_off;
 
@@ -119,18 +125,22 @@ k_gen_normal(const msg_preset* __restrict__ presets, const msg_event* __restrict
     c.mode = pr.gen_mode == MSG_GEN_FALLBACK ? MSG_GEN_NOISE_BURST : pr.gen_mode;   // MS:686
     c.n = n;
     c.fade = (int)(0.01 * n) > 8 ? (int)(0.01 * n) : 8;
-    c.inv_sr = 1.0 / (double)e.gen_sr;
-    c.f_ring = fmax(10.0, pr.ring_hz);
-    c.inv_tau = 1.0 / fmax(1e-6, pr.ring_decay_ms / 1000.0);
-    c.inv_tau_exc = 1.0 / fmax(1e-6, (pr.micro_ms / 1000.0) * 0.15);
+    c.inv_fade = (float)(1.0 / (double)c.fade);
+    const double inv_sr = 1.0 / (double)e.gen_sr;
+    c.f_over_sr = fmax(10.0, pr.ring_hz) * inv_sr;
+    const double log2e = 1.4426950408889634;
+    c.k_ring = (float)(-inv_sr / fmax(1e-6, pr.ring_decay_ms / 1000.0) * log2e);
+    c.k_exc = (float)(-inv_sr / fmax(1e-6, (pr.micro_ms / 1000.0) * 0.15) * log2e);
     const int sigma = (int)(0.0025 * n) > 1 ? (int)(0.0025 * n) : 1;
-    c.inv_sigma = 1.0 / (double)sigma;
+    c.inv_sigma = (float)(1.0 / (double)sigma);
 
     // default_rng(seed + i): every lane computes the (uniform) seed state.
     const nprng::Pcg64 g0 = nprng::default_rng((uint64_t)(pr.seed + e.index));
     const nprng::u128 inc = g0.inc;
+    const nprng::u128 a64 = jt->a64;
     const nprng::u128 c64 = inc * jt->s64;
     nprng::u128 st = jt->a[lane] * g0.state + inc * jt->s[lane];   // state after lane+1 steps
+    __syncthreads();
 
     int produced = 0;
     int local = 0;   // parse position within the current chunk
@@ -139,9 +149,9 @@ k_gen_normal(const msg_preset* __restrict__ presets, const msg_event* __restrict
         const int idx = (int)(raw & 0xff);
         const uint64_t rr = raw >> 8;
         const uint64_t rabs = (rr >> 1) & 0x000fffffffffffffULL;
-        double x = (double)rabs * z.wi[idx];
+        double x = (double)rabs * s_wi[idx];
         if (rr & 1) x = -x;
-        const bool fast = rabs < z.ki[idx];
+        const bool fast = rabs < s_ki[idx];
         const uint64_t F = __ballot(fast);
         while (local < 64 && produced < n) {
             const uint64_t S = ~F & (~0ULL << local);
@@ -162,7 +172,7 @@ k_gen_normal(const msg_preset* __restrict__ presets, const msg_event* __restrict
             local = q + consumed;
         }
         do {   // advance all lanes by one chunk; skip chunks a slow normal consumed
-            st = jt->a64 * st + c64;
+            st = a64 * st + c64;
             local -= 64;
         } while (local >= 64);
     }
@@ -242,48 +252,80 @@ k_ola_env(const msg_event* __restrict__ events, const PresetRt* __restrict__ rt,
 // Stereo (even n: exact 25-tap Bessel FIR form of the spectral rotation),
 // tanh saturation and peak normalisation.
 // ---------------------------------------------------------------------------
-MSG_DEV void stereo_pair(const PresetRt& r, const float* __restrict__ y, int64_t t, float& L, float& R) {
+// A block handles ST_TILE frames [t0, t0+ST_TILE) of one preset.  The
+// right-channel window y[(t0 + dr - 24 + u) mod n], u < ST_TILE + 48, is staged
+// in LDS once (one modulo per block), so each output is 25 LDS reads + FMAs.
+// L[t] = y[(t - dl) mod n] is a shifted coalesced read.
+struct StereoTile {
+    int64_t t0, t1;          // frames of this tile
+    int64_t lbase;           // (t0 - dl) mod n
+};
+
+MSG_DEV int64_t mod_n(int64_t i, int64_t n) {
+    i %= n;
+    return i < 0 ? i + n : i;
+}
+
+// Stage the R window into w[0 .. ST_TILE+48); returns the tile bounds.
+MSG_DEV StereoTile stereo_stage(const PresetRt& r, const float* __restrict__ y, int64_t t0, float* w) {
     const int64_t n = r.out_n;
-    if (!r.stereo_fir) { L = R = y[t]; return; }
-    int64_t il = t - r.dl;
-    il %= n; if (il < 0) il += n;
+    StereoTile st;
+    st.t0 = t0;
+    st.t1 = t0 + ST_TILE < n ? t0 + ST_TILE : n;
+    st.lbase = mod_n(t0 - r.dl, n);
+    if (r.stereo_fir) {
+        const int64_t b0 = mod_n(t0 + r.dr - 24, n);
+        for (int u = threadIdx.x; u < ST_TILE + 48; u += ST_T) {
+            int64_t i = b0 + u;
+            while (i >= n) i -= n;
+            w[u] = y[i];
+        }
+    }
+    __syncthreads();
+    return st;
+}
+
+MSG_DEV void stereo_at(const PresetRt& r, const float* __restrict__ y, const float* w, const StereoTile& st,
+                       int u, float& L, float& R) {
+    const int64_t n = r.out_n;
+    if (!r.stereo_fir) { L = R = y[st.t0 + u]; return; }
+    int64_t il = st.lbase + u;
+    if (il >= n) il -= n;
     L = y[il];
     float acc = 0.f;
-    int64_t base = (t + r.dr - 24) % n;
-    if (base < 0) base += n;
 #pragma unroll
-    for (int m = 0; m < 25; ++m) {
-        int64_t idx = base + 2 * m;
-        if (idx >= n) idx -= n;
-        if (idx >= n) idx -= n;
-        acc = fmaf(r.bess[m], y[idx], acc);
-    }
+    for (int m = 0; m < 25; ++m) acc = fmaf(r.bess[m], w[u + 2 * m], acc);
     R = acc;
 }
 
 __global__ void __launch_bounds__(ST_T)
 k_stereo_max(const PresetRt* __restrict__ rt, const int32_t* __restrict__ st_begin, int n_presets,
              const float* __restrict__ ybuf, unsigned* __restrict__ maxbits) {
+    __shared__ float w[ST_TILE + 48];
+    __shared__ float wm[ST_T / 64];
     const int b = blockIdx.x;
     const int p = find_preset(st_begin, n_presets, b);
     const PresetRt& r = rt[p];
-    const int64_t t0 = (int64_t)(b - st_begin[p]) * ST_TILE;
     const float* y = ybuf + r.y_off;
+    const StereoTile st = stereo_stage(r, y, (int64_t)(b - st_begin[p]) * ST_TILE, w);
+    const int cnt = (int)(st.t1 - st.t0);
     float m = 0.f;
-    for (int u = threadIdx.x; u < ST_TILE; u += ST_T) {
-        const int64_t t = t0 + u;
-        if (t >= r.out_n) break;
-        float L, R;
-        stereo_pair(r, y, t, L, R);
-        m = fmaxf(m, fmaxf(fabsf(L), fabsf(R)));
+    for (int u = threadIdx.x; u < cnt; u += ST_T) {
+        // max|L| over all frames equals max|y| (L is a rotation of y): read y directly
+        m = fmaxf(m, fabsf(y[st.t0 + u]));
+        if (r.stereo_fir) {
+            float acc = 0.f;
+#pragma unroll
+            for (int k = 0; k < 25; ++k) acc = fmaf(r.bess[k], w[u + 2 * k], acc);
+            m = fmaxf(m, fabsf(acc));
+        }
     }
     for (int off = 32; off > 0; off >>= 1) m = fmaxf(m, __shfl_xor(m, off));
-    __shared__ float wm[ST_T / 64];
     if ((threadIdx.x & 63) == 0) wm[threadIdx.x >> 6] = m;
     __syncthreads();
     if (threadIdx.x == 0) {
         float v = wm[0];
-        for (int w = 1; w < ST_T / 64; ++w) v = fmaxf(v, wm[w]);
+        for (int k = 1; k < ST_T / 64; ++k) v = fmaxf(v, wm[k]);
         atomicMax(maxbits + p, __float_as_uint(v));
     }
 }
@@ -293,22 +335,22 @@ MSG_DEV float sat(float v, float d, float inv_td) { return d > 0.f ? tanhf(v * d
 __global__ void __launch_bounds__(ST_T)
 k_stereo_out(const PresetRt* __restrict__ rt, const int32_t* __restrict__ st_begin, int n_presets,
              const float* __restrict__ ybuf, const unsigned* __restrict__ maxbits, float* __restrict__ out) {
+    __shared__ float w[ST_TILE + 48];
     const int b = blockIdx.x;
     const int p = find_preset(st_begin, n_presets, b);
     const PresetRt& r = rt[p];
-    const int64_t t0 = (int64_t)(b - st_begin[p]) * ST_TILE;
     const float* y = ybuf + r.y_off;
+    const StereoTile st = stereo_stage(r, y, (int64_t)(b - st_begin[p]) * ST_TILE, w);
     const float d = r.drive;
     const float inv_td = d > 0.f ? 1.0f / tanhf(d) : 1.f;
     const float M = __uint_as_float(maxbits[p]);
     const float mc = sat(M, d, inv_td);
     const float scale = mc > 0.f ? r.peak / mc : 1.f;
-    float2* o = reinterpret_cast<float2*>(out) + r.out_off;
-    for (int u = threadIdx.x; u < ST_TILE; u += ST_T) {
-        const int64_t t = t0 + u;
-        if (t >= r.out_n) break;
+    float2* o = reinterpret_cast<float2*>(out) + r.out_off + st.t0;
+    const int cnt = (int)(st.t1 - st.t0);
+    for (int u = threadIdx.x; u < cnt; u += ST_T) {
         float L, R;
-        stereo_pair(r, y, t, L, R);
-        o[t] = make_float2(sat(L, d, inv_td) * scale, sat(R, d, inv_td) * scale);
+        stereo_at(r, y, w, st, u, L, R);
+        o[u] = make_float2(sat(L, d, inv_td) * scale, sat(R, d, inv_td) * scale);
     }
 }

@@ -21,9 +21,9 @@ k_ir_spec(const int64_t* __restrict__ jobs /* [ir_off, ir_len, plan, out_off] */
     const int64_t irl = j[1];
     for (int u = threadIdx.x; u < rp.n; u += T) rx_set(lds, rp, u, u < irl ? (float)ir[u] : 0.f);
     const TwLds tw = stage_twiddles<T>(lds + rp.lds_c, rp.c);
-    rfft_lds<T, MAXM>(lds, rp, tw);
+    rtransform<T, MAXM, RSET_PO2>(lds, rp, tw, false);
     float2* dst = ir_spec + j[3];
-    for (int k = threadIdx.x; k <= rp.n / 2; k += T) dst[k] = lds[k];
+    for (int k = threadIdx.x; k <= rp.n / 2; k += T) dst[k] = cx(lds, k);
 }
 
 // One workgroup per (preset, partition q): build h in LDS (ER taps scattered,
@@ -44,49 +44,54 @@ k_fir_h(const PresetRt* __restrict__ rt, const int32_t* __restrict__ hblk_begin,
     const RealPlan& rp = fir_plans[fir_plan_of[p]];
     const int N = r.fir_N, P = r.fir_P;
     const TwLds tw = stage_twiddles<T>(lds + rp.lds_c, rp.c);
-    float* h = reinterpret_cast<float*>(lds);   // N real samples (N even)
     const int irl = r.ir_len;
+    const bool conv = r.n_taps > 0 && irl > 0;   // h = e * ir through the IR spectrum
     if (r.n_taps > 0) {
-        for (int u = threadIdx.x; u < N; u += T) h[u] = u == 0 ? 1.f : 0.f;
+        for (int u = threadIdx.x; u < N; u += T) rx_set(lds, rp, u, u == 0 ? 1.f : 0.f);
         __syncthreads();
         for (int k = threadIdx.x; k < r.n_taps; k += T) {
             const int64_t o = er_off[r.er_base + k];
             if (o <= 0 || o >= r.out_n || o >= N) continue;   // MS:418-420
-            atomicAdd(h + o, (float)er_gain[r.er_base + k]);
-        }
-        __syncthreads();
-        if (irl > 0) {   // h = e * ir via the IR spectrum (linear: M <= N checked on the host)
-            rfft_lds<T, MAXM>(lds, rp, tw);
-            const float2* S = ir_spec + r.irs_off;
-            for (int k = threadIdx.x; k <= N / 2; k += T) lds[k] = cmul(lds[k], S[k]);
-            __syncthreads();
-            irfft_lds<T, MAXM>(lds, rp, tw);
+            float* h = reinterpret_cast<float*>(lds);
+            atomicAdd(h + 2 * lp((int)o >> 1) + ((int)o & 1), (float)er_gain[r.er_base + k]);
         }
     } else {
         const double* ir = ir_bank + r.ir_off;
-        for (int u = threadIdx.x; u < N; u += T) h[u] = u < irl ? (float)ir[u] : 0.f;
-        __syncthreads();
-    }
-    // cut partition q into place
-    constexpr int PER = (2 * MAXM + T - 1) / T;
-    float v[PER];
-#pragma unroll
-    for (int i = 0; i < PER; ++i) {
-        const int u = (int)threadIdx.x + i * T;
-        const int src = q * P + u;
-        v[i] = (u < P && src < N) ? h[src] : 0.f;
+        for (int u = threadIdx.x; u < N; u += T) rx_set(lds, rp, u, u < irl ? (float)ir[u] : 0.f);
     }
     __syncthreads();
+    // transform sequence: conv ? [F, I, F] : [F]; one rtransform call site
+    const int nsteps = conv ? 3 : 1;
+    for (int step = 0; step < nsteps; ++step) {
+        const int Nn = opaque(N);
+        const int tid = otid();
+        if (step == nsteps - 1) {   // cut partition q of h into place, zero-padded to N
+            constexpr int PER = (2 * MAXM + T - 1) / T;
+            float v[PER];
 #pragma unroll
-    for (int i = 0; i < PER; ++i) {
-        const int u = (int)threadIdx.x + i * T;
-        if (u < N) h[u] = v[i];
+            for (int i = 0; i < PER; ++i) {
+                const int u = tid + i * T;
+                const int src = q * P + u;
+                v[i] = (u < P && src < Nn) ? rx_get(lds, rp, src) : 0.f;
+            }
+            __syncthreads();
+#pragma unroll
+            for (int i = 0; i < PER; ++i) {
+                const int u = tid + i * T;
+                if (u < Nn) rx_set(lds, rp, u, v[i]);
+            }
+            __syncthreads();
+        }
+        rtransform<T, MAXM, RSET_PO2>(lds, rp, tw, step == 1);
+        if (step == 0 && conv) {
+            const float2* S = ir_spec + r.irs_off;
+            for (int k = tid; k <= N / 2; k += T) cx(lds, k) = cmul(cx(lds, k), S[k]);
+            __syncthreads();
+        }
     }
-    __syncthreads();
-    rfft_lds<T, MAXM>(lds, rp, tw);
     const int K = N / 2 + 1;
     float2* dst = hspec + r.h_off + (int64_t)q * K;
-    for (int k = threadIdx.x; k < K; k += T) dst[k] = lds[k];
+    for (int k = threadIdx.x; k < K; k += T) dst[k] = cx(lds, k);
 }
 
 // Partitioned FFT overlap-save: a block outputs B samples; Q forward FFTs
@@ -111,29 +116,44 @@ k_fir(const PresetRt* __restrict__ rt, const int32_t* __restrict__ fblk_begin, i
     float2 acc[PER];
 #pragma unroll
     for (int u = 0; u < PER; ++u) acc[u] = make_float2(0.f, 0.f);
-    for (int q = 0; q < Q; ++q) {
-        const int64_t s0 = t0 - (int64_t)q * P - (P - 1);
-        for (int u = threadIdx.x; u < N; u += T) {
-            const int64_t s = s0 + u;
-            rx_set(lds, rp, u, (s >= 0 && s < n) ? x[s] : 0.f);
+    for (int step = 0; step <= Q; ++step) {   // Q forward transforms, then the inverse
+        const int Nn = opaque(N);
+        const int tid = otid();
+        if (step < Q) {
+            const int64_t s0 = t0 - (int64_t)step * P - (P - 1);
+            for (int u0 = 0; u0 < Nn; u0 += 8 * T) {   // 8 loads in flight per thread
+                float v[8];
+#pragma unroll
+                for (int i = 0; i < 8; ++i) {
+                    const int u = u0 + i * T + tid;
+                    const int64_t s = s0 + u;
+                    v[i] = (u < Nn && s >= 0 && s < n) ? x[s] : 0.f;
+                }
+#pragma unroll
+                for (int i = 0; i < 8; ++i) {
+                    const int u = u0 + i * T + tid;
+                    if (u < Nn) rx_set(lds, rp, u, v[i]);
+                }
+            }
+        } else {
+#pragma unroll
+            for (int u = 0; u < PER; ++u) {
+                const int k = tid + u * T;
+                if (k < K) cx(lds, k) = acc[u];
+            }
         }
         __syncthreads();
-        rfft_lds<T, MAXM>(lds, rp, tw);
-        const float2* H = hspec + r.h_off + (int64_t)q * K;
+        rtransform<T, MAXM, RSET_PO2>(lds, rp, tw, step == Q);
+        if (step < Q) {
+            const float2* H = hspec + r.h_off + (int64_t)step * K;
 #pragma unroll
-        for (int u = 0; u < PER; ++u) {
-            const int k = (int)threadIdx.x + u * T;
-            if (k < K) acc[u] = cadd(acc[u], cmul(lds[k], H[k]));
+            for (int u = 0; u < PER; ++u) {
+                const int k = tid + u * T;
+                if (k < K) acc[u] = cadd(acc[u], cmul(cx(lds, k), H[k]));
+            }
+            __syncthreads();
         }
-        __syncthreads();
     }
-#pragma unroll
-    for (int u = 0; u < PER; ++u) {
-        const int k = (int)threadIdx.x + u * T;
-        if (k < K) lds[k] = acc[u];
-    }
-    __syncthreads();
-    irfft_lds<T, MAXM>(lds, rp, tw);
     float* y = y_out + r.y_off;
     for (int u = threadIdx.x + (P - 1); u < N; u += T) {
         const int64_t t = t0 + (u - (P - 1));

@@ -25,20 +25,21 @@ MSG_DEV float lowpass_w(int k, int n, int sr, double cutoff, double roll) {
 template <int T, int MAXK, class Src>
 MSG_DEV void spectral_gather(float2* buf, int K, Src src) {
     constexpr int PER = (MAXK + T - 1) / T;
+    const int tid = otid();
     float2 y[PER];
 #pragma unroll
     for (int b = 0; b < PER; ++b) {
-        const int k = (int)threadIdx.x + b * T;
+        const int k = tid + b * T;
         y[b] = make_float2(0.f, 0.f);
         if (k < K) {
             const double xs = src(k);
             if (xs >= 0.0 && xs <= (double)(K - 1)) {
                 const int j = (int)xs;
                 if (j >= K - 1) {
-                    y[b] = buf[K - 1];
+                    y[b] = cx(buf, K - 1);
                 } else {
                     const float fr = (float)(xs - (double)j);
-                    const float2 a = buf[j], c = buf[j + 1];
+                    const float2 a = cx(buf, j), c = cx(buf, j + 1);
                     y[b] = make_float2((c.x - a.x) * fr + a.x, (c.y - a.y) * fr + a.y);
                 }
             }
@@ -47,8 +48,8 @@ MSG_DEV void spectral_gather(float2* buf, int K, Src src) {
     __syncthreads();
 #pragma unroll
     for (int b = 0; b < PER; ++b) {
-        const int k = (int)threadIdx.x + b * T;
-        if (k < K) buf[k] = y[b];
+        const int k = tid + b * T;
+        if (k < K) cx(buf, k) = y[b];
     }
     __syncthreads();
 }
@@ -57,8 +58,8 @@ MSG_DEV void spectral_gather(float2* buf, int K, Src src) {
 // reproduce that between fused spectral stages.
 MSG_DEV void drop_edge_imag(float2* buf, const RealPlan& rp) {
     if (threadIdx.x == 0) {
-        buf[0].y = 0.f;
-        if (rp.even) buf[rp.n / 2].y = 0.f;
+        cx(buf, 0).y = 0.f;
+        if (rp.even) cx(buf, rp.n / 2).y = 0.f;
     }
     __syncthreads();
 }
@@ -86,75 +87,90 @@ k_spectral(const msg_preset* __restrict__ presets, const msg_event* __restrict__
     }
     const RealPlan& rp = plans[er.plan];
     const int K = n / 2 + 1;
-    for (int j = threadIdx.x; j < n; j += T) rx_set(lds, rp, j, micro[j]);
+    for (int j0 = 0; j0 < n; j0 += 8 * T) {   // 8 loads in flight per thread
+        float v[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int j = j0 + i * T + (int)threadIdx.x;
+            v[i] = j < n ? micro[j] : 0.f;
+        }
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int j = j0 + i * T + (int)threadIdx.x;
+            if (j < n) rx_set(lds, rp, j, v[i]);
+        }
+    }
     const TwLds tw = stage_twiddles<T>(lds + rp.lds_c, rp.c);   // includes the barrier
 
-    if (ops & (SPEC_TILT_NOISE | SPEC_TILT_SKEW)) {
-        // tilted_noise (MS:224-233): W *= (f/f1)^alpha with f[0] := f[1]
-        rfft_lds<T, MAXM>(lds, rp, tw);
-        const double val = 1.0 / ((double)n * (1.0 / (double)er.gen_sr));
-        for (int k = threadIdx.x; k < K; k += T) {
-            double sh = 1.0;
-            if (K > 1 && k > 0) sh = pow(((double)k * val) / fmax(1e-12, val), er.tilt_alpha);
-            lds[k] = cscale(lds[k], (float)sh);
-        }
-        __syncthreads();
-        irfft_lds<T, MAXM>(lds, rp, tw);
-        // envelope, skew, fade (MS:246-255, 265-268)
-        const int fade = (int)(0.01 * n) > 8 ? (int)(0.01 * n) : 8;
-        const double inv_sr = 1.0 / (double)er.gen_sr;
-        if (ops & SPEC_TILT_SKEW) {
-            // d = diff(max(0, w), prepend=w[0]): needs neighbours -> via registers
-            constexpr int PER = (2 * MAXM + T - 1) / T;
-            float d[PER];
-#pragma unroll
-            for (int b = 0; b < PER; ++b) {
-                const int j = (int)threadIdx.x + b * T;
-                d[b] = 0.f;
-                if (j < n && j > 0) d[b] = fmaxf(0.f, rx_get(lds, rp, j)) - fmaxf(0.f, rx_get(lds, rp, j - 1));
+    // Transform sequence: [tilt F, tilt I] for noise/skew generators, then
+    // [chain F, chain I] for the band-limit / warp / stretch chain.  One call
+    // site of rtransform keeps one copy of the FFT engine in the kernel.
+    const bool tilt = (ops & (SPEC_TILT_NOISE | SPEC_TILT_SKEW)) != 0;
+    const bool chain = (ops & (SPEC_LOWPASS | SPEC_STRETCH | SPEC_WARP)) != 0;
+    const int first = tilt ? 0 : 2;
+    const int last = chain ? 4 : 2;
+    for (int step = first; step < last; ++step) {
+        const bool inv = (step & 1) != 0;
+        const int tid = otid();
+        rtransform<T, MAXM, RSET_ALL>(lds, rp, tw, inv);
+        if (step == 0) {
+            // tilted_noise (MS:224-233): W *= (f/f1)^alpha with f[0] := f[1]
+            const double val = 1.0 / ((double)n * (1.0 / (double)er.gen_sr));
+            for (int k = tid; k < K; k += T) {
+                double sh = 1.0;
+                if (K > 1 && k > 0) sh = pow(((double)k * val) / fmax(1e-12, val), er.tilt_alpha);
+                cx(lds, k) = cscale(cx(lds, k), (float)sh);
             }
             __syncthreads();
+        } else if (step == 1) {
+            // envelope, skew, fade (MS:246-255, 265-268); the result is micro_last
+            const int fade = (int)(0.01 * n) > 8 ? (int)(0.01 * n) : 8;
+            const double inv_sr = 1.0 / (double)er.gen_sr;
+            if (ops & SPEC_TILT_SKEW) {
+                // d = diff(max(0, w), prepend=w[0]): needs neighbours -> via registers
+                constexpr int PER = (2 * MAXM + T - 1) / T;
+                float d[PER];
 #pragma unroll
-            for (int b = 0; b < PER; ++b) {
-                const int j = (int)threadIdx.x + b * T;
-                if (j < n) {
+                for (int b = 0; b < PER; ++b) {
+                    const int j = tid + b * T;
+                    d[b] = 0.f;
+                    if (j < n && j > 0) d[b] = fmaxf(0.f, rx_get(lds, rp, j)) - fmaxf(0.f, rx_get(lds, rp, j - 1));
+                }
+                __syncthreads();
+#pragma unroll
+                for (int b = 0; b < PER; ++b) {
+                    const int j = tid + b * T;
+                    if (j < n) {
+                        const float env = (float)exp(-((double)j * inv_sr) / er.env_tau);
+                        rx_set(lds, rp, j, d[b] * env * fade_w(j, n, fade));
+                    }
+                }
+            } else {
+                for (int j = tid; j < n; j += T) {
                     const float env = (float)exp(-((double)j * inv_sr) / er.env_tau);
-                    rx_set(lds, rp, j, d[b] * env * fade_w(j, n, fade));
+                    rx_set(lds, rp, j, rx_get(lds, rp, j) * env * fade_w(j, n, fade));
                 }
             }
-        } else {
-            for (int j = threadIdx.x; j < n; j += T) {
-                const float env = (float)exp(-((double)j * inv_sr) / er.env_tau);
-                rx_set(lds, rp, j, rx_get(lds, rp, j) * env * fade_w(j, n, fade));
+            __syncthreads();
+            for (int j = tid; j < n; j += T) micro[j] = rx_get(lds, rp, j);
+        } else if (step == 2) {
+            if (ops & SPEC_LOWPASS) {
+                for (int k = tid; k < K; k += T)
+                    cx(lds, k) = cscale(cx(lds, k), lowpass_w(k, n, er.gen_sr, er.cutoff_gen, er.roll));
+                __syncthreads();
+            }
+            if (ops & SPEC_WARP) {   // fft_warp_power (MS:103-115)
+                drop_edge_imag(lds, rp);
+                const double kmax = fmax(1.0, (double)(K - 1));
+                const double ip = 1.0 / fmax(1e-6, er.warp_power);
+                spectral_gather<T, MAXM + 1>(lds, K, [&](int k) { return pow((double)k / kmax, ip) * kmax; });
+            }
+            if (ops & SPEC_STRETCH) {   // fft_partial_stretch (MS:117-128)
+                drop_edge_imag(lds, rp);
+                const double f = fmax(1e-12, er.stretch);
+                spectral_gather<T, MAXM + 1>(lds, K, [&](int k) { return (double)k / f; });
             }
         }
-        __syncthreads();
-        for (int j = threadIdx.x; j < n; j += T) micro[j] = rx_get(lds, rp, j);
-        if (!(ops & (SPEC_LOWPASS | SPEC_STRETCH | SPEC_WARP))) {
-            for (int j = threadIdx.x; j < n; j += T) grain[j] = rx_get(lds, rp, j);
-            return;
-        }
-        __syncthreads();
     }
-
-    rfft_lds<T, MAXM>(lds, rp, tw);
-    if (ops & SPEC_LOWPASS) {
-        for (int k = threadIdx.x; k < K; k += T)
-            lds[k] = cscale(lds[k], lowpass_w(k, n, er.gen_sr, er.cutoff_gen, er.roll));
-        __syncthreads();
-    }
-    if (ops & SPEC_WARP) {   // fft_warp_power (MS:103-115)
-        drop_edge_imag(lds, rp);
-        const double kmax = fmax(1.0, (double)(K - 1));
-        const double ip = 1.0 / fmax(1e-6, er.warp_power);
-        spectral_gather<T, MAXM + 1>(lds, K, [&](int k) { return pow((double)k / kmax, ip) * kmax; });
-    }
-    if (ops & SPEC_STRETCH) {   // fft_partial_stretch (MS:117-128)
-        drop_edge_imag(lds, rp);
-        const double f = fmax(1e-12, er.stretch);
-        spectral_gather<T, MAXM + 1>(lds, K, [&](int k) { return (double)k / f; });
-    }
-    irfft_lds<T, MAXM>(lds, rp, tw);
     for (int j = threadIdx.x; j < n; j += T) grain[j] = rx_get(lds, rp, j);
 }
-

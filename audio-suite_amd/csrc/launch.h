@@ -6,10 +6,10 @@
 #include "rt.h"
 
 constexpr int LDS_MAX = 163840;                              // 160 KiB per CU
-constexpr int SPEC_T_BIG = 1024, SPEC_M_BIG = 20480;          // up to 160 KiB LDS
+constexpr int SPEC_T_BIG = 512, SPEC_M_BIG = 20480;           // up to 160 KiB LDS
 constexpr int SPEC_T_SMALL = 256, SPEC_M_SMALL = 8192;        // up to 64 KiB LDS
 constexpr int SPEC_SMALL_BYTES = 65536;
-constexpr int FIR_T = 1024, FIR_M = 16384;                    // N <= 32768 real
+constexpr int FIR_T = 512, FIR_M = 16384;                     // N <= 32768 real
 constexpr int FIR_NMAX = 32768;
 
 void spectral_init_attrs();

@@ -163,7 +163,7 @@ static int real_plan(PlanStore& ps, int n, std::string& why) {
     rp.even = (n % 2 == 0);
     const int m = rp.even ? n / 2 : n;
     if (!make_fftdesc(ps, m, rp.c, why)) return -1;
-    rp.lds_c = std::max(rp.even ? m + 1 : m, rp.c.size);
+    rp.lds_c = lds_phys(std::max(rp.even ? m + 1 : m, rp.c.size));
     rp.lds_bytes = (rp.lds_c + TW_LO + rp.c.tw_hi_n) * 8;
     if (rp.even) {
         std::vector<float> t(2 * (size_t)(m + 1));
