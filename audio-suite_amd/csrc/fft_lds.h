@@ -43,7 +43,10 @@ struct RealPlan {
     int32_t lds_c;        // physical complex slots of LDS for data (padded, lds_phys)
     int32_t lds_bytes;    // data + staged twiddle tables
     FftDesc c;
-    const float2* rtw;    // even: exp(-2 pi i k / n), k <= n/2
+    int32_t rt_hi_n;      // even: entries of rt1 = ceil((n/2+1) / 128)
+    int32_t pad2;
+    const float2* rt0;    // even: exp(-2 pi i j / n), j < 128
+    const float2* rt1;    // even: exp(-2 pi i 128 j / n), j < rt_hi_n
 };
 
 MSG_DEV float2 cmul(float2 a, float2 b) { return make_float2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x); }
@@ -155,8 +158,11 @@ MSG_DEV int lp(int i) { return i ^ ((i >> 4) & 15); }
 MSG_HD constexpr int lds_phys(int logical) { return (logical + 15) & ~15; }
 
 // Staged twiddle tables in LDS.
-struct TwLds { const float2* t0; const float2* t1; };
+// t0/t1: FFT twiddles exp(-2 pi i j/size); r0/r1: real-FFT post-twiddles
+// exp(-2 pi i k/n), both as two-level tables: w(i) = hi[i>>7] * lo[i&127].
+struct TwLds { const float2* t0; const float2* t1; const float2* r0; const float2* r1; };
 MSG_DEV float2 tw_at(const TwLds& tw, int i) { return cmul(tw.t1[i >> 7], tw.t0[i & (TW_LO - 1)]); }
+MSG_DEV float2 rtw_at(const TwLds& tw, int k) { return cmul(tw.r1[k >> 7], tw.r0[k & (TW_LO - 1)]); }
 
 // floor(j / d) for 0 <= j < 2^24 via a float reciprocal plus one correction.
 MSG_DEV int fdiv(int j, int d, float inv_d) {
@@ -277,11 +283,17 @@ MSG_DEV void stockham_fwd(float2* buf, int size, const int32_t* rad, int nrad, c
 
 // Copy the plan's twiddle tables into LDS at `dst` (after the data region).
 template <int T>
-MSG_DEV TwLds stage_twiddles(float2* dst, const FftDesc& d) {
+MSG_DEV TwLds stage_twiddles(float2* dst, const RealPlan& rp) {
+    const FftDesc& d = rp.c;
+    float2* r0 = dst + TW_LO + d.tw_hi_n;
     for (int i = threadIdx.x; i < TW_LO; i += T) dst[i] = d.tw0[i];
     for (int i = threadIdx.x; i < d.tw_hi_n; i += T) dst[TW_LO + i] = d.tw1[i];
+    if (rp.even) {
+        for (int i = threadIdx.x; i < TW_LO; i += T) r0[i] = rp.rt0[i];
+        for (int i = threadIdx.x; i < rp.rt_hi_n; i += T) r0[TW_LO + i] = rp.rt1[i];
+    }
     __syncthreads();
-    return TwLds{dst, dst + TW_LO};
+    return TwLds{dst, dst + TW_LO, r0, r0 + TW_LO};
 }
 
 // Forward complex DFT of length d.m in buf (Bluestein-aware, exp(-2 pi i jk/m)).
@@ -344,9 +356,9 @@ MSG_DEV void rtransform(float2* buf, const RealPlan& rp, const TwLds& tw, bool i
                 }
                 const float2 yk = cx(buf, k), ym = cx(buf, m - k);
                 const float2 e1 = cscale(cadd(yk, cconj(ym)), 0.5f);
-                const float2 o1 = cscale(cmulc(csub(yk, cconj(ym)), rp.rtw[k]), 0.5f);
+                const float2 o1 = cscale(cmulc(csub(yk, cconj(ym)), rtw_at(tw, k)), 0.5f);
                 const float2 e2 = cscale(cadd(ym, cconj(yk)), 0.5f);
-                const float2 o2 = cscale(cmulc(csub(ym, cconj(yk)), rp.rtw[m - k]), 0.5f);
+                const float2 o2 = cscale(cmulc(csub(ym, cconj(yk)), rtw_at(tw, m - k)), 0.5f);
                 cx(buf, k) = make_float2(e1.x - o1.y, -(e1.y + o1.x));
                 cx(buf, m - k) = make_float2(e2.x - o2.y, -(e2.y + o2.x));
             }
@@ -379,8 +391,8 @@ MSG_DEV void rtransform(float2* buf, const RealPlan& rp, const TwLds& tw, bool i
             const float2 e2 = cscale(cadd(zm, cconj(zk)), 0.5f);
             const float2 d2 = csub(zm, cconj(zk));
             const float2 o2 = make_float2(0.5f * d2.y, -0.5f * d2.x);
-            cx(buf, k) = cadd(e1, cmul(rp.rtw[k], o1));
-            cx(buf, m - k) = cadd(e2, cmul(rp.rtw[m - k], o2));
+            cx(buf, k) = cadd(e1, cmul(rtw_at(tw, k), o1));
+            cx(buf, m - k) = cadd(e2, cmul(rtw_at(tw, m - k), o2));
         }
         __syncthreads();
     } else {

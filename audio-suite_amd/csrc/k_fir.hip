@@ -32,3 +32,34 @@ hipError_t launch_fir(unsigned grid, int lds_bytes, hipStream_t s, const PresetR
                        fir_plans, fir_plan_of, hspec, x_in, y_out);
     return hipGetLastError();
 }
+
+// ---- FFT engine micro-benchmark (msg_bench_fft): reps x (forward + inverse)
+// real transforms of length n per block, LDS-resident, no HBM traffic.
+template <int T, int MAXM, int RSET>
+__global__ void __launch_bounds__(T) k_fft_bench(const RealPlan* __restrict__ plans, int plan, int reps,
+                                                  float* __restrict__ sink) {
+    extern __shared__ __attribute__((aligned(16))) float2 lds[];
+    const RealPlan& rp = plans[plan];
+    for (int u = threadIdx.x; u < rp.n; u += T) rx_set(lds, rp, u, (float)((u * 7919) % 113) * 1e-2f);
+    const TwLds tw = stage_twiddles<T>(lds + rp.lds_c, rp);
+    for (int r = 0; r < 2 * reps; ++r) rtransform<T, MAXM, RSET>(lds, rp, tw, (r & 1) != 0);
+    if (threadIdx.x == 0) sink[blockIdx.x] = rx_get(lds, rp, 1);
+}
+
+void fft_bench_init_attrs() {
+    (void)hipFuncSetAttribute((const void*)k_fft_bench<FIR_T, FIR_M, RSET_PO2>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
+    (void)hipFuncSetAttribute((const void*)k_fft_bench<SPEC_T_BIG, SPEC_M_BIG, RSET_ALL>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
+}
+
+hipError_t launch_fft_bench(bool po2, unsigned grid, int lds_bytes, hipStream_t s, const RealPlan* plans, int plan,
+                            int reps, float* sink) {
+    if (po2)
+        hipLaunchKernelGGL((k_fft_bench<FIR_T, FIR_M, RSET_PO2>), dim3(grid), dim3(FIR_T), lds_bytes, s, plans, plan,
+                           reps, sink);
+    else
+        hipLaunchKernelGGL((k_fft_bench<SPEC_T_BIG, SPEC_M_BIG, RSET_ALL>), dim3(grid), dim3(SPEC_T_BIG), lds_bytes,
+                           s, plans, plan, reps, sink);
+    return hipGetLastError();
+}

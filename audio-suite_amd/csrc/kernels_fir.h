@@ -20,7 +20,7 @@ k_ir_spec(const int64_t* __restrict__ jobs /* [ir_off, ir_len, plan, out_off] */
     const double* ir = ir_bank + j[0];
     const int64_t irl = j[1];
     for (int u = threadIdx.x; u < rp.n; u += T) rx_set(lds, rp, u, u < irl ? (float)ir[u] : 0.f);
-    const TwLds tw = stage_twiddles<T>(lds + rp.lds_c, rp.c);
+    const TwLds tw = stage_twiddles<T>(lds + rp.lds_c, rp);
     rtransform<T, MAXM, RSET_PO2>(lds, rp, tw, false);
     float2* dst = ir_spec + j[3];
     for (int k = threadIdx.x; k <= rp.n / 2; k += T) dst[k] = cx(lds, k);
@@ -43,7 +43,7 @@ k_fir_h(const PresetRt* __restrict__ rt, const int32_t* __restrict__ hblk_begin,
     const int q = b - r.h_block_begin;
     const RealPlan& rp = fir_plans[fir_plan_of[p]];
     const int N = r.fir_N, P = r.fir_P;
-    const TwLds tw = stage_twiddles<T>(lds + rp.lds_c, rp.c);
+    const TwLds tw = stage_twiddles<T>(lds + rp.lds_c, rp);
     const int irl = r.ir_len;
     const bool conv = r.n_taps > 0 && irl > 0;   // h = e * ir through the IR spectrum
     if (r.n_taps > 0) {
@@ -94,6 +94,43 @@ k_fir_h(const PresetRt* __restrict__ rt, const int32_t* __restrict__ hblk_begin,
     for (int k = threadIdx.x; k < K; k += T) dst[k] = cx(lds, k);
 }
 
+// x[s0 + u] for u < N (zero outside [0, n)) into the LDS real view, read as
+// 16-byte aligned float4 quads (x is 16-byte aligned: y_off % 4 == 0).
+template <int T>
+MSG_DEV void load_segment(float2* lds, const RealPlan& rp, const float* __restrict__ x, int64_t n, int64_t s0,
+                          int N, int tid) {
+    const int64_t a0 = (s0 >> 2) << 2;
+    const int shift = (int)(s0 - a0);
+    const int nq = (N + shift + 3) >> 2;
+    const float4* xq = reinterpret_cast<const float4*>(x);
+    for (int v0 = 0; v0 < nq; v0 += 8 * T) {
+        float4 q[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int v = v0 + i * T + tid;
+            const int64_t a = a0 + 4 * (int64_t)v;
+            if (v < nq && a >= 0 && a + 3 < n) {
+                q[i] = xq[a >> 2];
+            } else {
+                q[i].x = (v < nq && a >= 0 && a < n) ? x[a] : 0.f;
+                q[i].y = (v < nq && a + 1 >= 0 && a + 1 < n) ? x[a + 1] : 0.f;
+                q[i].z = (v < nq && a + 2 >= 0 && a + 2 < n) ? x[a + 2] : 0.f;
+                q[i].w = (v < nq && a + 3 >= 0 && a + 3 < n) ? x[a + 3] : 0.f;
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int v = v0 + i * T + tid;
+            if (v >= nq) continue;
+            const int u = 4 * v - shift;
+            const float e[4] = {q[i].x, q[i].y, q[i].z, q[i].w};
+#pragma unroll
+            for (int c = 0; c < 4; ++c)
+                if (u + c >= 0 && u + c < N) rx_set(lds, rp, u + c, e[c]);
+        }
+    }
+}
+
 // Partitioned FFT overlap-save: a block outputs B samples; Q forward FFTs
 // accumulate X_q * H_q in registers, then one inverse FFT.
 template <int T, int MAXM>
@@ -111,7 +148,7 @@ k_fir(const PresetRt* __restrict__ rt, const int32_t* __restrict__ fblk_begin, i
     const int64_t t0 = (int64_t)(b - r.fir_block_begin) * B;
     const float* x = x_in + r.y_off;
     const int K = N / 2 + 1;
-    const TwLds tw = stage_twiddles<T>(lds + rp.lds_c, rp.c);
+    const TwLds tw = stage_twiddles<T>(lds + rp.lds_c, rp);
     constexpr int PER = (MAXM + 1 + T - 1) / T;
     float2 acc[PER];
 #pragma unroll
@@ -121,20 +158,7 @@ k_fir(const PresetRt* __restrict__ rt, const int32_t* __restrict__ fblk_begin, i
         const int tid = otid();
         if (step < Q) {
             const int64_t s0 = t0 - (int64_t)step * P - (P - 1);
-            for (int u0 = 0; u0 < Nn; u0 += 8 * T) {   // 8 loads in flight per thread
-                float v[8];
-#pragma unroll
-                for (int i = 0; i < 8; ++i) {
-                    const int u = u0 + i * T + tid;
-                    const int64_t s = s0 + u;
-                    v[i] = (u < Nn && s >= 0 && s < n) ? x[s] : 0.f;
-                }
-#pragma unroll
-                for (int i = 0; i < 8; ++i) {
-                    const int u = u0 + i * T + tid;
-                    if (u < Nn) rx_set(lds, rp, u, v[i]);
-                }
-            }
+            load_segment<T>(lds, rp, x, n, s0, Nn, tid);
         } else {
 #pragma unroll
             for (int u = 0; u < PER; ++u) {

@@ -100,7 +100,7 @@ k_spectral(const msg_preset* __restrict__ presets, const msg_event* __restrict__
             if (j < n) rx_set(lds, rp, j, v[i]);
         }
     }
-    const TwLds tw = stage_twiddles<T>(lds + rp.lds_c, rp.c);   // includes the barrier
+    const TwLds tw = stage_twiddles<T>(lds + rp.lds_c, rp);   // includes the barrier
 
     // Transform sequence: [tilt F, tilt I] for noise/skew generators, then
     // [chain F, chain I] for the band-limit / warp / stretch chain.  One call

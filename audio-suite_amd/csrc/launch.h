@@ -28,3 +28,7 @@ hipError_t launch_fir_h(unsigned grid, int lds_bytes, hipStream_t s, const Prese
 hipError_t launch_fir(unsigned grid, int lds_bytes, hipStream_t s, const PresetRt* rt, const int32_t* fblk_begin,
                       int n_presets, const RealPlan* fir_plans, const int32_t* fir_plan_of,
                       const float2* hspec, const float* x_in, float* y_out);
+
+void fft_bench_init_attrs();
+hipError_t launch_fft_bench(bool po2, unsigned grid, int lds_bytes, hipStream_t s, const RealPlan* plans, int plan,
+                            int reps, float* sink);

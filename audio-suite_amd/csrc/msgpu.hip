@@ -164,16 +164,15 @@ static int real_plan(PlanStore& ps, int n, std::string& why) {
     const int m = rp.even ? n / 2 : n;
     if (!make_fftdesc(ps, m, rp.c, why)) return -1;
     rp.lds_c = lds_phys(std::max(rp.even ? m + 1 : m, rp.c.size));
-    rp.lds_bytes = (rp.lds_c + TW_LO + rp.c.tw_hi_n) * 8;
     if (rp.even) {
-        std::vector<float> t(2 * (size_t)(m + 1));
-        for (int k = 0; k <= m; ++k) {
-            const long double a = -2.0L * 3.14159265358979323846264338327950288L * k / (long double)n;
-            t[2 * k] = (float)std::cos(a);
-            t[2 * k + 1] = (float)std::sin(a);
+        rp.rt_hi_n = (m + 1 + TW_LO - 1) / TW_LO;
+        if (upload(ps, fftplan::twiddles(n, TW_LO, 1), &rp.rt0) != hipSuccess ||
+            upload(ps, fftplan::twiddles(n, rp.rt_hi_n, TW_LO), &rp.rt1) != hipSuccess) {
+            why = "hip upload failed";
+            return -1;
         }
-        if (upload(ps, t, &rp.rtw) != hipSuccess) { why = "hip upload failed"; return -1; }
     }
+    rp.lds_bytes = (rp.lds_c + TW_LO + rp.c.tw_hi_n + (rp.even ? TW_LO + rp.rt_hi_n : 0)) * 8;
     const int idx = (int)ps.host.size();
     ps.host.push_back(rp);
     ps.by_n[n] = idx;
@@ -297,6 +296,7 @@ msg_ctx* msg_create(int device_ordinal) {
     for (auto& ev : ctx->ev) hipEventCreate(&ev);
     spectral_init_attrs();
     fir_init_attrs();
+    fft_bench_init_attrs();
     return ctx.release();
 }
 
@@ -438,6 +438,32 @@ int msg_rng_normal_chunked(uint64_t seed, double* out, int64_t n) {
             local -= 64;
         } while (local >= 64);
     }
+    return MSG_OK;
+}
+
+int msg_bench_fft(msg_ctx* ctx, int32_t n, int32_t reps, int32_t blocks, float* ms_out) {
+    if (!ctx || !ms_out || n < 2 || reps < 1 || blocks < 1) return MSG_E_ARG;
+    HIPCHK(ctx, hipSetDevice(ctx->device));
+    std::string why;
+    const bool po2 = (n & (n - 1)) == 0;
+    PlanStore& ps = po2 ? ctx->fir_plans : ctx->grain_plans;
+    const int pi = real_plan(ps, n, why);
+    if (pi < 0) return fail(ctx, MSG_E_DEVICE, why);
+    HIPCHK(ctx, sync_plans(ps, nullptr));
+    const RealPlan& rp = ps.host[pi];
+    if (rp.lds_bytes > LDS_MAX) return fail(ctx, MSG_E_UNSUPPORTED, "too large for LDS");
+    float* sink = nullptr;
+    HIPCHK(ctx, hipMalloc(&sink, sizeof(float) * blocks));
+    hipEvent_t a, b;
+    hipEventCreate(&a); hipEventCreate(&b);
+    HIPCHK(ctx, launch_fft_bench(po2, blocks, rp.lds_bytes, nullptr, ps.dev.p, pi, 1, sink));   // warm-up
+    hipEventRecord(a, nullptr);
+    HIPCHK(ctx, launch_fft_bench(po2, blocks, rp.lds_bytes, nullptr, ps.dev.p, pi, reps, sink));
+    hipEventRecord(b, nullptr);
+    HIPCHK(ctx, hipEventSynchronize(b));
+    hipEventElapsedTime(ms_out, a, b);
+    hipEventDestroy(a); hipEventDestroy(b);
+    hipFree(sink);
     return MSG_OK;
 }
 
@@ -651,7 +677,7 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
         stiles += (int32_t)((inf.out_n + ST_TILE - 1) / ST_TILE);
         tiles += (int32_t)((inf.out_n + OLA_TILE - 1) / OLA_TILE);
         pool += inf.pool_len;
-        ysum += inf.out_n;
+        ysum += (inf.out_n + 3) & ~int64_t(3);   // keep every mono region 16-byte aligned
         // events
         for (int k = 0; k < inf.n_events; ++k) {
             const int ei = slot_base[p] + k;

@@ -152,6 +152,10 @@ int msg_last_meta(msg_ctx* ctx, int32_t preset, double* micro, double* grain,
 int msg_set_profiling(msg_ctx* ctx, int32_t on);
 int msg_stage_times(msg_ctx* ctx, float* ms, int32_t n);
 
+/* Micro-benchmark of the LDS FFT engine: `blocks` workgroups each run `reps`
+ * forward+inverse real transforms of length n; *ms receives the device time. */
+int msg_bench_fft(msg_ctx* ctx, int32_t n, int32_t reps, int32_t blocks, float* ms);
+
 /* ---- NumPy stream primitives on the host (tests pin them against NumPy) ---- */
 /* Raw PCG64 outputs of np.random.default_rng(seed).bit_generator.random_raw(n). */
 int msg_rng_raw(uint64_t seed, uint64_t* out, int64_t n);
