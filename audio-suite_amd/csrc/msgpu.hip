@@ -64,8 +64,8 @@ struct msg_ctx {
     int device = 0;
     std::string err;
     bool profiling = false;
-    float stage_ms[8] = {0};
-    hipEvent_t ev[9] = {};
+    float stage_ms[10] = {0};
+    hipEvent_t ev[10] = {};
     // constant tables
     uint64_t* d_ki = nullptr; double* d_wi = nullptr; double* d_fi = nullptr;
     uint64_t* d_ke = nullptr; double* d_we = nullptr; double* d_fe = nullptr;
@@ -330,7 +330,7 @@ int msg_set_profiling(msg_ctx* ctx, int32_t on) {
 
 int msg_stage_times(msg_ctx* ctx, float* ms, int32_t n) {
     if (!ctx || !ms) return MSG_E_ARG;
-    for (int i = 0; i < n && i < 8; ++i) ms[i] = ctx->stage_ms[i];
+    for (int i = 0; i < n && i < 10; ++i) ms[i] = ctx->stage_ms[i];
     return MSG_OK;
 }
 
@@ -788,8 +788,10 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
         HIPCHK(ctx, launch_fir_h((unsigned)hblocks, fir_lds, s, ctx->prt.p, ctx->h_begin.p, P,
                                  ctx->fir_plans.dev.p, ctx->fir_plan_of.p, ctx->er_off.p, ctx->er_gain.p,
                                  ctx->irbank.p, ctx->irspec.p, ctx->hspec.p));
+        stage_mark(ctx, 8, s);
         HIPCHK(ctx, launch_fir((unsigned)fblocks, fir_lds, s, ctx->prt.p, ctx->fir_begin.p, P, ctx->fir_plans.dev.p,
                                ctx->fir_plan_of.p, ctx->hspec.p, ctx->mono_a.p, ctx->mono_y.p));
+        stage_mark(ctx, 9, s);
         // presets with fir_on == 0 in a mixed batch: copy a -> y
         for (int p = 0; p < P; ++p)
             if (!prt[p].fir_on)
@@ -814,6 +816,11 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
         HIPCHK(ctx, hipEventSynchronize(ctx->ev[7]));
         for (int i = 0; i < 7; ++i) hipEventElapsedTime(&ctx->stage_ms[i], ctx->ev[i], ctx->ev[i + 1]);
         hipEventElapsedTime(&ctx->stage_ms[7], ctx->ev[0], ctx->ev[7]);
+        ctx->stage_ms[8] = ctx->stage_ms[9] = 0.f;
+        if (hblocks > 0) {   // the FIR kernel alone, and the h build before it
+            hipEventElapsedTime(&ctx->stage_ms[8], ctx->ev[8], ctx->ev[9]);
+            hipEventElapsedTime(&ctx->stage_ms[9], ctx->ev[5], ctx->ev[8]);
+        }
     }
     return MSG_OK;
 }

@@ -29,6 +29,12 @@ sys.path.insert(0, REPO)
 import numpy as np  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: 8.0 TB/s spec
+# Per-launch HBM bytes of each kernel from rocprofv3 PMC passes (FETCH_SIZE x2
+# per the gfx950 correction + WRITE_SIZE), written by tools/pmc_traffic.py.
+TRAFFIC_JSON = os.path.join(REPO, "profiles", "traffic.json")
+# bench stage -> the kernel it times (rocprofv3 kernel-name prefix)
+STAGE_KERNEL = {"generate": "k_gen_normal", "spectral": "k_spectral", "overlap_add": "k_ola_env",
+                "fir_kernel": "k_fir<", "stereo": "k_stereo_out"}
 
 
 def load_irs():
@@ -45,8 +51,25 @@ def stage_bytes(infos, packed, params):
         "spectral": 8 * sum_n,                 # grain read + grain written (one LDS round trip)
         "overlap_add": 4 * sum_n + 4 * out_n,  # placed grains read + mono written (upper bound)
         "fir": 8 * out_n,                      # mono read + mono written
+        "fir_kernel": 8 * out_n,               # k_fir alone: same compulsory bytes
         "stereo": 16 * out_n,                  # max pass reads y; output pass reads y, writes L/R
     }
+
+
+def measured_traffic(kernel, cfg, batch):
+    """HBM bytes per launch of `kernel` from the committed PMC summary, or None
+    when no summary for this workload exists (bench cannot read PMC itself)."""
+    try:
+        with open(TRAFFIC_JSON) as f:
+            t = json.load(f)
+    except (OSError, ValueError):
+        return None
+    if t.get("config") != cfg or int(t.get("batch", -1)) != batch:
+        return None
+    for name, rec in t.get("kernels", {}).items():
+        if name.startswith(kernel):
+            return rec.get("hbm_bytes_per_launch")
+    return None
 
 
 def cpu_baseline(cfg, irs, budget_s):
@@ -67,6 +90,22 @@ def cpu_baseline(cfg, irs, budget_s):
             "sample": f"{done} {cfg} presets (seeds 1000..{999 + done}) rendered sequentially by "
                       f"oracle/msound_oracle.py (NumPy restatement of main_v2.render) on 1 host core "
                       f"in {dt:.1f} s"}
+
+
+def rank_seeds(rank, batch):
+    """Preset seeds of one rank: contiguous, disjoint across ranks (weak scaling)."""
+    return [1000 + rank * batch + b for b in range(batch)]
+
+
+def max_over_ranks(elapsed, world, device):
+    """The job's time is the slowest rank's (all-reduce MAX; no data-path collective)."""
+    if world <= 1:
+        return elapsed
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
 
 
 def main():
@@ -95,7 +134,7 @@ def main():
     from msgpu.pack import PackedBatch
 
     irs = load_irs()
-    seeds = [1000 + rank * args.batch + b for b in range(args.batch)]
+    seeds = rank_seeds(rank, args.batch)
     params = [msgpu.config_params(args.config, seed=s, irs=irs) for s in seeds]
     packed = PackedBatch(params)
     eng = Engine(dev)
@@ -112,7 +151,7 @@ def main():
     infos = eng.last_plan()
 
     eng.set_profiling(True)
-    stage_sum = np.zeros(8)
+    stage_sum = np.zeros(10)
     barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
@@ -123,23 +162,23 @@ def main():
     barrier()
     elapsed = time.perf_counter() - t0
     eng.set_profiling(False)
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{dev}")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = max_over_ranks(elapsed, world, f"cuda:{dev}")
 
     frames_rank = packed.total_frames
     total_frames = frames_rank * world * args.steps
     value = total_frames / elapsed / 1e6
     ms_step = elapsed / args.steps * 1e3
     stage_ms = stage_sum / args.steps
-    names = ["plan", "host_prep", "generate", "spectral", "overlap_add", "fir", "stereo", "total"]
+    names = ["plan", "host_prep", "generate", "spectral", "overlap_add", "fir", "stereo", "total",
+             "fir_kernel", "fir_h"]
     stages = {n: round(float(v), 4) for n, v in zip(names, stage_ms)}
     sb = stage_bytes(infos, packed, params)
     stage_gbs = {k: round(sb[k] / (stages[k] * 1e-3) / 1e9, 1) for k in sb if stages.get(k, 0) > 0}
-    kernel_stages = ["generate", "spectral", "overlap_add", "fir", "stereo"]
+    # dominant single kernel (the FIR stage is timed without its h build)
+    kernel_stages = ["generate", "spectral", "overlap_add", "fir_kernel", "stereo"]
     dom = max(kernel_stages, key=lambda k: stages[k])
     achieved = sb[dom] / (stages[dom] * 1e-3) / 1e9
+    traffic = measured_traffic(STAGE_KERNEL[dom], args.config, args.batch)
     sum_n = sum(int(i.pool_len) for i in infos)
     n_ev = sum(int(i.n_events) for i in infos)
 
@@ -159,9 +198,10 @@ def main():
                        "presets_per_gpu": args.batch, "frames_per_gpu_step": frames_rank,
                        "events_per_gpu_step": n_ev, "design_samples_per_gpu_step": sum_n,
                        "parallelism": f"preset-sharded x{world}"},
-            "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1),
-                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                         "traffic": None, "algorithmic_bytes": sb[dom]},
+            "roofline": {"bound": "hbm", "kernel": STAGE_KERNEL[dom].rstrip("<"),
+                         "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                         "algorithmic_bytes": sb[dom], "kernel_ms": stages[dom]},
             "stage_ms": stages, "stage_algorithmic_GBs": stage_gbs,
             "design_msamples_per_s": round(sum_n * world * args.steps / elapsed / 1e6, 1),
             "cpu_baseline": cpu,

@@ -148,7 +148,8 @@ int msg_last_meta(msg_ctx* ctx, int32_t preset, double* micro, double* grain,
 /* Device time of each stage of the last batch in ms (HIP events):
  * [0] device plan + read-back, [1] host prep + uploads, [2] generate,
  * [3] spectral, [4] overlap-add x ADSR, [5] FIR (h build + FIR),
- * [6] stereo+clip+normalise, [7] total.  Needs msg_set_profiling(ctx, 1).  */
+ * [6] stereo+clip+normalise, [7] total, [8] the FIR kernel alone,
+ * [9] the h build (IR spectra + h spectra).  Needs msg_set_profiling(ctx, 1).  */
 int msg_set_profiling(msg_ctx* ctx, int32_t on);
 int msg_stage_times(msg_ctx* ctx, float* ms, int32_t n);
 
