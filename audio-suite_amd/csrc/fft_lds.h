@@ -108,6 +108,18 @@ template <bool INV> struct Dft<3, INV> { static MSG_DEV void run(float2* v) { Df
 template <bool INV> struct Dft<5, INV> { static MSG_DEV void run(float2* v) { DftOdd<5, INV>::run(v); } };
 template <bool INV> struct Dft<7, INV> { static MSG_DEV void run(float2* v) { DftOdd<7, INV>::run(v); } };
 
+// a * exp(-+2 pi i e / N) for a compile-time e (after unrolling): the
+// quarter turns are swaps/negations (x * 0.f is not folded without fast-math).
+template <bool INV> MSG_DEV float2 twc(float2 a, int e, int N) {
+    if (e == 0) return a;
+    if (4 * e == N) return mul_mi<INV>(a);
+    if (2 * e == N) return make_float2(-a.x, -a.y);
+    if (4 * e == 3 * N) return mul_mi<!INV>(a);
+    const float c = (float)__builtin_cos(2.0 * 3.14159265358979323846 * e / N);
+    const float s = (float)__builtin_sin(2.0 * 3.14159265358979323846 * e / N);
+    return cmul(a, make_float2(c, INV ? s : -s));
+}
+
 // Composite radix R1*R2 by Cooley-Tukey in registers: input n = R2*n1 + n2,
 // output k = k1 + R1*k2.
 template <int R1, int R2, bool INV> struct DftComp {
@@ -122,10 +134,7 @@ template <int R1, int R2, bool INV> struct DftComp {
 #pragma unroll
             for (int k1 = 1; k1 < R1; ++k1) {
                 if (n2 == 0) continue;
-                const int e = (n2 * k1) % N;
-                const float c = (float)__builtin_cos(2.0 * 3.14159265358979323846 * e / N);
-                const float s = (float)__builtin_sin(2.0 * 3.14159265358979323846 * e / N);
-                a[n2][k1] = cmul(a[n2][k1], make_float2(c, INV ? s : -s));
+                a[n2][k1] = twc<INV>(a[n2][k1], (n2 * k1) % N, N);
             }
         }
 #pragma unroll
@@ -148,6 +157,7 @@ template <bool INV> struct Dft<15, INV> { static MSG_DEV void run(float2* v) { D
 template <bool INV> struct Dft<16, INV> { static MSG_DEV void run(float2* v) { DftComp<4, 4, INV>::run(v); } };
 template <bool INV> struct Dft<20, INV> { static MSG_DEV void run(float2* v) { DftComp<4, 5, INV>::run(v); } };
 template <bool INV> struct Dft<25, INV> { static MSG_DEV void run(float2* v) { DftComp<5, 5, INV>::run(v); } };
+template <bool INV> struct Dft<32, INV> { static MSG_DEV void run(float2* v) { DftComp<4, 8, INV>::run(v); } };
 
 // LDS data layout: logical complex element i lives at lp(i) = i ^ ((i>>4)&15),
 // an XOR swizzle inside each aligned 16-element (128-byte) block.  Contiguous

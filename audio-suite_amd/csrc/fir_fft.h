@@ -1,0 +1,353 @@
+// fir_fft.h — register-resident partitioned FFT overlap-save FIR (TU: k_fir.hip).
+//
+// The space FIR (ER taps + IR as one filter h, MS:409-445, 766-773) on an
+// output block of B = N - P + 1 frames:
+//     y_block = last B samples of IFFT_N( sum_q FFT_N(x segment q) . H_q ).
+// N = 2M real samples go through an M-point complex FFT (even/odd packing).
+// Everything about the transform is compile-time for each M in {1024 ..
+// 16384}: three Stockham passes of radices (R1, R2, R3), T = M / (2 R3)
+// threads, every LDS offset an immediate.
+//
+// Data movement per forward transform:
+//   pass 1  global x -> registers (packed pairs, coalesced) -> DFT_R1 -> LDS (A)
+//   pass 2  LDS (A) -> twiddle (exact table) -> DFT_R2 -> LDS (B)
+//   pass 3  LDS (B) -> twiddle (power tree) -> DFT_R3 -> stays in registers
+// Pass 3 gives each thread the butterflies j and NB3 - j, so bins k and M - k
+// of the packed spectrum are in the same thread: the real-FFT split
+// (X[k], X[M-k] from Z[k], Z[M-k]), the multiply-accumulate with H_q and the
+// inverse's pre-step all run in registers.  The inverse runs the same engine
+// on conj(Z') with radices (R3, R2, R1): its first pass reads the registers,
+// its last pass writes the output block straight to HBM.  Two LDS exchanges
+// per transform instead of one per pass plus staging.
+//
+// LDS exchanges use "one pad slot per S" layouts, phys(x) = x + x / S, chosen
+// per exchange so the strided Stockham stores hit distinct banks
+// (ds_write_b64: 16-lane groups over 32 banks) while the unit-stride reads
+// stay conflict-free; twiddle tables sit below the data at LDS offset 0.
+#pragma once
+#include <cmath>
+#include <vector>
+#include "rt.h"
+
+template <int M> struct FirCfg;
+template <> struct FirCfg<16384> { static constexpr int R1 = 32, R2 = 32, R3 = 16; };
+template <> struct FirCfg<8192> { static constexpr int R1 = 32, R2 = 16, R3 = 16; };
+template <> struct FirCfg<4096> { static constexpr int R1 = 16, R2 = 16, R3 = 16; };
+template <> struct FirCfg<2048> { static constexpr int R1 = 16, R2 = 16, R3 = 8; };
+template <> struct FirCfg<1024> { static constexpr int R1 = 16, R2 = 8, R3 = 8; };
+
+constexpr int fir_ilog2(int x) { return x <= 1 ? 0 : 1 + fir_ilog2(x / 2); }
+
+template <int M> struct FirGeo {
+    static constexpr int R1 = FirCfg<M>::R1, R2 = FirCfg<M>::R2, R3 = FirCfg<M>::R3;
+    static constexpr int T = M / (2 * R3);
+    static constexpr int NB1 = M / R1, NB2 = M / R2, NB3 = M / R3;
+    static constexpr int BP1 = NB1 / T, BP2 = NB2 / T;        // butterflies per thread
+    static_assert(NB1 % T == 0 && NB2 % T == 0 && NB3 == 2 * T, "FIR FFT plan");
+    // twiddle tables (float2 entries) at LDS offset 0
+    static constexpr int S2 = R2 * (R1 > R3 ? R1 : R3);        // w_S2^x: passes 2 and 2'
+    static constexpr int OFF_S2 = 0;
+    static constexpr int OFF_MLO = S2;                          // w_M^x, x < 128
+    static constexpr int OFF_MHI = OFF_MLO + 128;               // w_M^(128 x), x < M/128
+    static constexpr int OFF_PLO = OFF_MHI + M / 128;           // w_2M^x, x < 128
+    static constexpr int OFF_PHI = OFF_PLO + 128;               // w_2M^(128 x), 128 x <= NB3
+    static constexpr int TAB_USED = OFF_PHI + NB3 / 128 + 1;
+    static constexpr int TAB = (TAB_USED + 15) & ~15;
+    // exchange layouts: A (pass 1 -> 2), B (2 -> 3), C (1' -> 2'), D (2' -> 3')
+    static constexpr int SA = R1, SB = 32, SC = R3, SD = 32;
+    static constexpr int SMIN = SA < SC ? SA : SC;
+    static constexpr int BUF = M + M / SMIN;
+    static constexpr int LDS_BYTES = (TAB + BUF) * 8;
+    static_assert(LDS_BYTES <= 163840, "FIR LDS budget");
+};
+
+// phys(x) = x + x / S (S a power of two)
+template <int S> MSG_HD constexpr int padx(int x) { return x + (x >> fir_ilog2(S)); }
+
+// v[r] *= w^r for r < R, powers by a balanced product tree (depth <= 2 log2 R)
+template <int R>
+MSG_DEV void twiddle_pow(float2 (&v)[R], float2 w) {
+    float2 p[R];
+    p[1] = w;
+#pragma unroll
+    for (int r = 2; r < R; ++r) {
+        const int hb = 1 << (31 - __builtin_clz(r));
+        p[r] = (r == hb) ? cmul(p[hb / 2], p[hb / 2]) : cmul(p[hb], p[r - hb]);
+    }
+#pragma unroll
+    for (int r = 1; r < R; ++r) v[r] = cmul(v[r], p[r]);
+}
+
+// One radix-R Stockham pass LDS -> LDS: read layout SI with NB = M/R
+// butterflies, twiddles w_{NS R}^{k r} from the exact S2 table, write layout SO.
+template <int M, int R, int NS, int BP, int SI, int SO>
+MSG_DEV void fir_pass_lds(float2* buf, const float2* tab, int t) {
+    using G = FirGeo<M>;
+    constexpr int NB = M / R, T = G::T, F = G::S2 / (NS * R);
+    float2 v[BP][R];
+#pragma unroll
+    for (int b = 0; b < BP; ++b) {
+        const int base = padx<SI>(t + b * T);
+#pragma unroll
+        for (int r = 0; r < R; ++r) v[b][r] = buf[base + padx<SI>(r * NB)];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int b = 0; b < BP; ++b) {
+        const int j = t + b * T;
+        const int k = j & (NS - 1), q = j / NS;
+        const int kf = k * F;
+#pragma unroll
+        for (int r = 1; r < R; ++r) v[b][r] = cmul(v[b][r], tab[G::OFF_S2 + ((kf * r) & (G::S2 - 1))]);
+        Dft<R, false>::run(v[b]);
+        const int obase = padx<SO>(q * NS * R + k);
+#pragma unroll
+        for (int r = 0; r < R; ++r) buf[obase + r * NS + (r * NS) / SO] = v[b][r];
+    }
+}
+
+MSG_DEV float2 fir_wM(const float2* tab, int lo, int hi, int j) {   // two-level table
+    return cmul(tab[hi + (j >> 7)], tab[lo + (j & 127)]);
+}
+
+// forward real-FFT split of bins k, M-k and the multiply-accumulate with H
+MSG_DEV void fir_pair_mac(float2 zk, float2 zm, float2 wk, float2 hk, float2 hm, float2& ak, float2& am) {
+    const float2 e = make_float2(0.5f * (zk.x + zm.x), 0.5f * (zk.y - zm.y));   // (Zk + conj Zm) / 2
+    const float2 d = make_float2(zk.x - zm.x, zk.y + zm.y);                     // Zk - conj Zm
+    const float2 o = make_float2(0.5f * d.y, -0.5f * d.x);                      // d / 2i
+    const float2 wo = cmul(wk, o);
+    const float2 xk = cadd(e, wo);
+    const float2 xm = make_float2(e.x - wo.x, wo.y - e.y);                      // conj(e - wo)
+    ak = cadd(ak, cmul(xk, hk));
+    am = cadd(am, cmul(xm, hm));
+}
+
+// inverse pre-step: Y[k], Y[M-k] -> conj Z'[k], conj Z'[M-k] (irfft packing)
+MSG_DEV void fir_pair_pre(float2& yk, float2& ym, float2 wk) {
+    const float2 e = make_float2(0.5f * (yk.x + ym.x), 0.5f * (yk.y - ym.y));
+    const float2 d = make_float2(yk.x - ym.x, yk.y + ym.y);                     // Yk - conj Ym
+    const float2 o = cscale(cmulc(d, wk), 0.5f);                                // d conj(wk) / 2
+    yk = make_float2(e.x - o.y, -(e.y + o.x));
+    ym = make_float2(e.x + o.y, e.y - o.x);
+}
+
+// exp(-pi i r / R3): the post-twiddle step between the butterflies' bins
+template <int R3> MSG_DEV float2 fir_cr(int r) {
+    return make_float2((float)__builtin_cos(3.14159265358979323846 * r / R3),
+                       (float)-__builtin_sin(3.14159265358979323846 * r / R3));
+}
+
+// Thread 0 holds the two self-paired butterflies j = 0 and j = NB3/2.  Its
+// bins are permuted into the general slot pairing (A'[r] <-> B'[R3-1-r], bins
+// k and M-k) so every thread runs the same branch-free split; the one slot
+// left over (A'[R3-1] = DC/Nyquist, B'[0] = bin M/2) is fixed up by select.
+//   A'[r]: r < R3/2 -> (B, r); r < R3-1 -> (A, r - R3/2 + 1); r = R3-1 -> (A, 0)
+//   B'[u]: u >= R3/2 -> (B, u); u >= 1 -> (A, R3/2 + u); u = 0 -> (A, R3/2)
+template <int R3> MSG_HD constexpr int slotA_h(int r) { return r < R3 / 2 ? 1 : 0; }
+template <int R3> MSG_HD constexpr int slotA_r(int r) { return r < R3 / 2 ? r : (r < R3 - 1 ? r - R3 / 2 + 1 : 0); }
+template <int R3> MSG_HD constexpr int slotB_h(int u) { return u >= R3 / 2 ? 1 : 0; }
+template <int R3> MSG_HD constexpr int slotB_r(int u) { return u >= R3 / 2 ? u : (u >= 1 ? R3 / 2 + u : R3 / 2); }
+// bin k of slot A'[r] in thread 0, and w_2M^k
+template <int M, int R3> MSG_HD constexpr int fir_k0(int r) {
+    return r < R3 / 2 ? M / R3 / 2 + (M / R3) * r : (r < R3 - 1 ? (M / R3) * (r - R3 / 2 + 1) : 0);
+}
+template <int M, int R3> MSG_DEV float2 fir_w0(int r) {
+    const double a = 3.14159265358979323846 * (double)fir_k0<M, R3>(r) / (double)M;
+    return make_float2((float)__builtin_cos(a), (float)-__builtin_sin(a));
+}
+
+template <int R3>
+MSG_DEV void fir_slots(const float2 (&v)[2][R3], float2 (&a)[R3], float2 (&b)[R3], bool t0z) {
+#pragma unroll
+    for (int r = 0; r < R3; ++r) {
+        a[r] = t0z ? v[slotA_h<R3>(r)][slotA_r<R3>(r)] : v[0][r];
+        b[r] = t0z ? v[slotB_h<R3>(r)][slotB_r<R3>(r)] : v[1][r];
+    }
+}
+
+template <int R3>
+MSG_DEV void fir_unslots(float2 (&acc)[2][R3], bool t0z) {
+    float2 v[2][R3];
+#pragma unroll
+    for (int r = 0; r < R3; ++r) {
+        v[slotA_h<R3>(r)][slotA_r<R3>(r)] = acc[0][r];
+        v[slotB_h<R3>(r)][slotB_r<R3>(r)] = acc[1][r];
+    }
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int r = 0; r < R3; ++r) acc[h][r] = t0z ? v[h][r] : acc[h][r];
+}
+
+template <int M>
+__global__ void __launch_bounds__(FirGeo<M>::T)
+k_fir2(const PresetRt* __restrict__ rt, const int2* __restrict__ jobs, const float2* __restrict__ tables,
+       const float2* __restrict__ hspec, const float* __restrict__ x_in, float* __restrict__ y_out) {
+    using G = FirGeo<M>;
+    constexpr int T = G::T, R1 = G::R1, R2 = G::R2, R3 = G::R3;
+    constexpr int NB1 = G::NB1, NB3 = G::NB3, BP1 = G::BP1, BP2 = G::BP2;
+    extern __shared__ __attribute__((aligned(16))) float2 lds[];
+    float2* tab = lds;
+    float2* buf = lds + G::TAB;
+    const int2 job = jobs[blockIdx.x];
+    const PresetRt& pr = rt[job.x];
+    const int P = pr.fir_P, Q = pr.fir_Q;
+    const int64_t n = pr.out_n;
+    const int64_t t0 = (int64_t)job.y * pr.fir_B;
+    const float* x = x_in + pr.y_off;
+    const int t = threadIdx.x;
+    for (int i = t; i < G::TAB_USED; i += T) tab[i] = tables[i];   // visible after the first exchange
+
+    float2 acc[2][R3];
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int r = 0; r < R3; ++r) acc[h][r] = make_float2(0.f, 0.f);
+
+    for (int q = 0; q < Q; ++q) {
+        // per-iteration opaque copy of the thread index: nothing derived from it
+        // is hoisted out of the segment loop (register pressure)
+        const int t = otid();
+        const bool t0z = (t == 0);
+        const int js[2] = {t, t0z ? NB3 / 2 : NB3 - t};
+        // ---- pass 1: x segment (zero outside [0, n)) -> DFT_R1 -> LDS A
+        const int64_t s0 = t0 - (int64_t)q * P - (P - 1);
+        const bool fast = s0 >= 0 && s0 + 2 * M <= n && (s0 & 1) == 0;
+#pragma unroll
+        for (int b = 0; b < BP1; ++b) {
+            const int j = t + b * T;
+            float2 v[R1];
+            if (fast) {
+                const float2* z = reinterpret_cast<const float2*>(x + s0);
+#pragma unroll
+                for (int r = 0; r < R1; ++r) v[r] = z[(uint32_t)(j + r * NB1)];   // 32-bit offsets: saddr
+            } else {
+#pragma unroll
+                for (int r = 0; r < R1; ++r) {
+                    const int64_t a = s0 + 2 * (int64_t)(j + r * NB1);
+                    const bool in0 = a >= 0 && a < n, in1 = a + 1 >= 0 && a + 1 < n;   // branch-free
+                    const float x0 = x[(uint32_t)(in0 ? a : 0)], x1 = x[(uint32_t)(in1 ? a + 1 : 0)];
+                    v[r] = make_float2(in0 ? x0 : 0.f, in1 ? x1 : 0.f);
+                }
+            }
+            Dft<R1, false>::run(v);
+            const int base = padx<G::SA>(j * R1);
+#pragma unroll
+            for (int r = 0; r < R1; ++r) buf[base + r] = v[r];
+        }
+        __syncthreads();
+        // ---- pass 2: LDS A -> LDS B
+        fir_pass_lds<M, R2, R1, BP2, G::SA, G::SB>(buf, tab, t);
+        __syncthreads();
+        // ---- pass 3: LDS B -> registers
+        float2 v[2][R3];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int base = padx<G::SB>(js[h]);
+#pragma unroll
+            for (int r = 0; r < R3; ++r) v[h][r] = buf[base + padx<G::SB>(r * NB3)];
+        }
+        __syncthreads();   // LDS free for the next segment / the inverse
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            twiddle_pow<R3>(v[h], fir_wM(tab, G::OFF_MLO, G::OFF_MHI, js[h]));
+            Dft<R3, false>::run(v[h]);
+        }
+        // ---- real split, X . H_q accumulated in registers (slot layout, fir_slots)
+        const float2* H = hspec + pr.h_off + (int64_t)q * (M + 1);
+        float2 a[R3], bb[R3];
+        fir_slots<R3>(v, a, bb, t0z);
+        const float2 wA = fir_wM(tab, G::OFF_PLO, G::OFF_PHI, js[0]);
+        const float2 hmid = H[M / 2];
+#pragma unroll
+        for (int r = 0; r < R3; ++r) {
+            const int kA = t0z ? fir_k0<M, R3>(r) : js[0] + r * NB3;
+            const float2 hk = H[(uint32_t)kA], hm = H[(uint32_t)(M - kA)];
+            const float2 wk = t0z ? fir_w0<M, R3>(r) : cmul(wA, fir_cr<R3>(r));
+            if (r < R3 - 1) {
+                fir_pair_mac(a[r], bb[R3 - 1 - r], wk, hk, hm, acc[0][r], acc[1][R3 - 1 - r]);
+            } else {   // thread 0: DC/Nyquist packed as (Y[0], Y[M]) and bin M/2
+                float2 dk = make_float2(0.f, 0.f), dm = dk;
+                fir_pair_mac(a[r], bb[0], wk, hk, hm, dk, dm);
+                const float2 z0 = a[r];
+                const float2 dc = make_float2((z0.x + z0.y) * hk.x, (z0.x - z0.y) * hm.x);
+                const float2 mid = cmul(cconj(bb[0]), hmid);
+                acc[0][r] = cadd(acc[0][r], t0z ? dc : dk);
+                acc[1][0] = cadd(acc[1][0], t0z ? mid : dm);
+            }
+        }
+    }
+
+    // ---- inverse: conj Z' from Y in registers, back to the natural butterflies
+    {
+        const int t = otid();
+        const bool t0z = (t == 0);
+        const float2 wA = fir_wM(tab, G::OFF_PLO, G::OFF_PHI, t);
+#pragma unroll
+        for (int r = 0; r < R3; ++r) {
+            const float2 wk = t0z ? fir_w0<M, R3>(r) : cmul(wA, fir_cr<R3>(r));
+            if (r < R3 - 1) {
+                fir_pair_pre(acc[0][r], acc[1][R3 - 1 - r], wk);
+            } else {
+                float2 yk = acc[0][r], ym = acc[1][0];
+                fir_pair_pre(yk, ym, wk);
+                const float y0 = acc[0][r].x, yN = acc[0][r].y;
+                const float2 dc = make_float2(0.5f * (y0 + yN), -0.5f * (y0 - yN));
+                acc[0][r] = t0z ? dc : yk;
+                acc[1][0] = t0z ? acc[1][0] : ym;   // bin M/2: conj Z' = Y
+            }
+        }
+        fir_unslots<R3>(acc, t0z);
+    }
+    // ---- pass 1': registers -> DFT_R3 -> LDS C
+    const int js[2] = {t, t == 0 ? NB3 / 2 : NB3 - t};
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        Dft<R3, false>::run(acc[h]);
+        const int base = padx<G::SC>(js[h] * R3);
+#pragma unroll
+        for (int r = 0; r < R3; ++r) buf[base + r] = acc[h][r];
+    }
+    __syncthreads();
+    // ---- pass 2': LDS C -> LDS D
+    fir_pass_lds<M, R2, R3, BP2, G::SC, G::SD>(buf, tab, t);
+    __syncthreads();
+    // ---- pass 3': LDS D -> DFT_R1 -> output block (samples u >= P-1 of the segment)
+    float* y = y_out + pr.y_off;
+    const float s = 1.0f / (float)M;
+#pragma unroll
+    for (int b = 0; b < BP1; ++b) {
+        const int j = t + b * T;
+        float2 v[R1];
+        const int base = padx<G::SD>(j);
+#pragma unroll
+        for (int r = 0; r < R1; ++r) v[r] = buf[base + padx<G::SD>(r * NB1)];
+        twiddle_pow<R1>(v, fir_wM(tab, G::OFF_MLO, G::OFF_MHI, j));
+        Dft<R1, false>::run(v);
+#pragma unroll
+        for (int r = 0; r < R1; ++r) {
+            const int u = 2 * (j + r * NB1);                 // z[u/2] = x[u] + i x[u+1]
+            const int64_t o = t0 + u - (P - 1);
+            if (u >= P - 1 && o < n) y[(uint32_t)o] = v[r].x * s;
+            if (u + 1 >= P - 1 && o + 1 < n) y[(uint32_t)(o + 1)] = -v[r].y * s;
+        }
+    }
+}
+
+// Host: the twiddle tables of FirGeo<M> (float64-built, rounded once).
+template <int M>
+inline void fir2_tables(std::vector<float>& out) {
+    using G = FirGeo<M>;
+    out.assign(2 * (size_t)G::TAB_USED, 0.f);
+    const long double PI = 3.14159265358979323846264338327950288L;
+    auto put = [&](int at, long double num, long double den) {
+        const long double a = -2.0L * PI * num / den;
+        out[2 * at] = (float)cosl(a);
+        out[2 * at + 1] = (float)sinl(a);
+    };
+    for (int x = 0; x < G::S2; ++x) put(G::OFF_S2 + x, x, G::S2);
+    for (int x = 0; x < 128; ++x) put(G::OFF_MLO + x, x, M);
+    for (int x = 0; x < M / 128; ++x) put(G::OFF_MHI + x, 128.0L * x, M);
+    for (int x = 0; x < 128; ++x) put(G::OFF_PLO + x, x, 2.0L * M);
+    for (int x = 0; x <= G::NB3 / 128; ++x) put(G::OFF_PHI + x, 128.0L * x, 2.0L * M);
+}

@@ -1,8 +1,15 @@
 // k_fir.hip — translation unit of the space FIR kernels.
 #include "kernels_fir.h"
+#include "fir_fft.h"
 #include "launch.h"
 
+template <int M> static void fir2_attr() {
+    (void)hipFuncSetAttribute((const void*)k_fir2<M>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              FirGeo<M>::LDS_BYTES);
+}
+
 void fir_init_attrs() {
+    fir2_attr<1024>(); fir2_attr<2048>(); fir2_attr<4096>(); fir2_attr<8192>(); fir2_attr<16384>();
     (void)hipFuncSetAttribute((const void*)k_fir<FIR_T, FIR_M>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
     (void)hipFuncSetAttribute((const void*)k_fir_h<FIR_T, FIR_M>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
     (void)hipFuncSetAttribute((const void*)k_ir_spec<FIR_T, FIR_M>, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -23,6 +30,37 @@ hipError_t launch_fir_h(unsigned grid, int lds_bytes, hipStream_t s, const Prese
     hipLaunchKernelGGL((k_fir_h<FIR_T, FIR_M>), dim3(grid), dim3(FIR_T), lds_bytes, s, rt, hblk_begin, n_presets,
                        fir_plans, fir_plan_of, er_off, er_gain, ir_bank, ir_spec, hspec);
     return hipGetLastError();
+}
+
+bool fir2_tables_host(int M, std::vector<float>& out) {
+    switch (M) {
+        case 1024: fir2_tables<1024>(out); return true;
+        case 2048: fir2_tables<2048>(out); return true;
+        case 4096: fir2_tables<4096>(out); return true;
+        case 8192: fir2_tables<8192>(out); return true;
+        case 16384: fir2_tables<16384>(out); return true;
+        default: return false;
+    }
+}
+
+template <int M>
+static hipError_t fir2_go(unsigned grid, hipStream_t s, const PresetRt* rt, const int2* jobs, const float2* tables,
+                          const float2* hspec, const float* x_in, float* y_out) {
+    hipLaunchKernelGGL((k_fir2<M>), dim3(grid), dim3(FirGeo<M>::T), FirGeo<M>::LDS_BYTES, s, rt, jobs, tables, hspec,
+                       x_in, y_out);
+    return hipGetLastError();
+}
+
+hipError_t launch_fir2(int M, unsigned grid, hipStream_t s, const PresetRt* rt, const int2* jobs,
+                       const float2* tables, const float2* hspec, const float* x_in, float* y_out) {
+    switch (M) {
+        case 1024: return fir2_go<1024>(grid, s, rt, jobs, tables, hspec, x_in, y_out);
+        case 2048: return fir2_go<2048>(grid, s, rt, jobs, tables, hspec, x_in, y_out);
+        case 4096: return fir2_go<4096>(grid, s, rt, jobs, tables, hspec, x_in, y_out);
+        case 8192: return fir2_go<8192>(grid, s, rt, jobs, tables, hspec, x_in, y_out);
+        case 16384: return fir2_go<16384>(grid, s, rt, jobs, tables, hspec, x_in, y_out);
+        default: return hipErrorInvalidValue;
+    }
 }
 
 hipError_t launch_fir(unsigned grid, int lds_bytes, hipStream_t s, const PresetRt* rt, const int32_t* fblk_begin,

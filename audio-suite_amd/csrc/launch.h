@@ -3,6 +3,7 @@
 // build in parallel.
 #pragma once
 #include <hip/hip_runtime.h>
+#include <vector>
 #include "rt.h"
 
 constexpr int LDS_MAX = 163840;                              // 160 KiB per CU
@@ -28,6 +29,11 @@ hipError_t launch_fir_h(unsigned grid, int lds_bytes, hipStream_t s, const Prese
 hipError_t launch_fir(unsigned grid, int lds_bytes, hipStream_t s, const PresetRt* rt, const int32_t* fblk_begin,
                       int n_presets, const RealPlan* fir_plans, const int32_t* fir_plan_of,
                       const float2* hspec, const float* x_in, float* y_out);
+
+// register-resident FIR with compile-time transform size M = N/2 in {1024..16384}
+bool fir2_tables_host(int M, std::vector<float>& out);
+hipError_t launch_fir2(int M, unsigned grid, hipStream_t s, const PresetRt* rt, const int2* jobs,
+                       const float2* tables, const float2* hspec, const float* x_in, float* y_out);
 
 void fft_bench_init_attrs();
 hipError_t launch_fft_bench(bool po2, unsigned grid, int lds_bytes, hipStream_t s, const RealPlan* plans, int plan,

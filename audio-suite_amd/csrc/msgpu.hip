@@ -70,6 +70,7 @@ struct msg_ctx {
     uint64_t* d_ki = nullptr; double* d_wi = nullptr; double* d_fi = nullptr;
     uint64_t* d_ke = nullptr; double* d_we = nullptr; double* d_fe = nullptr;
     JumpTab* d_jump = nullptr;
+    float2* d_fir2tab[5] = {};   // k_fir2 twiddle tables, M = 1024 << i
     nprng::Zig dzig{};
     PlanStore grain_plans, fir_plans;
     // per-batch buffers
@@ -85,6 +86,7 @@ struct msg_ctx {
     DevBuf<int32_t> gen_list, spec_small, spec_big, tile_begin, fir_begin, h_begin, st_begin, fir_plan_of;
     DevBuf<float> micro, grain, mono_a, mono_y;
     DevBuf<float2> hspec, irspec;
+    DevBuf<int2> fir_jobs;
     DevBuf<int64_t> irjobs;
     DevBuf<double> irbank;
     DevBuf<unsigned> maxbits;
@@ -207,7 +209,7 @@ static double bessel_j(int m, double x) {
 static void choose_fir(int64_t M, int64_t n, int& N, int& P, int& Q) {
     double best = 1e300;
     N = FIR_NMAX; P = (int)std::min<int64_t>(M, FIR_NMAX / 2); Q = (int)((M + P - 1) / P);
-    for (int lg = 10; lg <= 15; ++lg) {
+    for (int lg = 11; lg <= 15; ++lg) {   // k_fir2 sizes: M = N/2 in 1024..16384
         const int NN = 1 << lg;
         for (int q = 1; q <= 64; ++q) {
             const int64_t pp = (M + q - 1) / q;
@@ -293,6 +295,14 @@ msg_ctx* msg_create(int device_ordinal) {
     const nprng::Jump j64 = nprng::jump_of(GEN_T);
     jt.a64 = j64.a; jt.s64 = j64.s;
     if (!up(ctx->d_jump, &jt, 1)) { g_err = "uploading jump table failed"; return nullptr; }
+    for (int i = 0; i < 5; ++i) {
+        std::vector<float> tab;
+        if (!fir2_tables_host(1024 << i, tab) || !up(ctx->d_fir2tab[i], reinterpret_cast<float2*>(tab.data()),
+                                                     tab.size() / 2)) {
+            g_err = "uploading FIR twiddle tables failed";
+            return nullptr;
+        }
+    }
     for (auto& ev : ctx->ev) hipEventCreate(&ev);
     spectral_init_attrs();
     fir_init_attrs();
@@ -310,6 +320,8 @@ void msg_destroy(msg_ctx* ctx) {
     }
     hipFree(ctx->d_ki); hipFree(ctx->d_wi); hipFree(ctx->d_fi);
     hipFree(ctx->d_ke); hipFree(ctx->d_we); hipFree(ctx->d_fe); hipFree(ctx->d_jump);
+    for (float2* t : ctx->d_fir2tab) hipFree(t);
+    ctx->fir_jobs.release();
     for (auto& ev : ctx->ev) hipEventDestroy(ev);
     ctx->presets.release(); ctx->frag_len.release(); ctx->info.release(); ctx->slot_base.release();
     ctx->tap_base.release(); ctx->events.release(); ctx->er_off.release(); ctx->er_gain.release();
@@ -589,6 +601,7 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
     int32_t tiles = 0, fblocks = 0, hblocks = 0, stiles = 0;
     int spec_small_lds = 0, spec_big_lds = 0, fir_lds = 0;
     std::map<std::pair<int, int>, int64_t> ir_spec_of;   // (IR index, N) -> offset
+    std::vector<int2> fjobs_by[5];                        // FIR output blocks per transform size
     std::vector<int64_t> ir_jobs;                         // [ir_off, ir_len, plan, out_off] per job
     for (int p = 0; p < P; ++p) {
         const msg_preset& pr = presets[p];
@@ -653,7 +666,10 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
             } else if (er && M > N) {
                 return fail(ctx, MSG_E_UNSUPPORTED, "early-reflection span exceeds the FIR transform");
             }
-            fblocks += (int32_t)((inf.out_n + r.fir_B - 1) / r.fir_B);
+            const int32_t nblk = (int32_t)((inf.out_n + r.fir_B - 1) / r.fir_B);
+            std::vector<int2>& fj = fjobs_by[__builtin_ctz(N) - 11];
+            for (int32_t b = 0; b < nblk; ++b) fj.push_back(make_int2(p, b));
+            fblocks += nblk;
             hblocks += Q;
             hsum += (int64_t)Q * (N / 2 + 1);
         }
@@ -725,6 +741,14 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
     HIPCHK(ctx, ctx->spec_big.ensure(spec_big.size()));
     HIPCHK(ctx, ctx->tile_begin.ensure(P));
     HIPCHK(ctx, ctx->fir_begin.ensure(P));
+    std::vector<int2> fir_jobs;
+    int32_t fjob_off[6] = {0};
+    for (int i = 0; i < 5; ++i) {
+        fjob_off[i] = (int32_t)fir_jobs.size();
+        fir_jobs.insert(fir_jobs.end(), fjobs_by[i].begin(), fjobs_by[i].end());
+    }
+    fjob_off[5] = (int32_t)fir_jobs.size();
+    HIPCHK(ctx, ctx->fir_jobs.ensure(fir_jobs.size()));
     HIPCHK(ctx, ctx->h_begin.ensure(P));
     HIPCHK(ctx, ctx->st_begin.ensure(P));
     HIPCHK(ctx, ctx->fir_plan_of.ensure(P));
@@ -748,6 +772,7 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
     HIPCHK(ctx, h2d(ctx->spec_big.p, spec_big.data(), sizeof(int32_t) * spec_big.size()));
     HIPCHK(ctx, h2d(ctx->tile_begin.p, tile_begin.data(), sizeof(int32_t) * P));
     HIPCHK(ctx, h2d(ctx->fir_begin.p, fir_begin.data(), sizeof(int32_t) * P));
+    HIPCHK(ctx, h2d(ctx->fir_jobs.p, fir_jobs.data(), sizeof(int2) * fir_jobs.size()));
     HIPCHK(ctx, h2d(ctx->h_begin.p, h_begin.data(), sizeof(int32_t) * P));
     HIPCHK(ctx, h2d(ctx->st_begin.p, st_begin.data(), sizeof(int32_t) * P));
     HIPCHK(ctx, h2d(ctx->fir_plan_of.p, fir_plan_of.data(), sizeof(int32_t) * P));
@@ -789,8 +814,11 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
                                  ctx->fir_plans.dev.p, ctx->fir_plan_of.p, ctx->er_off.p, ctx->er_gain.p,
                                  ctx->irbank.p, ctx->irspec.p, ctx->hspec.p));
         stage_mark(ctx, 8, s);
-        HIPCHK(ctx, launch_fir((unsigned)fblocks, fir_lds, s, ctx->prt.p, ctx->fir_begin.p, P, ctx->fir_plans.dev.p,
-                               ctx->fir_plan_of.p, ctx->hspec.p, ctx->mono_a.p, ctx->mono_y.p));
+        for (int i = 0; i < 5; ++i)
+            if (fjob_off[i + 1] > fjob_off[i])
+                HIPCHK(ctx, launch_fir2(1024 << i, (unsigned)(fjob_off[i + 1] - fjob_off[i]), s, ctx->prt.p,
+                                        ctx->fir_jobs.p + fjob_off[i], ctx->d_fir2tab[i], ctx->hspec.p,
+                                        ctx->mono_a.p, ctx->mono_y.p));
         stage_mark(ctx, 9, s);
         // presets with fir_on == 0 in a mixed batch: copy a -> y
         for (int p = 0; p < P; ++p)

@@ -114,3 +114,26 @@ def test_error_behaviour(msgpu):
         msgpu.render(msgpu.merged(out_dur_s=0.01, env_a=100.0))
     with pytest.raises(ValueError):                 # "a:b:c" breakpoint (MS:461)
         msgpu.render(msgpu.merged(out_dur_s=0.1, bp_density="1:2:3"))
+
+
+def test_fir_transform_sizes(msgpu, irs):
+    """Every compile-time FIR transform size (N = 2048 .. 32768, one and two
+    partitions), odd and even block alignments, ER-only / IR-only / both."""
+    from oracle import msound_oracle as O
+    base = dict(base_sr=48000, out_dur_s=0.3, gen_mode="Resonant strike", event_process="Poisson",
+                space_ir_on=True, seed=21)
+    params = []
+    for taps in (100, 300, 700, 1500, 8192):                  # N = 2048, 4096, 8192, 16384, 32768
+        params.append(msgpu.merged(base, er_cloud_on=False, space_ir_max_samps=taps,
+                                   _ir_audio=irs["tiny_room_ir"]))
+    params.append(msgpu.merged(base, er_cloud_on=True, space_ir_max_samps=8192,
+                               _ir_audio=irs["tiny_room_ir"]))          # ER + IR
+    params.append(msgpu.merged(base, er_cloud_on=True, space_ir_on=False, seed=5))   # ER only
+    params.append(msgpu.merged(base, base_sr=192000, out_dur_s=0.21, er_cloud_on=True,
+                               space_ir_max_samps=8192, _ir_audio=irs["tiny_room_ir"]))   # Q = 2
+    outs = msgpu.render_batch(params)
+    for i, (p, a) in enumerate(zip(params, outs)):
+        ref, _ = O.render(p)
+        err = rms(a, ref)
+        print(f"fir case {i}: rms err {err:.3e}")
+        assert err <= RMS_TOL, i
