@@ -417,3 +417,41 @@ MSG_DEV void rtransform(float2* buf, const RealPlan& rp, const TwLds& tw, bool i
         __syncthreads();
     }
 }
+
+// x[s0 + u] for u < N (zero outside [0, n)) into the LDS real view, read as
+// 16-byte aligned float4 quads (x must be 16-byte aligned), Q4 quads in flight
+// per thread per round (a whole 150 KB grain in one round trip at T = 512).
+template <int T, int Q4>
+MSG_DEV void load_real_segment(float2* lds, const RealPlan& rp, const float* __restrict__ x, int64_t n,
+                               int64_t s0, int N, int tid) {
+    const int64_t a0 = (s0 >> 2) << 2;
+    const int shift = (int)(s0 - a0);
+    const int nq = (N + shift + 3) >> 2;
+    const float4* xq = reinterpret_cast<const float4*>(x);
+    for (int v0 = 0; v0 < nq; v0 += Q4 * T) {
+        float4 q[Q4];
+#pragma unroll
+        for (int i = 0; i < Q4; ++i) {
+            const int v = v0 + i * T + tid;
+            const int64_t a = a0 + 4 * (int64_t)v;
+            if (v < nq && a >= 0 && a + 3 < n) {
+                q[i] = xq[a >> 2];
+            } else {
+                q[i].x = (v < nq && a >= 0 && a < n) ? x[a] : 0.f;
+                q[i].y = (v < nq && a + 1 >= 0 && a + 1 < n) ? x[a + 1] : 0.f;
+                q[i].z = (v < nq && a + 2 >= 0 && a + 2 < n) ? x[a + 2] : 0.f;
+                q[i].w = (v < nq && a + 3 >= 0 && a + 3 < n) ? x[a + 3] : 0.f;
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < Q4; ++i) {
+            const int v = v0 + i * T + tid;
+            if (v >= nq) continue;
+            const int u = 4 * v - shift;
+            const float e[4] = {q[i].x, q[i].y, q[i].z, q[i].w};
+#pragma unroll
+            for (int c = 0; c < 4; ++c)
+                if (u + c >= 0 && u + c < N) rx_set(lds, rp, u + c, e[c]);
+        }
+    }
+}

@@ -10,7 +10,6 @@ template <int M> static void fir2_attr() {
 
 void fir_init_attrs() {
     fir2_attr<1024>(); fir2_attr<2048>(); fir2_attr<4096>(); fir2_attr<8192>(); fir2_attr<16384>();
-    (void)hipFuncSetAttribute((const void*)k_fir<FIR_T, FIR_M>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
     (void)hipFuncSetAttribute((const void*)k_fir_h<FIR_T, FIR_M>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
     (void)hipFuncSetAttribute((const void*)k_ir_spec<FIR_T, FIR_M>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               LDS_MAX);
@@ -61,14 +60,6 @@ hipError_t launch_fir2(int M, unsigned grid, hipStream_t s, const PresetRt* rt, 
         case 16384: return fir2_go<16384>(grid, s, rt, jobs, tables, hspec, x_in, y_out);
         default: return hipErrorInvalidValue;
     }
-}
-
-hipError_t launch_fir(unsigned grid, int lds_bytes, hipStream_t s, const PresetRt* rt, const int32_t* fblk_begin,
-                      int n_presets, const RealPlan* fir_plans, const int32_t* fir_plan_of,
-                      const float2* hspec, const float* x_in, float* y_out) {
-    hipLaunchKernelGGL((k_fir<FIR_T, FIR_M>), dim3(grid), dim3(FIR_T), lds_bytes, s, rt, fblk_begin, n_presets,
-                       fir_plans, fir_plan_of, hspec, x_in, y_out);
-    return hipGetLastError();
 }
 
 // ---- FFT engine micro-benchmark (msg_bench_fft): reps x (forward + inverse)

@@ -36,9 +36,9 @@ __global__ void k_plan_events(const msg_preset* __restrict__ presets, int n_pres
 // The stream of raw PCG64 draws is consumed 64 at a time: lane l holds the
 // state of draw base+l (jump-ahead), classifies it as a fast ziggurat accept,
 // and a wave ballot locates the rare draws that start a slow (rejection)
-// normal.  That lane finishes the slow normal sequentially from its own
-// state and reports how many draws it consumed, which moves the parse
-// position.  The emitted sequence is exactly NumPy's standard_normal(n).
+// normal.  Those lanes finish their slow normal from their own state and
+// report how many draws it consumed, which moves the parse position.  The
+// emitted sequence is exactly NumPy's standard_normal(n).
 // ---------------------------------------------------------------------------
 struct JumpTab { nprng::u128 a[GEN_T]; nprng::u128 s[GEN_T]; nprng::u128 a64, s64; };
 
@@ -142,8 +142,12 @@ k_gen_normal(const msg_preset* __restrict__ presets, const msg_event* __restrict
     nprng::u128 st = jt->a[lane] * g0.state + inc * jt->s[lane];   // state after lane+1 steps
     __syncthreads();
 
+    // Per chunk of 64 draws: every slow lane evaluates its rejection normal
+    // tentatively (in parallel); a wave-uniform walk over the slow lanes then
+    // marks the draws each one consumed, and all surviving lanes emit their
+    // sample at once (rank = popcount of the valid lanes below).
     int produced = 0;
-    int local = 0;   // parse position within the current chunk
+    int local = 0;   // first lane of this chunk that is not consumed by an earlier slow normal
     while (produced < n) {
         const uint64_t raw = nprng::xsl_rr(st);
         const int idx = (int)(raw & 0xff);
@@ -153,24 +157,26 @@ k_gen_normal(const msg_preset* __restrict__ presets, const msg_event* __restrict
         if (rr & 1) x = -x;
         const bool fast = rabs < s_ki[idx];
         const uint64_t F = __ballot(fast);
-        while (local < 64 && produced < n) {
-            const uint64_t S = ~F & (~0ULL << local);
-            const int q = S ? __builtin_ctzll(S) : 64;
-            if (lane >= local && lane < q) {
-                const int j = produced + lane - local;
-                if (j < n) out[j] = gen_basic_sample(c, j, x);
-            }
-            produced += q - local;
-            if (q == 64) { local = 64; break; }
-            int consumed = 1;
-            double v = 0.0;
-            if (lane == q) v = slow_normal(st, inc, rabs, idx, x, z, consumed);
-            v = __shfl(v, q);
-            consumed = __shfl(consumed, q);
-            if (produced < n && lane == 0) out[produced] = gen_basic_sample(c, produced, v);
-            ++produced;
-            local = q + consumed;
+        int consumed = 1;
+        if (!fast && lane >= local) x = slow_normal(st, inc, rabs, idx, x, z, consumed);
+        uint64_t valid = ~0ULL << local;          // local < 64 here
+        uint64_t S = ~F & valid;
+        int pos = 64;
+        while (S) {                               // wave-uniform
+            const int q = __builtin_ctzll(S);
+            const int end = q + __builtin_amdgcn_readlane(consumed, q);
+            const uint64_t after_q = ~((2ULL << q) - 1);                  // lanes q+1..63
+            const uint64_t before_end = end >= 64 ? ~0ULL : ((1ULL << end) - 1);
+            valid &= ~(after_q & before_end);
+            if (end >= 64) { pos = end; break; }
+            S &= ~0ULL << end;
         }
+        if ((valid >> lane) & 1) {
+            const int j = produced + __popcll(valid & ((1ULL << lane) - 1));
+            if (j < n) out[j] = gen_basic_sample(c, j, x);
+        }
+        produced += __popcll(valid);
+        local = pos;
         do {   // advance all lanes by one chunk; skip chunks a slow normal consumed
             st = a64 * st + c64;
             local -= 64;

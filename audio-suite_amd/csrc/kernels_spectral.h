@@ -87,19 +87,9 @@ k_spectral(const msg_preset* __restrict__ presets, const msg_event* __restrict__
     }
     const RealPlan& rp = plans[er.plan];
     const int K = n / 2 + 1;
-    for (int j0 = 0; j0 < n; j0 += 8 * T) {   // 8 loads in flight per thread
-        float v[8];
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            const int j = j0 + i * T + (int)threadIdx.x;
-            v[i] = j < n ? micro[j] : 0.f;
-        }
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            const int j = j0 + i * T + (int)threadIdx.x;
-            if (j < n) rx_set(lds, rp, j, v[i]);
-        }
-    }
+    // the whole grain in flight at once (float4 loads from the 16-byte aligned preset pool)
+    load_real_segment<T, (2 * MAXM + 4 * T - 1) / (4 * T)>(lds, rp, micro_pool + r.pool_base, e.pool_off + n,
+                                                           e.pool_off, n, threadIdx.x);
     const TwLds tw = stage_twiddles<T>(lds + rp.lds_c, rp);   // includes the barrier
 
     // Transform sequence: [tilt F, tilt I] for noise/skew generators, then

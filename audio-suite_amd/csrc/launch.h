@@ -26,10 +26,6 @@ hipError_t launch_fir_h(unsigned grid, int lds_bytes, hipStream_t s, const Prese
                         int n_presets, const RealPlan* fir_plans, const int32_t* fir_plan_of,
                         const int32_t* er_off, const double* er_gain, const double* ir_bank,
                         const float2* ir_spec, float2* hspec);
-hipError_t launch_fir(unsigned grid, int lds_bytes, hipStream_t s, const PresetRt* rt, const int32_t* fblk_begin,
-                      int n_presets, const RealPlan* fir_plans, const int32_t* fir_plan_of,
-                      const float2* hspec, const float* x_in, float* y_out);
-
 // register-resident FIR with compile-time transform size M = N/2 in {1024..16384}
 bool fir2_tables_host(int M, std::vector<float>& out);
 hipError_t launch_fir2(int M, unsigned grid, hipStream_t s, const PresetRt* rt, const int2* jobs,

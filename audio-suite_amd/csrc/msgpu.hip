@@ -692,7 +692,7 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
         st_begin[p] = stiles;
         stiles += (int32_t)((inf.out_n + ST_TILE - 1) / ST_TILE);
         tiles += (int32_t)((inf.out_n + OLA_TILE - 1) / OLA_TILE);
-        pool += inf.pool_len;
+        pool += (inf.pool_len + 3) & ~int64_t(3);   // 16-byte aligned grain regions (float4 loads)
         ysum += (inf.out_n + 3) & ~int64_t(3);   // keep every mono region 16-byte aligned
         // events
         for (int k = 0; k < inf.n_events; ++k) {

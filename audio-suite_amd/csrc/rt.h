@@ -5,7 +5,7 @@
 //   k_spectral<T>                  LDS-resident spectral chain, one WG per event    MS:39-128, 224-233, 690-702
 //   k_ola_env                      grain overlap-add x ADSR, one WG per tile        MS:742-764
 //   k_fir_h                        (delta + ER) * IR kernel spectra per partition   MS:409-445
-//   k_fir                          partitioned FFT overlap-save FIR                 MS:766-773
+//   k_fir2<M>                      register-resident FFT overlap-save FIR           MS:766-773
 //   k_stereo_max / k_stereo_out    25-tap Bessel stereo, tanh, peak normalise       MS:423-436, 775-781
 #pragma once
 #include "msg_common.h"
