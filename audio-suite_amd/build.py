@@ -1,7 +1,11 @@
 #!/usr/bin/env python3
 """Build libmsgpu.so in-tree for gfx950 with hipcc (translation units in parallel).
 
-    python audio-suite_amd/build.py [--force]
+    python audio-suite_amd/build.py [--force] [--stamps]
+
+--stamps builds msgpu/libmsgpu_stamps.so with per-phase clock stamps in the
+spectral kernel (-DMSG_STAMPS, read by tools/spec_stamps.py); load it with
+MSGPU_LIB=.../libmsgpu_stamps.so.  Never the product library.
 """
 import concurrent.futures as cf
 import os
@@ -24,27 +28,34 @@ def _newest_header():
     return max(os.path.getmtime(h) for h in HEADERS)
 
 
-def _compile(tu):
+VARIANTS = {"": ([], "build", "libmsgpu.so"), "stamps": (["-DMSG_STAMPS"], "build_stamps", "libmsgpu_stamps.so")}
+
+
+def _compile(tu, variant=""):
+    defs, objdir, _ = VARIANTS[variant]
     src = os.path.join(CSRC, tu)
-    obj = os.path.join(OBJ, tu.replace(".hip", ".o"))
+    obj = os.path.join(HERE, objdir, tu.replace(".hip", ".o"))
     if os.path.exists(obj) and os.path.getmtime(obj) >= max(os.path.getmtime(src), _newest_header()):
         return obj
-    cmd = [HIPCC, *FLAGS, "-c", "-o", obj + ".tmp", src]
+    cmd = [HIPCC, *FLAGS, *defs, "-c", "-o", obj + ".tmp", src]
     print("[msgpu build]", " ".join(cmd), flush=True)
     subprocess.check_call(cmd)
     os.replace(obj + ".tmp", obj)
     return obj
 
 
-def build(force: bool = False) -> str:
-    os.makedirs(OBJ, exist_ok=True)
+def build(force: bool = False, variant: str = "") -> str:
+    _, objdir, libname = VARIANTS[variant]
+    out = os.path.join(HERE, "msgpu", libname)
+    os.makedirs(os.path.join(HERE, objdir), exist_ok=True)
     if force:
         for tu in TUS:
-            o = os.path.join(OBJ, tu.replace(".hip", ".o"))
+            o = os.path.join(HERE, objdir, tu.replace(".hip", ".o"))
             if os.path.exists(o):
                 os.remove(o)
     with cf.ThreadPoolExecutor(max_workers=len(TUS)) as ex:
-        objs = list(ex.map(_compile, TUS))
+        objs = list(ex.map(lambda tu: _compile(tu, variant), TUS))
+    OUT = out
     if not os.path.exists(OUT) or any(os.path.getmtime(o) > os.path.getmtime(OUT) for o in objs):
         cmd = [HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", OUT + ".tmp", *objs]
         print("[msgpu build]", " ".join(cmd), flush=True)
@@ -54,4 +65,4 @@ def build(force: bool = False) -> str:
 
 
 if __name__ == "__main__":
-    print(build(force="--force" in sys.argv))
+    print(build(force="--force" in sys.argv, variant="stamps" if "--stamps" in sys.argv else ""))

@@ -190,6 +190,16 @@ MSG_DEV int opaque(int v) {
     return o;
 }
 
+// Opaque copy of a wave-uniform pointer: loads through it are re-issued
+// (scalar loads) where they are used instead of being hoisted and kept live.
+template <class P> MSG_DEV P* opaque_ptr(P* p) {
+    const uint64_t v = (uint64_t)p;
+    uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+    uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+    asm volatile("" : "+s"(lo), "+s"(hi));
+    return (P*)(((uint64_t)hi << 32) | lo);
+}
+
 // Opaque thread index: per-thread LDS addresses derived from it are rebuilt
 // inside each pass/step instead of being hoisted (and spilled) by LICM.
 MSG_DEV int otid() {
@@ -337,12 +347,12 @@ MSG_DEV void cfft_fwd(float2* buf, const FftDesc& d, const TwLds& tw) {
 // Spectrum bin / complex element k lives at cx(buf, k) (swizzled).  Real
 // samples x[t] are the packed pairs of element t/2 (even n) or element t's
 // real part (odd n): rx_get / rx_set.
-MSG_DEV float rx_get(const float2* buf, const RealPlan& rp, int t) {
-    if (rp.even) { const float2 c = buf[lp(t >> 1)]; return (t & 1) ? c.y : c.x; }
-    return buf[lp(t)].x;
-}
-MSG_DEV void rx_set(float2* buf, const RealPlan& rp, int t, float v) {
-    if (rp.even) reinterpret_cast<float*>(buf)[2 * lp(t >> 1) + (t & 1)] = v;
+// `even` is the plan's parity, passed by value (a uniform bit, not re-read
+// from the plan in global memory on every access).
+MSG_DEV int rx_idx(bool even, int t) { return even ? 2 * lp(t >> 1) + (t & 1) : 2 * lp(t); }
+MSG_DEV float rx_get(const float2* buf, bool even, int t) { return reinterpret_cast<const float*>(buf)[rx_idx(even, t)]; }
+MSG_DEV void rx_set(float2* buf, bool even, int t, float v) {
+    if (even) reinterpret_cast<float*>(buf)[rx_idx(true, t)] = v;
     else buf[lp(t)] = make_float2(v, 0.f);
 }
 MSG_DEV float2& cx(float2* buf, int k) { return buf[lp(k)]; }
@@ -418,30 +428,24 @@ MSG_DEV void rtransform(float2* buf, const RealPlan& rp, const TwLds& tw, bool i
     }
 }
 
-// x[s0 + u] for u < N (zero outside [0, n)) into the LDS real view, read as
-// 16-byte aligned float4 quads (x must be 16-byte aligned), Q4 quads in flight
-// per thread per round (a whole 150 KB grain in one round trip at T = 512).
+// x[s0 + u] for u < N into the LDS real view, read as 16-byte aligned float4
+// quads, Q4 quads in flight per thread per round (a whole 150 KB grain in one
+// round trip at T = 512).  Loads are unconditional (clamped index) so no
+// branch splits them: x + [floor4(s0), ceil4(s0 + N)) must lie inside the
+// allocation (16-byte aligned regions padded to whole quads).
 template <int T, int Q4>
-MSG_DEV void load_real_segment(float2* lds, const RealPlan& rp, const float* __restrict__ x, int64_t n,
-                               int64_t s0, int N, int tid) {
+MSG_DEV void load_real_segment(float2* lds, bool evn, const float* __restrict__ x, int64_t s0, int N,
+                               int tid) {
     const int64_t a0 = (s0 >> 2) << 2;
     const int shift = (int)(s0 - a0);
     const int nq = (N + shift + 3) >> 2;
-    const float4* xq = reinterpret_cast<const float4*>(x);
+    const float4* xq = reinterpret_cast<const float4*>(x + a0);
     for (int v0 = 0; v0 < nq; v0 += Q4 * T) {
         float4 q[Q4];
 #pragma unroll
         for (int i = 0; i < Q4; ++i) {
             const int v = v0 + i * T + tid;
-            const int64_t a = a0 + 4 * (int64_t)v;
-            if (v < nq && a >= 0 && a + 3 < n) {
-                q[i] = xq[a >> 2];
-            } else {
-                q[i].x = (v < nq && a >= 0 && a < n) ? x[a] : 0.f;
-                q[i].y = (v < nq && a + 1 >= 0 && a + 1 < n) ? x[a + 1] : 0.f;
-                q[i].z = (v < nq && a + 2 >= 0 && a + 2 < n) ? x[a + 2] : 0.f;
-                q[i].w = (v < nq && a + 3 >= 0 && a + 3 < n) ? x[a + 3] : 0.f;
-            }
+            q[i] = xq[v < nq ? v : nq - 1];
         }
 #pragma unroll
         for (int i = 0; i < Q4; ++i) {
@@ -451,7 +455,7 @@ MSG_DEV void load_real_segment(float2* lds, const RealPlan& rp, const float* __r
             const float e[4] = {q[i].x, q[i].y, q[i].z, q[i].w};
 #pragma unroll
             for (int c = 0; c < 4; ++c)
-                if (u + c >= 0 && u + c < N) rx_set(lds, rp, u + c, e[c]);
+                if (u + c >= 0 && u + c < N) rx_set(lds, evn, u + c, e[c]);
         }
     }
 }

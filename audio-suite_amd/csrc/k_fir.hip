@@ -69,10 +69,11 @@ __global__ void __launch_bounds__(T) k_fft_bench(const RealPlan* __restrict__ pl
                                                   float* __restrict__ sink) {
     extern __shared__ __attribute__((aligned(16))) float2 lds[];
     const RealPlan& rp = plans[plan];
-    for (int u = threadIdx.x; u < rp.n; u += T) rx_set(lds, rp, u, (float)((u * 7919) % 113) * 1e-2f);
+    const bool evn = rp.even != 0;
+    for (int u = threadIdx.x; u < rp.n; u += T) rx_set(lds, evn, u, (float)((u * 7919) % 113) * 1e-2f);
     const TwLds tw = stage_twiddles<T>(lds + rp.lds_c, rp);
     for (int r = 0; r < 2 * reps; ++r) rtransform<T, MAXM, RSET>(lds, rp, tw, (r & 1) != 0);
-    if (threadIdx.x == 0) sink[blockIdx.x] = rx_get(lds, rp, 1);
+    if (threadIdx.x == 0) sink[blockIdx.x] = rx_get(lds, evn, 1);
 }
 
 void fft_bench_init_attrs() {

@@ -21,3 +21,17 @@ hipError_t launch_spectral(bool big, unsigned grid, int lds_bytes, hipStream_t s
                            presets, events, ert, rt, plans, ev_list, n_list, micro_pool, grain_pool);
     return hipGetLastError();
 }
+
+#ifdef MSG_STAMPS
+extern "C" int msg_debug_skip(int flags) {
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_spec_skip), &flags, sizeof(int)) == hipSuccess ? 0 : 3;
+}
+
+extern "C" int msg_debug_stamps(unsigned long long* out, int n) {
+    unsigned long long h[16];
+    if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_spec_stamps), sizeof(h)) != hipSuccess) return 3;
+    for (int i = 0; i < n && i < 16; ++i) out[i] = h[i];
+    const unsigned long long z[16] = {};
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_spec_stamps), z, sizeof(z)) == hipSuccess ? 0 : 3;
+}
+#endif

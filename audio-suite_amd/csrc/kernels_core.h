@@ -187,28 +187,18 @@ k_gen_normal(const msg_preset* __restrict__ presets, const msg_event* __restrict
 // ---------------------------------------------------------------------------
 // Overlap-add of placed grains (event order) x ADSR -> mono a[t].
 // ---------------------------------------------------------------------------
-MSG_DEV float adsr_at(const PresetRt& r, int64_t t) {
-    const int64_t n = r.out_n;
-    const int64_t A = r.envA, D = r.envD, R = r.envR;
-    const int64_t i = A;
-    const int64_t j = n < i + D ? n : i + D;
-    const int64_t s1 = (j > n - R) ? j : n - R;
+// x^c for x in [0, 1] (hardware log2/exp2; exact at 0 and 1)
+MSG_DEV float env_pow(float x, float c) { return x > 0.f ? exp2f(c * __log2f(x)) : 0.f; }
+
+// make_adsr (MS:172-195) at frame t < n; region bounds and reciprocals precomputed on the host
+MSG_DEV float adsr_at(const PresetRt& r, int t) {
     const float c = r.envC, S = r.envS;
-    if (A > 0 && t < A) return powf((float)((double)t * (1.0 / (double)A)), c);
-    if (D > 0 && j > i && t >= i && t < j) {
-        const float d = (float)((double)(t - i) * (1.0 / (double)(j - i)));
-        return 1.0f - (1.0f - S) * powf(d, c);
-    }
-    if (t >= j && t < s1) return S;
-    if (R > 0 && n > s1 && t >= s1) {
-        const int64_t num = n - s1;
-        float u;
-        if (num == 1) u = 0.f;
-        else if (t == n - 1) u = 1.f;
-        else u = (float)((double)(t - s1) * (1.0 / (double)(num - 1)));
-        return S * (1.0f - powf(u, c));
-    }
-    return 1.0f;
+    if (t < r.envA) return env_pow((float)t * r.envInvA, c);
+    if (t < r.envJ) return 1.0f - (1.0f - S) * env_pow((float)(t - r.envA) * r.envInvD, c);
+    if (t < r.envS1) return S;
+    const int n = (int)r.out_n;
+    const float u = (n - r.envS1 == 1) ? 0.f : (t == n - 1 ? 1.f : (float)(t - r.envS1) * r.envInvR);
+    return S * (1.0f - env_pow(u, c));
 }
 
 __global__ void __launch_bounds__(OLA_T)
@@ -221,10 +211,11 @@ k_ola_env(const msg_event* __restrict__ events, const PresetRt* __restrict__ rt,
     const int64_t t0 = (int64_t)(b - r.tile_begin) * OLA_TILE;
     const int64_t t1 = t0 + OLA_TILE < r.out_n ? t0 + OLA_TILE : r.out_n;
     constexpr int PER = OLA_TILE / OLA_T;
+    const int lane = threadIdx.x & 63;
     float acc[PER];
 #pragma unroll
     for (int u = 0; u < PER; ++u) acc[u] = 0.f;
-    // events sorted by start: first event whose start > t0 - max_n
+    // events are sorted by start: the first one that can reach t0 starts after t0 - max_n
     const msg_event* ev = events + r.ev_begin;
     int lo = 0, hi = r.n_events;
     const int64_t lim = t0 - (int64_t)r.max_n;
@@ -232,25 +223,43 @@ k_ola_env(const msg_event* __restrict__ events, const PresetRt* __restrict__ rt,
         const int mid = (lo + hi) >> 1;
         if ((int64_t)ev[mid].start <= lim) lo = mid + 1; else hi = mid;
     }
-    for (int k = lo; k < r.n_events; ++k) {
-        const msg_event& e = ev[k];
-        if ((int64_t)e.start >= t1) break;
-        if (e.len <= 0) continue;
-        const int64_t s = e.start, L = e.len;
-        if (s + L <= t0) continue;
-        const float amp = (float)e.amp;
-        const float* g = grain_pool + r.pool_base + e.pool_off + e.offset;
-#pragma unroll
-        for (int u = 0; u < PER; ++u) {
-            const int64_t t = t0 + threadIdx.x + u * OLA_T;
-            const int64_t q = t - s;
-            if (t < t1 && q >= 0 && q < L) acc[u] += amp * g[q];
+    // 64 events per round: lane k fetches event lo+k, then the wave walks them
+    // from registers (readlane) so all their grain reads are in flight together
+    for (int k0 = lo; k0 < r.n_events; k0 += 64) {
+        const int k = k0 + lane;
+        int s = INT32_MAX, L = 0;
+        float amp = 0.f;
+        int64_t goff = 0;
+        if (k < r.n_events) {
+            const msg_event& e = ev[k];
+            s = e.start; L = e.len; amp = (float)e.amp;
+            goff = r.pool_base + e.pool_off + e.offset;
         }
+        const uint64_t live = __ballot(s < t1);           // sorted: a prefix of the lanes
+        const int cnt = __popcll(live);
+        for (int i = 0; i < cnt; ++i) {
+            const int si = __builtin_amdgcn_readlane(s, i);
+            const int Li = __builtin_amdgcn_readlane(L, i);
+            if (Li <= 0 || (int64_t)si + Li <= t0) continue;
+            const float ai = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(amp), i));
+            const int64_t gi = ((int64_t)__builtin_amdgcn_readlane((int)(goff >> 32), i) << 32) |
+                               (uint32_t)__builtin_amdgcn_readlane((int)goff, i);
+            const float* g = grain_pool + gi;
+            const int q0 = (int)t0 - si + (int)threadIdx.x;
+#pragma unroll
+            for (int u = 0; u < PER; ++u) {
+                const int q = q0 + u * OLA_T;
+                if (u * OLA_T + (int)threadIdx.x < (int)(t1 - t0) && q >= 0 && q < Li)
+                    acc[u] = fmaf(ai, g[q], acc[u]);
+            }
+        }
+        if (cnt < 64) break;
     }
+    float* y = mono + r.y_off;
 #pragma unroll
     for (int u = 0; u < PER; ++u) {
-        const int64_t t = t0 + threadIdx.x + u * OLA_T;
-        if (t < t1) mono[r.y_off + t] = acc[u] * adsr_at(r, t);
+        const int t = (int)t0 + (int)threadIdx.x + u * OLA_T;
+        if (t < t1) y[t] = acc[u] * adsr_at(r, t);
     }
 }
 
@@ -260,48 +269,54 @@ k_ola_env(const msg_event* __restrict__ events, const PresetRt* __restrict__ rt,
 // ---------------------------------------------------------------------------
 // A block handles ST_TILE frames [t0, t0+ST_TILE) of one preset.  The
 // right-channel window y[(t0 + dr - 24 + u) mod n], u < ST_TILE + 48, is staged
-// in LDS once (one modulo per block), so each output is 25 LDS reads + FMAs.
-// L[t] = y[(t - dl) mod n] is a shifted coalesced read.
+// in LDS (all loads of a thread in flight at once), so each output is 25 LDS
+// reads + FMAs.  L[t] = y[(t - dl) mod n] is a shifted coalesced read.
+constexpr int ST_PER = ST_TILE / ST_T;
+constexpr int ST_WPER = (ST_TILE + 48 + ST_T - 1) / ST_T;
+
 struct StereoTile {
-    int64_t t0, t1;          // frames of this tile
-    int64_t lbase;           // (t0 - dl) mod n
+    int t0, cnt;             // first frame, frames in this tile
+    int lbase;               // (t0 - dl) mod n
 };
 
-MSG_DEV int64_t mod_n(int64_t i, int64_t n) {
+MSG_DEV int mod_n(int64_t i, int64_t n) {
     i %= n;
-    return i < 0 ? i + n : i;
+    return (int)(i < 0 ? i + n : i);
 }
 
 // Stage the R window into w[0 .. ST_TILE+48); returns the tile bounds.
 MSG_DEV StereoTile stereo_stage(const PresetRt& r, const float* __restrict__ y, int64_t t0, float* w) {
-    const int64_t n = r.out_n;
+    const int n = (int)r.out_n;
     StereoTile st;
-    st.t0 = t0;
-    st.t1 = t0 + ST_TILE < n ? t0 + ST_TILE : n;
+    st.t0 = (int)t0;
+    st.cnt = (int)(t0 + ST_TILE < n ? ST_TILE : n - t0);
     st.lbase = mod_n(t0 - r.dl, n);
     if (r.stereo_fir) {
-        const int64_t b0 = mod_n(t0 + r.dr - 24, n);
-        for (int u = threadIdx.x; u < ST_TILE + 48; u += ST_T) {
-            int64_t i = b0 + u;
-            while (i >= n) i -= n;
-            w[u] = y[i];
+        const int b0 = mod_n(t0 + r.dr - 24, n);
+        float v[ST_WPER];
+#pragma unroll
+        for (int i = 0; i < ST_WPER; ++i) {
+            const int u = threadIdx.x + i * ST_T;
+            int j = b0 + u;
+            if (n >= ST_TILE + 48) { if (j >= n) j -= n; }   // one wrap at most
+            else j %= n;
+            v[i] = u < ST_TILE + 48 ? y[j] : 0.f;
+        }
+#pragma unroll
+        for (int i = 0; i < ST_WPER; ++i) {
+            const int u = threadIdx.x + i * ST_T;
+            if (u < ST_TILE + 48) w[u] = v[i];
         }
     }
     __syncthreads();
     return st;
 }
 
-MSG_DEV void stereo_at(const PresetRt& r, const float* __restrict__ y, const float* w, const StereoTile& st,
-                       int u, float& L, float& R) {
-    const int64_t n = r.out_n;
-    if (!r.stereo_fir) { L = R = y[st.t0 + u]; return; }
-    int64_t il = st.lbase + u;
-    if (il >= n) il -= n;
-    L = y[il];
+MSG_DEV float stereo_r(const PresetRt& r, const float* w, int u) {
     float acc = 0.f;
 #pragma unroll
     for (int m = 0; m < 25; ++m) acc = fmaf(r.bess[m], w[u + 2 * m], acc);
-    R = acc;
+    return acc;
 }
 
 __global__ void __launch_bounds__(ST_T)
@@ -314,17 +329,19 @@ k_stereo_max(const PresetRt* __restrict__ rt, const int32_t* __restrict__ st_beg
     const PresetRt& r = rt[p];
     const float* y = ybuf + r.y_off;
     const StereoTile st = stereo_stage(r, y, (int64_t)(b - st_begin[p]) * ST_TILE, w);
-    const int cnt = (int)(st.t1 - st.t0);
     float m = 0.f;
-    for (int u = threadIdx.x; u < cnt; u += ST_T) {
-        // max|L| over all frames equals max|y| (L is a rotation of y): read y directly
-        m = fmaxf(m, fabsf(y[st.t0 + u]));
-        if (r.stereo_fir) {
-            float acc = 0.f;
+    // max|L| over all frames equals max|y| (L is a rotation of y): read y directly
+    float yv[ST_PER];
 #pragma unroll
-            for (int k = 0; k < 25; ++k) acc = fmaf(r.bess[k], w[u + 2 * k], acc);
-            m = fmaxf(m, fabsf(acc));
-        }
+    for (int i = 0; i < ST_PER; ++i) {
+        const int u = threadIdx.x + i * ST_T;
+        yv[i] = u < st.cnt ? y[st.t0 + u] : 0.f;
+    }
+#pragma unroll
+    for (int i = 0; i < ST_PER; ++i) {
+        const int u = threadIdx.x + i * ST_T;
+        m = fmaxf(m, fabsf(yv[i]));
+        if (r.stereo_fir && u < st.cnt) m = fmaxf(m, fabsf(stereo_r(r, w, u)));
     }
     for (int off = 32; off > 0; off >>= 1) m = fmaxf(m, __shfl_xor(m, off));
     if ((threadIdx.x & 63) == 0) wm[threadIdx.x >> 6] = m;
@@ -352,11 +369,22 @@ k_stereo_out(const PresetRt* __restrict__ rt, const int32_t* __restrict__ st_beg
     const float M = __uint_as_float(maxbits[p]);
     const float mc = sat(M, d, inv_td);
     const float scale = mc > 0.f ? r.peak / mc : 1.f;
+    const int n = (int)r.out_n;
     float2* o = reinterpret_cast<float2*>(out) + r.out_off + st.t0;
-    const int cnt = (int)(st.t1 - st.t0);
-    for (int u = threadIdx.x; u < cnt; u += ST_T) {
-        float L, R;
-        stereo_at(r, y, w, st, u, L, R);
+    float lv[ST_PER];
+#pragma unroll
+    for (int i = 0; i < ST_PER; ++i) {
+        const int u = threadIdx.x + i * ST_T;
+        int il = r.stereo_fir ? st.lbase + u : st.t0 + u;
+        if (il >= n) il -= n;
+        lv[i] = u < st.cnt ? y[il] : 0.f;
+    }
+#pragma unroll
+    for (int i = 0; i < ST_PER; ++i) {
+        const int u = threadIdx.x + i * ST_T;
+        if (u >= st.cnt) continue;
+        const float L = lv[i];
+        const float R = r.stereo_fir ? stereo_r(r, w, u) : L;
         o[u] = make_float2(sat(L, d, inv_td) * scale, sat(R, d, inv_td) * scale);
     }
 }

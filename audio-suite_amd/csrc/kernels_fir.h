@@ -17,9 +17,10 @@ k_ir_spec(const int64_t* __restrict__ jobs /* [ir_off, ir_len, plan, out_off] */
     if (b >= n_jobs) return;
     const int64_t* j = jobs + 4 * b;
     const RealPlan& rp = fir_plans[j[2]];
+    const bool evn = rp.even != 0;
     const double* ir = ir_bank + j[0];
     const int64_t irl = j[1];
-    for (int u = threadIdx.x; u < rp.n; u += T) rx_set(lds, rp, u, u < irl ? (float)ir[u] : 0.f);
+    for (int u = threadIdx.x; u < rp.n; u += T) rx_set(lds, evn, u, u < irl ? (float)ir[u] : 0.f);
     const TwLds tw = stage_twiddles<T>(lds + rp.lds_c, rp);
     rtransform<T, MAXM, RSET_PO2>(lds, rp, tw, false);
     float2* dst = ir_spec + j[3];
@@ -42,12 +43,13 @@ k_fir_h(const PresetRt* __restrict__ rt, const int32_t* __restrict__ hblk_begin,
     const PresetRt& r = rt[p];
     const int q = b - r.h_block_begin;
     const RealPlan& rp = fir_plans[fir_plan_of[p]];
+    const bool evn = rp.even != 0;
     const int N = r.fir_N, P = r.fir_P;
     const TwLds tw = stage_twiddles<T>(lds + rp.lds_c, rp);
     const int irl = r.ir_len;
     const bool conv = r.n_taps > 0 && irl > 0;   // h = e * ir through the IR spectrum
     if (r.n_taps > 0) {
-        for (int u = threadIdx.x; u < N; u += T) rx_set(lds, rp, u, u == 0 ? 1.f : 0.f);
+        for (int u = threadIdx.x; u < N; u += T) rx_set(lds, evn, u, u == 0 ? 1.f : 0.f);
         __syncthreads();
         for (int k = threadIdx.x; k < r.n_taps; k += T) {
             const int64_t o = er_off[r.er_base + k];
@@ -57,7 +59,7 @@ k_fir_h(const PresetRt* __restrict__ rt, const int32_t* __restrict__ hblk_begin,
         }
     } else {
         const double* ir = ir_bank + r.ir_off;
-        for (int u = threadIdx.x; u < N; u += T) rx_set(lds, rp, u, u < irl ? (float)ir[u] : 0.f);
+        for (int u = threadIdx.x; u < N; u += T) rx_set(lds, evn, u, u < irl ? (float)ir[u] : 0.f);
     }
     __syncthreads();
     // transform sequence: conv ? [F, I, F] : [F]; one rtransform call site
@@ -72,13 +74,13 @@ k_fir_h(const PresetRt* __restrict__ rt, const int32_t* __restrict__ hblk_begin,
             for (int i = 0; i < PER; ++i) {
                 const int u = tid + i * T;
                 const int src = q * P + u;
-                v[i] = (u < P && src < Nn) ? rx_get(lds, rp, src) : 0.f;
+                v[i] = (u < P && src < Nn) ? rx_get(lds, evn, src) : 0.f;
             }
             __syncthreads();
 #pragma unroll
             for (int i = 0; i < PER; ++i) {
                 const int u = tid + i * T;
-                if (u < Nn) rx_set(lds, rp, u, v[i]);
+                if (u < Nn) rx_set(lds, evn, u, v[i]);
             }
             __syncthreads();
         }

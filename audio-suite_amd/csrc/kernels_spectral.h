@@ -2,56 +2,91 @@
 #pragma once
 #include "rt.h"
 
+// Phase timing (debug builds with -DMSG_STAMPS): block-summed clock64 deltas
+// per phase, read back with msg_debug_stamps.
+#ifdef MSG_STAMPS
+__device__ unsigned long long g_spec_stamps[16];
+#define SPEC_STAMP(i)                                                            \
+    do {                                                                         \
+        __syncthreads();                                                         \
+        if (threadIdx.x == 0) {                                                  \
+            const long long now_ = wall_clock64();                               \
+            atomicAdd(&g_spec_stamps[i], (unsigned long long)(now_ - stamp_));   \
+            stamp_ = now_;                                                       \
+        }                                                                        \
+    } while (0)
+#define SPEC_STAMP_INIT long long stamp_ = wall_clock64()
+__device__ int g_spec_skip;   // debug: bit 0 skip lowpass, bit 1 skip gathers, bit 2 skip transforms
+#define SPEC_SKIP(b) ((g_spec_skip >> (b)) & 1)
+#else
+#define SPEC_SKIP(b) 0
+#define SPEC_STAMP(i) do {} while (0)
+#define SPEC_STAMP_INIT do {} while (0)
+#endif
+
 // ---------------------------------------------------------------------------
 // Spectral chain, one workgroup per event, grain resident in LDS.
 // ---------------------------------------------------------------------------
-// lowpass_fft weight of bin k (MS:39-58), float64 thresholds exactly as rfftfreq.
-MSG_DEV float lowpass_w(int k, int n, int sr, double cutoff, double roll) {
-    const double nyq = 0.5 * (double)sr;
-    const double c = fmin(fmax(cutoff, 1.0), nyq);
-    const double r = fmax(0.0, roll);
-    const double f = (double)k * (1.0 / ((double)n * (1.0 / (double)sr)));
-    if (r <= 0) return f > c ? 0.f : 1.f;
-    const double f1 = fmin(nyq, c + r);
-    if (f > f1) return 0.f;
-    if (f >= c) {
-        const double t = (f - c) / fmax(1e-12, (f1 - c));
-        return (float)(0.5 * (1.0 + cos(3.141592653589793 * t)));
+// lowpass_fft weights (MS:39-58): float64 thresholds exactly as rfftfreq
+// (f = k * (1 / (n * (1 / sr)))), per-event constants hoisted.
+struct Lowpass {
+    double val, c, r, f1, inv_band;
+    MSG_DEV Lowpass(int n, int sr, double cutoff, double roll) {
+        const double nyq = 0.5 * (double)sr;
+        c = fmin(fmax(cutoff, 1.0), nyq);
+        r = fmax(0.0, roll);
+        val = 1.0 / ((double)n * (1.0 / (double)sr));
+        f1 = fmin(nyq, c + r);
+        inv_band = 1.0 / fmax(1e-12, (f1 - c));
     }
-    return 1.f;
-}
+    MSG_DEV float w(int k) const {
+        const double f = (double)k * val;
+        if (r <= 0) return f > c ? 0.f : 1.f;
+        if (f > f1) return 0.f;
+        if (f >= c) return (float)(0.5 * (1.0 + cos(3.141592653589793 * ((f - c) * inv_band))));
+        return 1.f;
+    }
+};
 
-// Y[k] = interp(src(k), arange(K), X) for re/im, zero outside (np.interp, MS:112-127).
-template <int T, int MAXK, class Src>
-MSG_DEV void spectral_gather(float2* buf, int K, Src src) {
-    constexpr int PER = (MAXK + T - 1) / T;
+// Y[k] = interp(src(k), arange(K), X) for re/im, zero outside (np.interp, MS:112-127),
+// in place.  Every source lies on one side of its bin (ascending: src(k) >= k,
+// else src(k) <= k), so chunks of CH*T bins processed in that order -- read the
+// chunk's sources, barrier, write the chunk, barrier -- never read a bin that
+// was already overwritten.
+template <int T, int CH, class Src>
+MSG_DEV void spectral_gather(float2* buf, int K, bool ascending, Src src) {
+    constexpr int C = CH * T;
+    const int nch = (K + C - 1) / C;
     const int tid = otid();
-    float2 y[PER];
+    for (int c = 0; c < nch; ++c) {
+        const int base = (ascending ? c : nch - 1 - c) * C;
+        float2 y[CH];
 #pragma unroll
-    for (int b = 0; b < PER; ++b) {
-        const int k = tid + b * T;
-        y[b] = make_float2(0.f, 0.f);
-        if (k < K) {
-            const double xs = src(k);
-            if (xs >= 0.0 && xs <= (double)(K - 1)) {
-                const int j = (int)xs;
-                if (j >= K - 1) {
-                    y[b] = cx(buf, K - 1);
-                } else {
-                    const float fr = (float)(xs - (double)j);
-                    const float2 a = cx(buf, j), c = cx(buf, j + 1);
-                    y[b] = make_float2((c.x - a.x) * fr + a.x, (c.y - a.y) * fr + a.y);
+        for (int b = 0; b < CH; ++b) {
+            const int k = base + tid + b * T;
+            y[b] = make_float2(0.f, 0.f);
+            if (k < K) {
+                const double xs = src(k);
+                if (xs >= 0.0 && xs <= (double)(K - 1)) {
+                    const int j = (int)xs;
+                    if (j >= K - 1) {
+                        y[b] = cx(buf, K - 1);
+                    } else {
+                        const float fr = (float)(xs - (double)j);
+                        const float2 a = cx(buf, j), e = cx(buf, j + 1);
+                        y[b] = make_float2((e.x - a.x) * fr + a.x, (e.y - a.y) * fr + a.y);
+                    }
                 }
             }
         }
-    }
-    __syncthreads();
+        __syncthreads();
 #pragma unroll
-    for (int b = 0; b < PER; ++b) {
-        const int k = tid + b * T;
-        if (k < K) cx(buf, k) = y[b];
+        for (int b = 0; b < CH; ++b) {
+            const int k = base + tid + b * T;
+            if (k < K) cx(buf, k) = y[b];
+        }
+        __syncthreads();
     }
-    __syncthreads();
 }
 
 // irfft drops the imaginary part of the DC bin (and of the Nyquist bin for even n);
@@ -73,6 +108,7 @@ k_spectral(const msg_preset* __restrict__ presets, const msg_event* __restrict__
     extern __shared__ __attribute__((aligned(16))) float2 lds[];
     const int li = blockIdx.x;
     if (li >= n_list) return;
+    SPEC_STAMP_INIT;
     const int ei = ev_list[li];
     const msg_event& e = events[ei];
     const EventRt er = ert[ei];
@@ -86,11 +122,14 @@ k_spectral(const msg_preset* __restrict__ presets, const msg_event* __restrict__
         return;
     }
     const RealPlan& rp = plans[er.plan];
+    const bool evn = rp.even != 0;
     const int K = n / 2 + 1;
     // the whole grain in flight at once (float4 loads from the 16-byte aligned preset pool)
-    load_real_segment<T, (2 * MAXM + 4 * T - 1) / (4 * T)>(lds, rp, micro_pool + r.pool_base, e.pool_off + n,
-                                                           e.pool_off, n, threadIdx.x);
+    load_real_segment<T, (2 * MAXM + 4 * T - 1) / (4 * T)>(lds, evn, micro_pool + r.pool_base, e.pool_off, n,
+                                                           threadIdx.x);
+    SPEC_STAMP(0);
     const TwLds tw = stage_twiddles<T>(lds + rp.lds_c, rp);   // includes the barrier
+    SPEC_STAMP(1);
 
     // Transform sequence: [tilt F, tilt I] for noise/skew generators, then
     // [chain F, chain I] for the band-limit / warp / stretch chain.  One call
@@ -101,66 +140,85 @@ k_spectral(const msg_preset* __restrict__ presets, const msg_event* __restrict__
     const int last = chain ? 4 : 2;
     for (int step = first; step < last; ++step) {
         const bool inv = (step & 1) != 0;
+        if (!SPEC_SKIP(2)) rtransform<T, MAXM, RSET_ALL>(lds, rp, tw, inv);
+        SPEC_STAMP(2 + step);
+        // Per-step constants are re-read through opaque pointers: computed
+        // before the step loop (LICM) they stay live across the FFT engine's
+        // register peak and spill.
         const int tid = otid();
-        rtransform<T, MAXM, RSET_ALL>(lds, rp, tw, inv);
+        const EventRt& ex = *opaque_ptr(ert + ei);
+        const int nn = opaque(n);
+        const int KK = nn / 2 + 1;
         if (step == 0) {
             // tilted_noise (MS:224-233): W *= (f/f1)^alpha with f[0] := f[1]
-            const double val = 1.0 / ((double)n * (1.0 / (double)er.gen_sr));
-            for (int k = tid; k < K; k += T) {
+            const double val = 1.0 / ((double)nn * (1.0 / (double)ex.gen_sr));
+            const double ival = 1.0 / fmax(1e-12, val);
+            const double alpha = ex.tilt_alpha;
+            for (int k = tid; k < KK; k += T) {
                 double sh = 1.0;
-                if (K > 1 && k > 0) sh = pow(((double)k * val) / fmax(1e-12, val), er.tilt_alpha);
+                if (KK > 1 && k > 0) sh = pow(((double)k * val) * ival, alpha);
                 cx(lds, k) = cscale(cx(lds, k), (float)sh);
             }
             __syncthreads();
         } else if (step == 1) {
             // envelope, skew, fade (MS:246-255, 265-268); the result is micro_last
-            const int fade = (int)(0.01 * n) > 8 ? (int)(0.01 * n) : 8;
-            const double inv_sr = 1.0 / (double)er.gen_sr;
-            if (ops & SPEC_TILT_SKEW) {
-                // d = diff(max(0, w), prepend=w[0]): needs neighbours -> via registers
-                constexpr int PER = (2 * MAXM + T - 1) / T;
-                float d[PER];
+            const int fade = (int)(0.01 * nn) > 8 ? (int)(0.01 * nn) : 8;
+            const double k_env = -(1.0 / (double)ex.gen_sr) / ex.env_tau;
+            if (ex.ops & SPEC_TILT_SKEW) {
+                // d = diff(max(0, w), prepend=w[0]) in place: d[j] reads w[j-1], w[j],
+                // so chunks run top-down with read -> barrier -> write -> barrier
+                constexpr int CH = 8, C = CH * T;
+                const int nch = (nn + C - 1) / C;
+                for (int c = nch - 1; c >= 0; --c) {
+                    float d[CH];
 #pragma unroll
-                for (int b = 0; b < PER; ++b) {
-                    const int j = tid + b * T;
-                    d[b] = 0.f;
-                    if (j < n && j > 0) d[b] = fmaxf(0.f, rx_get(lds, rp, j)) - fmaxf(0.f, rx_get(lds, rp, j - 1));
-                }
-                __syncthreads();
-#pragma unroll
-                for (int b = 0; b < PER; ++b) {
-                    const int j = tid + b * T;
-                    if (j < n) {
-                        const float env = (float)exp(-((double)j * inv_sr) / er.env_tau);
-                        rx_set(lds, rp, j, d[b] * env * fade_w(j, n, fade));
+                    for (int b = 0; b < CH; ++b) {
+                        const int j = c * C + tid + b * T;
+                        d[b] = 0.f;
+                        if (j < nn && j > 0)
+                            d[b] = fmaxf(0.f, rx_get(lds, evn, j)) - fmaxf(0.f, rx_get(lds, evn, j - 1));
                     }
+                    __syncthreads();
+#pragma unroll
+                    for (int b = 0; b < CH; ++b) {
+                        const int j = c * C + tid + b * T;
+                        if (j < nn) rx_set(lds, evn, j, d[b] * (float)exp((double)j * k_env) * fade_w(j, nn, fade));
+                    }
+                    __syncthreads();
                 }
             } else {
-                for (int j = tid; j < n; j += T) {
-                    const float env = (float)exp(-((double)j * inv_sr) / er.env_tau);
-                    rx_set(lds, rp, j, rx_get(lds, rp, j) * env * fade_w(j, n, fade));
-                }
-            }
-            __syncthreads();
-            for (int j = tid; j < n; j += T) micro[j] = rx_get(lds, rp, j);
-        } else if (step == 2) {
-            if (ops & SPEC_LOWPASS) {
-                for (int k = tid; k < K; k += T)
-                    cx(lds, k) = cscale(cx(lds, k), lowpass_w(k, n, er.gen_sr, er.cutoff_gen, er.roll));
+                for (int j = tid; j < nn; j += T)
+                    rx_set(lds, evn, j, rx_get(lds, evn, j) * (float)exp((double)j * k_env) * fade_w(j, nn, fade));
                 __syncthreads();
             }
-            if (ops & SPEC_WARP) {   // fft_warp_power (MS:103-115)
-                drop_edge_imag(lds, rp);
-                const double kmax = fmax(1.0, (double)(K - 1));
-                const double ip = 1.0 / fmax(1e-6, er.warp_power);
-                spectral_gather<T, MAXM + 1>(lds, K, [&](int k) { return pow((double)k / kmax, ip) * kmax; });
+            float* mo = opaque_ptr(micro);
+            for (int j = tid; j < nn; j += T) mo[j] = rx_get(lds, evn, j);
+        } else if (step == 2) {
+            const int ops2 = ex.ops;
+            if ((ops2 & SPEC_LOWPASS) && !SPEC_SKIP(0)) {
+                const Lowpass lp(nn, ex.gen_sr, ex.cutoff_gen, ex.roll);
+                for (int k = tid; k < KK; k += T) {
+                    const float wk = lp.w(k);
+                    if (wk != 1.f) cx(lds, k) = cscale(cx(lds, k), wk);
+                }
+                __syncthreads();
             }
-            if (ops & SPEC_STRETCH) {   // fft_partial_stretch (MS:117-128)
+            if (ops2 & SPEC_WARP) {   // fft_warp_power (MS:103-115)
                 drop_edge_imag(lds, rp);
-                const double f = fmax(1e-12, er.stretch);
-                spectral_gather<T, MAXM + 1>(lds, K, [&](int k) { return (double)k / f; });
+                const double kmax = fmax(1.0, (double)(KK - 1));
+                const double ikmax = 1.0 / kmax;
+                const double ip = 1.0 / fmax(1e-6, ex.warp_power);
+                spectral_gather<T, 8>(lds, KK, ip <= 1.0, [&](int k) { return pow((double)k * ikmax, ip) * kmax; });
+            }
+            if ((ops2 & SPEC_STRETCH) && !SPEC_SKIP(1)) {   // fft_partial_stretch (MS:117-128)
+                drop_edge_imag(lds, rp);
+                const double f = fmax(1e-12, ex.stretch);
+                const double inv_f = 1.0 / f;
+                spectral_gather<T, 8>(lds, KK, f < 1.0, [&](int k) { return (double)k * inv_f; });
             }
         }
+        SPEC_STAMP(6 + step);
     }
-    for (int j = threadIdx.x; j < n; j += T) grain[j] = rx_get(lds, rp, j);
+    for (int j = threadIdx.x; j < n; j += T) grain[j] = rx_get(lds, evn, j);
+    SPEC_STAMP(10);
 }

@@ -630,6 +630,16 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
         r.envR = (int32_t)std::min<int64_t>(R, INT32_MAX);
         r.envS = (float)std::min(std::max(pr.env_s, 0.0), 1.0);
         r.envC = (float)std::max(1e-6, pr.env_curve);
+        {
+            const int64_t n = inf.out_n;
+            const int64_t j = std::min<int64_t>(n, A + D);
+            const int64_t s1 = std::max<int64_t>(j, n - R);
+            r.envJ = (int32_t)j;
+            r.envS1 = (int32_t)s1;
+            r.envInvA = A > 0 ? (float)(1.0 / (double)A) : 0.f;
+            r.envInvD = j > A ? (float)(1.0 / (double)(j - A)) : 0.f;
+            r.envInvR = n - s1 > 1 ? (float)(1.0 / (double)(n - s1 - 1)) : 0.f;
+        }
         // space FIR
         const bool er = (pr.flags & MSG_F_ER_CLOUD) != 0;
         const int ic = pr.ir_conv;

@@ -28,6 +28,8 @@ struct PresetRt {
     // ADSR (MS:172-195), in samples
     int32_t envA, envD, envR;
     float envS, envC;
+    int32_t envJ, envS1;           // decay end, release start (MS:185-190)
+    float envInvA, envInvD, envInvR;
     // FIR (combined ER + IR), 0 = identity
     int32_t fir_on, fir_N, fir_P, fir_Q, fir_B;
     int32_t fir_block_begin;
@@ -61,7 +63,7 @@ enum : int32_t {
 
 constexpr int GEN_T = 64;          // one wave per event
 constexpr int OLA_T = 256;
-constexpr int OLA_TILE = 2048;
+constexpr int OLA_TILE = 4096;
 constexpr int ST_T = 256;
 constexpr int ST_TILE = 4096;
 
