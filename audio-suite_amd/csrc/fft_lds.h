@@ -428,34 +428,16 @@ MSG_DEV void rtransform(float2* buf, const RealPlan& rp, const TwLds& tw, bool i
     }
 }
 
-// x[s0 + u] for u < N into the LDS real view, read as 16-byte aligned float4
-// quads, Q4 quads in flight per thread per round (a whole 150 KB grain in one
-// round trip at T = 512).  Loads are unconditional (clamped index) so no
-// branch splits them: x + [floor4(s0), ceil4(s0 + N)) must lie inside the
-// allocation (16-byte aligned regions padded to whole quads).
-template <int T, int Q4>
-MSG_DEV void load_real_segment(float2* lds, bool evn, const float* __restrict__ x, int64_t s0, int N,
-                               int tid) {
-    const int64_t a0 = (s0 >> 2) << 2;
-    const int shift = (int)(s0 - a0);
-    const int nq = (N + shift + 3) >> 2;
-    const float4* xq = reinterpret_cast<const float4*>(x + a0);
-    for (int v0 = 0; v0 < nq; v0 += Q4 * T) {
-        float4 q[Q4];
+// v[r] *= w^r for r < R, powers by a balanced product tree (depth <= 2 log2 R)
+template <int R>
+MSG_DEV void twiddle_pow(float2 (&v)[R], float2 w) {
+    float2 p[R];
+    p[1] = w;
+    v[1] = cmul(v[1], w);
 #pragma unroll
-        for (int i = 0; i < Q4; ++i) {
-            const int v = v0 + i * T + tid;
-            q[i] = xq[v < nq ? v : nq - 1];
-        }
-#pragma unroll
-        for (int i = 0; i < Q4; ++i) {
-            const int v = v0 + i * T + tid;
-            if (v >= nq) continue;
-            const int u = 4 * v - shift;
-            const float e[4] = {q[i].x, q[i].y, q[i].z, q[i].w};
-#pragma unroll
-            for (int c = 0; c < 4; ++c)
-                if (u + c >= 0 && u + c < N) rx_set(lds, evn, u + c, e[c]);
-        }
+    for (int r = 2; r < R; ++r) {   // each power applied as soon as it exists (short live ranges)
+        const int hb = 1 << (31 - __builtin_clz(r));
+        p[r] = (r == hb) ? cmul(p[hb / 2], p[hb / 2]) : cmul(p[hb], p[r - hb]);
+        v[r] = cmul(v[r], p[r]);
     }
 }

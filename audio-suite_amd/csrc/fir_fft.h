@@ -64,20 +64,6 @@ template <int M> struct FirGeo {
 // phys(x) = x + x / S (S a power of two)
 template <int S> MSG_HD constexpr int padx(int x) { return x + (x >> fir_ilog2(S)); }
 
-// v[r] *= w^r for r < R, powers by a balanced product tree (depth <= 2 log2 R)
-template <int R>
-MSG_DEV void twiddle_pow(float2 (&v)[R], float2 w) {
-    float2 p[R];
-    p[1] = w;
-#pragma unroll
-    for (int r = 2; r < R; ++r) {
-        const int hb = 1 << (31 - __builtin_clz(r));
-        p[r] = (r == hb) ? cmul(p[hb / 2], p[hb / 2]) : cmul(p[hb], p[r - hb]);
-    }
-#pragma unroll
-    for (int r = 1; r < R; ++r) v[r] = cmul(v[r], p[r]);
-}
-
 // One radix-R Stockham pass LDS -> LDS: read layout SI with NB = M/R
 // butterflies, twiddles w_{NS R}^{k r} from the exact S2 table, write layout SO.
 template <int M, int R, int NS, int BP, int SI, int SO>

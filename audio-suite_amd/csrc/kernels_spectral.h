@@ -16,17 +16,68 @@ __device__ unsigned long long g_spec_stamps[16];
         }                                                                        \
     } while (0)
 #define SPEC_STAMP_INIT long long stamp_ = wall_clock64()
+#define SPEC_STAMP_RESET stamp_ = wall_clock64()
 __device__ int g_spec_skip;   // debug: bit 0 skip lowpass, bit 1 skip gathers, bit 2 skip transforms
 #define SPEC_SKIP(b) ((g_spec_skip >> (b)) & 1)
 #else
 #define SPEC_SKIP(b) 0
 #define SPEC_STAMP(i) do {} while (0)
 #define SPEC_STAMP_INIT do {} while (0)
+#define SPEC_STAMP_RESET do {} while (0)
 #endif
 
 // ---------------------------------------------------------------------------
 // Spectral chain, one workgroup per event, grain resident in LDS.
+//
+// The chain (MS:219-269 tilt/envelope, MS:39-128 band-limit / warp / stretch)
+// is written once over an LDS layout policy L and a transform functor, and
+// instantiated twice: the runtime-plan engine (fft_lds.h, XOR-swizzled
+// layout) for any length, and compile-time plans for hot lengths
+// (spec_ct.h, identity layout).
 // ---------------------------------------------------------------------------
+struct LaySwz { static MSG_DEV int c(int k) { return lp(k); } };
+struct LayId { static MSG_DEV int c(int k) { return k; } };
+
+template <class L> MSG_DEV float2& cxl(float2* b, int k) { return b[L::c(k)]; }
+template <class L> MSG_DEV float rxl_get(const float2* b, bool even, int t) {
+    return reinterpret_cast<const float*>(b)[even ? 2 * L::c(t >> 1) + (t & 1) : 2 * L::c(t)];
+}
+template <class L> MSG_DEV void rxl_set(float2* b, bool even, int t, float v) {
+    if (even) reinterpret_cast<float*>(b)[2 * L::c(t >> 1) + (t & 1)] = v;
+    else b[L::c(t)] = make_float2(v, 0.f);
+}
+
+// x[s0 + u] for u < N into the LDS real view, read as 16-byte aligned float4
+// quads, Q4 quads in flight per thread per round (a whole 150 KB grain in one
+// round trip at T = 512).  Loads are unconditional (clamped index) so no
+// branch splits them: x + [floor4(s0), ceil4(s0 + N)) must lie inside the
+// allocation (16-byte aligned regions padded to whole quads).
+template <class L, int T, int Q4>
+MSG_DEV void load_real_segment(float2* lds, bool evn, const float* __restrict__ x, int64_t s0, int N, int tid) {
+    const int64_t a0 = (s0 >> 2) << 2;
+    const int shift = (int)(s0 - a0);
+    const int nq = (N + shift + 3) >> 2;
+    const float4* xq = reinterpret_cast<const float4*>(x + a0);
+    for (int v0 = 0; v0 < nq; v0 += Q4 * T) {
+        float4 q[Q4];
+#pragma unroll
+        for (int i = 0; i < Q4; ++i) {
+            const int v = v0 + i * T + tid;
+            q[i] = xq[v < nq ? v : nq - 1];
+        }
+#pragma unroll
+        for (int i = 0; i < Q4; ++i) {
+            const int v = v0 + i * T + tid;
+            if (v >= nq) continue;
+            const int u = 4 * v - shift;
+            const float e[4] = {q[i].x, q[i].y, q[i].z, q[i].w};
+#pragma unroll
+            for (int c = 0; c < 4; ++c)
+                if (u + c >= 0 && u + c < N) rxl_set<L>(lds, evn, u + c, e[c]);
+        }
+    }
+}
+
 // lowpass_fft weights (MS:39-58): float64 thresholds exactly as rfftfreq
 // (f = k * (1 / (n * (1 / sr)))), per-event constants hoisted.
 struct Lowpass {
@@ -53,7 +104,7 @@ struct Lowpass {
 // else src(k) <= k), so chunks of CH*T bins processed in that order -- read the
 // chunk's sources, barrier, write the chunk, barrier -- never read a bin that
 // was already overwritten.
-template <int T, int CH, class Src>
+template <class L, int T, int CH, class Src>
 MSG_DEV void spectral_gather(float2* buf, int K, bool ascending, Src src) {
     constexpr int C = CH * T;
     const int nch = (K + C - 1) / C;
@@ -70,10 +121,10 @@ MSG_DEV void spectral_gather(float2* buf, int K, bool ascending, Src src) {
                 if (xs >= 0.0 && xs <= (double)(K - 1)) {
                     const int j = (int)xs;
                     if (j >= K - 1) {
-                        y[b] = cx(buf, K - 1);
+                        y[b] = cxl<L>(buf, K - 1);
                     } else {
                         const float fr = (float)(xs - (double)j);
-                        const float2 a = cx(buf, j), e = cx(buf, j + 1);
+                        const float2 a = cxl<L>(buf, j), e = cxl<L>(buf, j + 1);
                         y[b] = make_float2((e.x - a.x) * fr + a.x, (e.y - a.y) * fr + a.y);
                     }
                 }
@@ -83,7 +134,7 @@ MSG_DEV void spectral_gather(float2* buf, int K, bool ascending, Src src) {
 #pragma unroll
         for (int b = 0; b < CH; ++b) {
             const int k = base + tid + b * T;
-            if (k < K) cx(buf, k) = y[b];
+            if (k < K) cxl<L>(buf, k) = y[b];
         }
         __syncthreads();
     }
@@ -91,60 +142,31 @@ MSG_DEV void spectral_gather(float2* buf, int K, bool ascending, Src src) {
 
 // irfft drops the imaginary part of the DC bin (and of the Nyquist bin for even n);
 // reproduce that between fused spectral stages.
-MSG_DEV void drop_edge_imag(float2* buf, const RealPlan& rp) {
+template <class L> MSG_DEV void drop_edge_imag(float2* buf, bool even, int n) {
     if (threadIdx.x == 0) {
-        cx(buf, 0).y = 0.f;
-        if (rp.even) cx(buf, rp.n / 2).y = 0.f;
+        cxl<L>(buf, 0).y = 0.f;
+        if (even) cxl<L>(buf, n / 2).y = 0.f;
     }
     __syncthreads();
 }
 
-template <int T, int MAXM>
-__global__ void __launch_bounds__(T)
-k_spectral(const msg_preset* __restrict__ presets, const msg_event* __restrict__ events,
-           const EventRt* __restrict__ ert, const PresetRt* __restrict__ rt,
-           const RealPlan* __restrict__ plans, const int32_t* __restrict__ ev_list, int n_list,
-           float* __restrict__ micro_pool, float* __restrict__ grain_pool) {
-    extern __shared__ __attribute__((aligned(16))) float2 lds[];
-    const int li = blockIdx.x;
-    if (li >= n_list) return;
+// Transform sequence: [tilt F, tilt I] for noise/skew generators, then
+// [chain F, chain I] for the band-limit / warp / stretch chain.  One call site
+// of the transform keeps one copy of the FFT engine in the kernel.  Per-step
+// constants are re-read through opaque pointers: computed before the step
+// loop (LICM) they stay live across the FFT engine's register peak and spill.
+template <class L, int T, class XF>
+MSG_DEV void spectral_chain(float2* lds, bool evn, const EventRt* __restrict__ ert, int ei, int n,
+                            float* micro, XF&& xf) {
     SPEC_STAMP_INIT;
-    const int ei = ev_list[li];
-    const msg_event& e = events[ei];
-    const EventRt er = ert[ei];
-    const PresetRt& r = rt[e.preset];
-    const int n = e.n;
-    float* micro = micro_pool + r.pool_base + e.pool_off;
-    float* grain = grain_pool + r.pool_base + e.pool_off;
-    const int ops = er.ops;
-    if (ops == 0) {   // no spectral stage: grain = micro
-        for (int j = threadIdx.x; j < n; j += T) grain[j] = micro[j];
-        return;
-    }
-    const RealPlan& rp = plans[er.plan];
-    const bool evn = rp.even != 0;
-    const int K = n / 2 + 1;
-    // the whole grain in flight at once (float4 loads from the 16-byte aligned preset pool)
-    load_real_segment<T, (2 * MAXM + 4 * T - 1) / (4 * T)>(lds, evn, micro_pool + r.pool_base, e.pool_off, n,
-                                                           threadIdx.x);
-    SPEC_STAMP(0);
-    const TwLds tw = stage_twiddles<T>(lds + rp.lds_c, rp);   // includes the barrier
-    SPEC_STAMP(1);
-
-    // Transform sequence: [tilt F, tilt I] for noise/skew generators, then
-    // [chain F, chain I] for the band-limit / warp / stretch chain.  One call
-    // site of rtransform keeps one copy of the FFT engine in the kernel.
+    const int ops = ert[ei].ops;
     const bool tilt = (ops & (SPEC_TILT_NOISE | SPEC_TILT_SKEW)) != 0;
     const bool chain = (ops & (SPEC_LOWPASS | SPEC_STRETCH | SPEC_WARP)) != 0;
     const int first = tilt ? 0 : 2;
     const int last = chain ? 4 : 2;
     for (int step = first; step < last; ++step) {
         const bool inv = (step & 1) != 0;
-        if (!SPEC_SKIP(2)) rtransform<T, MAXM, RSET_ALL>(lds, rp, tw, inv);
-        SPEC_STAMP(2 + step);
-        // Per-step constants are re-read through opaque pointers: computed
-        // before the step loop (LICM) they stay live across the FFT engine's
-        // register peak and spill.
+        if (!SPEC_SKIP(2)) xf(inv);
         const int tid = otid();
         const EventRt& ex = *opaque_ptr(ert + ei);
         const int nn = opaque(n);
@@ -157,7 +179,7 @@ k_spectral(const msg_preset* __restrict__ presets, const msg_event* __restrict__
             for (int k = tid; k < KK; k += T) {
                 double sh = 1.0;
                 if (KK > 1 && k > 0) sh = pow(((double)k * val) * ival, alpha);
-                cx(lds, k) = cscale(cx(lds, k), (float)sh);
+                cxl<L>(lds, k) = cscale(cxl<L>(lds, k), (float)sh);
             }
             __syncthreads();
         } else if (step == 1) {
@@ -176,49 +198,86 @@ k_spectral(const msg_preset* __restrict__ presets, const msg_event* __restrict__
                         const int j = c * C + tid + b * T;
                         d[b] = 0.f;
                         if (j < nn && j > 0)
-                            d[b] = fmaxf(0.f, rx_get(lds, evn, j)) - fmaxf(0.f, rx_get(lds, evn, j - 1));
+                            d[b] = fmaxf(0.f, rxl_get<L>(lds, evn, j)) - fmaxf(0.f, rxl_get<L>(lds, evn, j - 1));
                     }
                     __syncthreads();
 #pragma unroll
                     for (int b = 0; b < CH; ++b) {
                         const int j = c * C + tid + b * T;
-                        if (j < nn) rx_set(lds, evn, j, d[b] * (float)exp((double)j * k_env) * fade_w(j, nn, fade));
+                        if (j < nn)
+                            rxl_set<L>(lds, evn, j, d[b] * (float)exp((double)j * k_env) * fade_w(j, nn, fade));
                     }
                     __syncthreads();
                 }
             } else {
                 for (int j = tid; j < nn; j += T)
-                    rx_set(lds, evn, j, rx_get(lds, evn, j) * (float)exp((double)j * k_env) * fade_w(j, nn, fade));
+                    rxl_set<L>(lds, evn, j,
+                               rxl_get<L>(lds, evn, j) * (float)exp((double)j * k_env) * fade_w(j, nn, fade));
                 __syncthreads();
             }
             float* mo = opaque_ptr(micro);
-            for (int j = tid; j < nn; j += T) mo[j] = rx_get(lds, evn, j);
+            for (int j = tid; j < nn; j += T) mo[j] = rxl_get<L>(lds, evn, j);
         } else if (step == 2) {
             const int ops2 = ex.ops;
             if ((ops2 & SPEC_LOWPASS) && !SPEC_SKIP(0)) {
-                const Lowpass lp(nn, ex.gen_sr, ex.cutoff_gen, ex.roll);
+                const Lowpass lpw(nn, ex.gen_sr, ex.cutoff_gen, ex.roll);
                 for (int k = tid; k < KK; k += T) {
-                    const float wk = lp.w(k);
-                    if (wk != 1.f) cx(lds, k) = cscale(cx(lds, k), wk);
+                    const float wk = lpw.w(k);
+                    if (wk != 1.f) cxl<L>(lds, k) = cscale(cxl<L>(lds, k), wk);
                 }
                 __syncthreads();
             }
             if (ops2 & SPEC_WARP) {   // fft_warp_power (MS:103-115)
-                drop_edge_imag(lds, rp);
+                drop_edge_imag<L>(lds, evn, nn);
                 const double kmax = fmax(1.0, (double)(KK - 1));
                 const double ikmax = 1.0 / kmax;
                 const double ip = 1.0 / fmax(1e-6, ex.warp_power);
-                spectral_gather<T, 8>(lds, KK, ip <= 1.0, [&](int k) { return pow((double)k * ikmax, ip) * kmax; });
+                spectral_gather<L, T, 8>(lds, KK, ip <= 1.0,
+                                         [&](int k) { return pow((double)k * ikmax, ip) * kmax; });
             }
             if ((ops2 & SPEC_STRETCH) && !SPEC_SKIP(1)) {   // fft_partial_stretch (MS:117-128)
-                drop_edge_imag(lds, rp);
+                drop_edge_imag<L>(lds, evn, nn);
                 const double f = fmax(1e-12, ex.stretch);
                 const double inv_f = 1.0 / f;
-                spectral_gather<T, 8>(lds, KK, f < 1.0, [&](int k) { return (double)k * inv_f; });
+                spectral_gather<L, T, 8>(lds, KK, f < 1.0, [&](int k) { return (double)k * inv_f; });
             }
         }
-        SPEC_STAMP(6 + step);
+        SPEC_STAMP(2 + step);
     }
-    for (int j = threadIdx.x; j < n; j += T) grain[j] = rx_get(lds, evn, j);
+}
+
+// Runtime-plan kernel: any grain length (Bluestein for non-7-smooth lengths).
+template <int T, int MAXM>
+__global__ void __launch_bounds__(T)
+k_spectral(const msg_preset* __restrict__ presets, const msg_event* __restrict__ events,
+           const EventRt* __restrict__ ert, const PresetRt* __restrict__ rt,
+           const RealPlan* __restrict__ plans, const int32_t* __restrict__ ev_list, int n_list,
+           float* __restrict__ micro_pool, float* __restrict__ grain_pool) {
+    extern __shared__ __attribute__((aligned(16))) float2 lds[];
+    const int li = blockIdx.x;
+    if (li >= n_list) return;
+    SPEC_STAMP_INIT;
+    const int ei = ev_list[li];
+    const msg_event& e = events[ei];
+    const PresetRt& r = rt[e.preset];
+    const int n = e.n;
+    float* micro = micro_pool + r.pool_base + e.pool_off;
+    float* grain = grain_pool + r.pool_base + e.pool_off;
+    if (ert[ei].ops == 0) {   // no spectral stage: grain = micro
+        for (int j = threadIdx.x; j < n; j += T) grain[j] = micro[j];
+        return;
+    }
+    const RealPlan& rp = plans[ert[ei].plan];
+    const bool evn = rp.even != 0;
+    // the whole grain in flight at once (float4 loads from the 16-byte aligned preset pool)
+    load_real_segment<LaySwz, T, (2 * MAXM + 4 * T - 1) / (4 * T)>(lds, evn, micro_pool + r.pool_base,
+                                                                   e.pool_off, n, threadIdx.x);
+    SPEC_STAMP(0);
+    const TwLds tw = stage_twiddles<T>(lds + rp.lds_c, rp);   // includes the barrier
+    SPEC_STAMP(1);
+    spectral_chain<LaySwz, T>(lds, evn, ert, ei, n, micro,
+                              [&](bool inv) { rtransform<T, MAXM, RSET_ALL>(lds, rp, tw, inv); });
+    SPEC_STAMP_RESET;
+    for (int j = threadIdx.x; j < n; j += T) grain[j] = rxl_get<LaySwz>(lds, evn, j);
     SPEC_STAMP(10);
 }

@@ -19,6 +19,15 @@ hipError_t launch_spectral(bool big, unsigned grid, int lds_bytes, hipStream_t s
                            const PresetRt* rt, const RealPlan* plans, const int32_t* ev_list, int n_list,
                            float* micro_pool, float* grain_pool);
 
+// compile-time-plan spectral kernels for hot grain lengths (spec_ct.h)
+constexpr int SPEC_CT_PLANS = 5;
+void spectral_ct_init_attrs();
+int spectral_ct_plan(int n);
+bool spectral_ct_tables(int plan, std::vector<float>& out);
+hipError_t launch_spectral_ct(int plan, unsigned grid, hipStream_t s, const msg_event* events, const EventRt* ert,
+                              const PresetRt* rt, const float2* tables, const int32_t* ev_list, int n_list,
+                              float* micro_pool, float* grain_pool);
+
 void fir_init_attrs();
 hipError_t launch_ir_spec(unsigned grid, int lds_bytes, hipStream_t s, const int64_t* jobs, int n_jobs,
                           const RealPlan* fir_plans, const double* ir_bank, float2* ir_spec);

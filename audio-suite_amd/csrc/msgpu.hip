@@ -71,6 +71,7 @@ struct msg_ctx {
     uint64_t* d_ke = nullptr; double* d_we = nullptr; double* d_fe = nullptr;
     JumpTab* d_jump = nullptr;
     float2* d_fir2tab[5] = {};   // k_fir2 twiddle tables, M = 1024 << i
+    float2* d_spec_ct_tab[SPEC_CT_PLANS] = {};   // compile-time spectral plans (spec_ct.h)
     nprng::Zig dzig{};
     PlanStore grain_plans, fir_plans;
     // per-batch buffers
@@ -87,6 +88,7 @@ struct msg_ctx {
     DevBuf<float> micro, grain, mono_a, mono_y;
     DevBuf<float2> hspec, irspec;
     DevBuf<int2> fir_jobs;
+    DevBuf<int32_t> spec_ct_list;
     DevBuf<int64_t> irjobs;
     DevBuf<double> irbank;
     DevBuf<unsigned> maxbits;
@@ -303,7 +305,16 @@ msg_ctx* msg_create(int device_ordinal) {
             return nullptr;
         }
     }
+    for (int i = 0; i < SPEC_CT_PLANS; ++i) {
+        std::vector<float> tab;
+        if (!spectral_ct_tables(i, tab) || !up(ctx->d_spec_ct_tab[i], reinterpret_cast<float2*>(tab.data()),
+                                               tab.size() / 2)) {
+            g_err = "uploading spectral twiddle tables failed";
+            return nullptr;
+        }
+    }
     for (auto& ev : ctx->ev) hipEventCreate(&ev);
+    spectral_ct_init_attrs();
     spectral_init_attrs();
     fir_init_attrs();
     fft_bench_init_attrs();
@@ -321,6 +332,8 @@ void msg_destroy(msg_ctx* ctx) {
     hipFree(ctx->d_ki); hipFree(ctx->d_wi); hipFree(ctx->d_fi);
     hipFree(ctx->d_ke); hipFree(ctx->d_we); hipFree(ctx->d_fe); hipFree(ctx->d_jump);
     for (float2* t : ctx->d_fir2tab) hipFree(t);
+    for (float2* t : ctx->d_spec_ct_tab) hipFree(t);
+    ctx->spec_ct_list.release();
     ctx->fir_jobs.release();
     for (auto& ev : ctx->ev) hipEventDestroy(ev);
     ctx->presets.release(); ctx->frag_len.release(); ctx->info.release(); ctx->slot_base.release();
@@ -600,6 +613,9 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
     int64_t pool = 0, ysum = 0, hsum = 0, irs_sum = 0;
     int32_t tiles = 0, fblocks = 0, hblocks = 0, stiles = 0;
     int spec_small_lds = 0, spec_big_lds = 0, fir_lds = 0;
+    std::vector<int32_t> spec_ct[SPEC_CT_PLANS];           // events of the compile-time spectral plans
+    const char* ct_env = getenv("MSGPU_SPEC_CT");         // "0": runtime-plan kernels only (tests)
+    const bool use_ct = !(ct_env && ct_env[0] == '0');
     std::map<std::pair<int, int>, int64_t> ir_spec_of;   // (IR index, N) -> offset
     std::vector<int2> fjobs_by[5];                        // FIR output blocks per transform size
     std::vector<int64_t> ir_jobs;                         // [ir_off, ir_len, plan, out_off] per job
@@ -721,7 +737,10 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
             x.env_tau = std::max(1e-6, (pr.micro_ms / 1000.0) * (pr.gen_mode == MSG_GEN_SKEWED ? 0.2 : 0.25));
             x.warp_power = pr.nl_warp_power;
             gen_list.push_back(ei);
-            if (x.ops) {
+            const int ctp = (x.ops && use_ct) ? spectral_ct_plan(e.n) : -1;
+            if (ctp >= 0) {
+                spec_ct[ctp].push_back(ei);
+            } else if (x.ops) {
                 std::string why;
                 const int pi = real_plan(ctx->grain_plans, e.n, why);
                 if (pi < 0) return fail(ctx, MSG_E_DEVICE, "grain plan: " + why);
@@ -780,6 +799,15 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
     HIPCHK(ctx, h2d(ctx->gen_list.p, gen_list.data(), sizeof(int32_t) * gen_list.size()));
     HIPCHK(ctx, h2d(ctx->spec_small.p, spec_small.data(), sizeof(int32_t) * spec_small.size()));
     HIPCHK(ctx, h2d(ctx->spec_big.p, spec_big.data(), sizeof(int32_t) * spec_big.size()));
+    std::vector<int32_t> ct_list;
+    int32_t ct_off[SPEC_CT_PLANS + 1] = {0};
+    for (int i = 0; i < SPEC_CT_PLANS; ++i) {
+        ct_off[i] = (int32_t)ct_list.size();
+        ct_list.insert(ct_list.end(), spec_ct[i].begin(), spec_ct[i].end());
+    }
+    ct_off[SPEC_CT_PLANS] = (int32_t)ct_list.size();
+    HIPCHK(ctx, ctx->spec_ct_list.ensure(ct_list.size()));
+    HIPCHK(ctx, h2d(ctx->spec_ct_list.p, ct_list.data(), sizeof(int32_t) * ct_list.size()));
     HIPCHK(ctx, h2d(ctx->tile_begin.p, tile_begin.data(), sizeof(int32_t) * P));
     HIPCHK(ctx, h2d(ctx->fir_begin.p, fir_begin.data(), sizeof(int32_t) * P));
     HIPCHK(ctx, h2d(ctx->fir_jobs.p, fir_jobs.data(), sizeof(int2) * fir_jobs.size()));
@@ -799,6 +827,11 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
     HIPCHK(ctx, hipGetLastError());
     // ---- spectral chain ----
     stage_mark(ctx, 3, s);
+    for (int i = 0; i < SPEC_CT_PLANS; ++i)
+        if (ct_off[i + 1] > ct_off[i])
+            HIPCHK(ctx, launch_spectral_ct(i, (unsigned)(ct_off[i + 1] - ct_off[i]), s, ctx->events.p, ctx->ert.p,
+                                           ctx->prt.p, ctx->d_spec_ct_tab[i], ctx->spec_ct_list.p + ct_off[i],
+                                           ct_off[i + 1] - ct_off[i], ctx->micro.p, ctx->grain.p));
     if (!spec_small.empty())
         HIPCHK(ctx, launch_spectral(false, (unsigned)spec_small.size(), spec_small_lds, s, ctx->presets.p,
                                     ctx->events.p, ctx->ert.p, ctx->prt.p, ctx->grain_plans.dev.p, ctx->spec_small.p,

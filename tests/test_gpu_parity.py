@@ -137,3 +137,38 @@ def test_fir_transform_sizes(msgpu, irs):
         err = rms(a, ref)
         print(f"fir case {i}: rms err {err:.3e}")
         assert err <= RMS_TOL, i
+
+
+@pytest.mark.parametrize("name", ["C4", "C5"])
+def test_full_size_configs(msgpu, irs, large_renders, golden_info, name):
+    """C4 (384 kHz, 30 MHz design rate) and C5 (8.4 M frames, 4000 events) at full
+    size: every step-th frame, the first/last 8192 frames and the whole-buffer
+    rms / channel sums against the reference's render (seed 1000)."""
+    p = msgpu.config_params(name, seed=1000, irs=irs)
+    audio, _ = msgpu.render(p)
+    info = golden_info["summaries"][f"{name}_1000"]
+    assert list(audio.shape) == info["shape"]
+    step = int(large_renders[f"{name}_step"])
+    for part, ref in ((audio[::step], large_renders[f"{name}_dec"]),
+                      (audio[:8192], large_renders[f"{name}_head"]),
+                      (audio[-8192:], large_renders[f"{name}_tail"])):
+        assert rms(part, ref) <= RMS_TOL
+    a64 = audio.astype(np.float64)
+    assert abs(float(np.sqrt(np.mean(a64 ** 2))) - info["rms"]) <= RMS_TOL
+    n = audio.shape[0]
+    assert abs(float(a64[:, 0].sum()) - info["sum_l"]) <= RMS_TOL * n
+    assert abs(float(a64[:, 1].sum()) - info["sum_r"]) <= RMS_TOL * n
+
+
+@pytest.mark.parametrize("ct", ["0", "1"])
+def test_spectral_runtime_and_compile_time_plans(msgpu, irs, full_renders, monkeypatch, ct):
+    """Hot grain lengths run compile-time plans (spec_ct.h); MSGPU_SPEC_CT=0 forces
+    the runtime-plan engine.  Both must match the reference."""
+    monkeypatch.setenv("MSGPU_SPEC_CT", ct)
+    for name, cfg, kw in (("C2", "C2", {}), ("C3s1001", "C3", dict(seed=1001, out_dur_s=0.25))):
+        kw = dict(kw)
+        seed = kw.pop("seed", 1000)
+        audio, _ = msgpu.render(msgpu.config_params(cfg, seed=seed, irs=irs, **kw))
+        assert rms(audio, full_renders[f"{name}_audio"]) <= RMS_TOL, (name, ct)
+    audio, _ = msgpu.render(msgpu.merged(out_dur_s=0.5))      # factory default: n = 1500
+    assert rms(audio, full_renders["defaults_short_audio"]) <= RMS_TOL

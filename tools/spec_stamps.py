@@ -36,8 +36,8 @@ fn(buf, 16)                       # reset after warm-up
 eng.render_packed(packed, out)
 eng.torch.cuda.synchronize()
 fn(buf, 16)
-names = ["load", "twiddles", "xform step0", "xform step1", "xform step2", "xform step3",
-         "post step0", "post step1", "post step2", "post step3", "store"]
+names = ["load", "twiddles", "tilt fwd+shape", "tilt inv+env", "chain fwd+ops", "chain inv",
+         "-", "-", "-", "-", "store"]
 tot = sum(buf[i] for i in range(11))
 n_ev = sum(int(i.n_events) for i in eng.last_plan())
 for i, nm in enumerate(names):
