@@ -108,7 +108,8 @@ MSG_DEV float gen_basic_sample(const GenBasicConst& c, int j, double nrm) {
 __global__ void __launch_bounds__(GEN_T)
 k_gen_normal(const msg_preset* __restrict__ presets, const msg_event* __restrict__ events,
              const PresetRt* __restrict__ rt, const int32_t* __restrict__ ev_list, int n_list,
-             nprng::Zig z, const JumpTab* __restrict__ jt, float* __restrict__ pool) {
+             nprng::Zig z, const JumpTab* __restrict__ jt, float* __restrict__ pool,
+             double* __restrict__ pool64, const int64_t* __restrict__ off64) {
     __shared__ uint64_t s_ki[256];
     __shared__ double s_wi[256];
     const int li = blockIdx.x;
@@ -120,6 +121,8 @@ k_gen_normal(const msg_preset* __restrict__ presets, const msg_event* __restrict
     const PresetRt& r = rt[e.preset];
     const int n = e.n;
     float* out = pool + r.pool_base + e.pool_off;
+    // float64 grain chain (kernels_grain64.h): raw normals into its pool
+    double* out64 = off64 ? pool64 + off64[li] : nullptr;
 
     GenBasicConst c;
     c.mode = pr.gen_mode == MSG_GEN_FALLBACK ? MSG_GEN_NOISE_BURST : pr.gen_mode;   // MS:686
@@ -173,7 +176,10 @@ k_gen_normal(const msg_preset* __restrict__ presets, const msg_event* __restrict
         }
         if ((valid >> lane) & 1) {
             const int j = produced + __popcll(valid & ((1ULL << lane) - 1));
-            if (j < n) out[j] = gen_basic_sample(c, j, x);
+            if (j < n) {
+                if (out64) out64[j] = x;
+                else out[j] = gen_basic_sample(c, j, x);
+            }
         }
         produced += __popcll(valid);
         local = pos;

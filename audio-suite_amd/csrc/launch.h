@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 #include <vector>
 #include "rt.h"
+#include "fft64.h"
 
 constexpr int LDS_MAX = 163840;                              // 160 KiB per CU
 constexpr int SPEC_T_BIG = 512, SPEC_M_BIG = 20480;           // up to 160 KiB LDS
@@ -43,3 +44,16 @@ hipError_t launch_fir2(int M, unsigned grid, hipStream_t s, const PresetRt* rt, 
 void fft_bench_init_attrs();
 hipError_t launch_fft_bench(bool po2, unsigned grid, int lds_bytes, hipStream_t s, const RealPlan* plans, int plan,
                             int reps, float* sink);
+
+// float64 grain chain (kernels_grain64.h): one workgroup per event / per chained preset
+constexpr int G64_THREADS = 512, G64_SLOTS = 8192, G64_MAXPAR_HOST = 256;   // must match kernels_grain64.h
+void grain64_init_attrs();
+hipError_t launch_grain64(unsigned grid, int lds_bytes, hipStream_t s, const msg_preset* presets, const Ev64* ev64,
+                          const PresetRt* rt, const Real64Plan* plans, const int32_t* list, int n_list,
+                          const double* irbank, const uint8_t* imgbank, nprng::Zig z, double* micro64,
+                          double* grain64, double2* save, float* grain_pool);
+hipError_t launch_chain64(unsigned grid, int lds_bytes, hipStream_t s, const msg_preset* presets, const Ev64* ev64,
+                          const Chain64* chains, int n_chains, const Real64Plan* plans, const double* grain64,
+                          double* state, float* grain_pool);
+hipError_t launch_fft64_one(int lds_bytes, hipStream_t s, const Real64Plan* plans, int plan, int inverse,
+                            double* io);

@@ -50,13 +50,16 @@ struct DevBuf {
     void release() { if (p) hipFree(p); p = nullptr; cap = 0; }
 };
 
-struct PlanStore {
-    std::vector<RealPlan> host;          // descriptors (device pointers inside)
+template <class P>
+struct PlanStoreT {
+    std::vector<P> host;                 // descriptors (device pointers inside)
     std::vector<void*> allocs;
     std::map<int, int> by_n;
     bool dirty = false;
-    DevBuf<RealPlan> dev;
+    DevBuf<P> dev;
 };
+using PlanStore = PlanStoreT<RealPlan>;
+using Plan64Store = PlanStoreT<Real64Plan>;
 
 }  // namespace
 
@@ -92,11 +95,22 @@ struct msg_ctx {
     DevBuf<int64_t> irjobs;
     DevBuf<double> irbank;
     DevBuf<unsigned> maxbits;
+    // float64 grain chain (kernels_grain64.h)
+    Plan64Store plans64;
+    DevBuf<Ev64> ev64;
+    DevBuf<int32_t> g64_list, gen64_list;
+    DevBuf<int64_t> gen64_off;
+    DevBuf<double> micro64, grain64, state64;
+    DevBuf<double2> save64;
+    DevBuf<Chain64> chains;
+    DevBuf<uint8_t> imgbank;
     // host mirrors of the last batch
     std::vector<msg_plan_info> h_info;
     std::vector<msg_event> h_events;
     std::vector<PresetRt> h_prt;
     std::vector<int32_t> h_slot_base;
+    std::vector<Ev64> h_ev64;
+    std::vector<int32_t> h_last64;      // per preset: Ev64 index of its last event, -1 = float32 chain
     int32_t last_n = 0;
 };
 
@@ -184,11 +198,72 @@ static int real_plan(PlanStore& ps, int n, std::string& why) {
     return idx;
 }
 
-static hipError_t sync_plans(PlanStore& ps, hipStream_t s) {
+static hipError_t upload64(Plan64Store& ps, const std::vector<double>& v, const double2** out) {
+    void* d = nullptr;
+    hipError_t e = hipMalloc(&d, v.size() * sizeof(double));
+    if (e != hipSuccess) return e;
+    e = hipMemcpy(d, v.data(), v.size() * sizeof(double), hipMemcpyHostToDevice);
+    ps.allocs.push_back(d);
+    *out = reinterpret_cast<const double2*>(d);
+    return e;
+}
+
+// float64 real-FFT plan for n samples (fft64.h); returns index or -1.
+static int real64_plan(Plan64Store& ps, int n, std::string& why) {
+    auto it = ps.by_n.find(n);
+    if (it != ps.by_n.end()) return it->second;
+    Real64Plan rp;
+    memset(&rp, 0, sizeof(rp));
+    rp.n = n;
+    rp.even = (n % 2 == 0);
+    const int m = rp.even ? n / 2 : n;
+    Fft64& c = rp.c;
+    c.m = m;
+    std::vector<int> rad;
+    std::vector<double> tab;
+    if (fft64plan::factor(m, rad)) {
+        c.blue = 0;
+        c.size = m;
+    } else {
+        c.blue = 1;
+        c.size = fft64plan::next_pow2(2 * m - 1);
+        fft64plan::factor(c.size, rad);
+        std::vector<double> bs;
+        fft64plan::chirp(m, tab);
+        fft64plan::bluestein_spec(m, c.size, tab, bs);
+        if (upload64(ps, tab, &c.chirp) != hipSuccess || upload64(ps, bs, &c.bspec) != hipSuccess) {
+            why = "hip upload failed";
+            return -1;
+        }
+    }
+    if ((int)rad.size() > F64_MAXRAD) { why = "too many radix passes"; return -1; }
+    c.nrad = (int)rad.size();
+    for (size_t i = 0; i < rad.size(); ++i) c.rad[i] = rad[i];
+    fft64plan::twiddles(c.size, tab);
+    if (upload64(ps, tab, &c.tw) != hipSuccess) { why = "hip upload failed"; return -1; }
+    if (rp.even) {
+        std::vector<double> rt(2 * (size_t)(m + 1));
+        for (int k = 0; k <= m; ++k) {
+            const long double a = -2.0L * 3.14159265358979323846264338327950288L * (long double)k / (long double)n;
+            rt[2 * k] = (double)cosl(a);
+            rt[2 * k + 1] = (double)sinl(a);
+        }
+        if (upload64(ps, rt, &rp.rt) != hipSuccess) { why = "hip upload failed"; return -1; }
+    }
+    rp.cap = std::max(std::max(c.size, rp.even ? m + 1 : n), n);
+    const int idx = (int)ps.host.size();
+    ps.host.push_back(rp);
+    ps.by_n[n] = idx;
+    ps.dirty = true;
+    return idx;
+}
+
+template <class P>
+static hipError_t sync_plans(PlanStoreT<P>& ps, hipStream_t s) {
     if (!ps.dirty) return hipSuccess;
     hipError_t e = ps.dev.ensure(ps.host.size());
     if (e != hipSuccess) return e;
-    e = hipMemcpyAsync(ps.dev.p, ps.host.data(), ps.host.size() * sizeof(RealPlan), hipMemcpyHostToDevice, s);
+    e = hipMemcpyAsync(ps.dev.p, ps.host.data(), ps.host.size() * sizeof(P), hipMemcpyHostToDevice, s);
     if (e == hipSuccess) e = hipStreamSynchronize(s);
     ps.dirty = false;
     return e;
@@ -234,17 +309,51 @@ static int spec_ops(const msg_preset& p, const msg_event& e) {
     return ops;
 }
 
-static bool supported(const msg_preset& p, std::string& why) {
-    const uint32_t unsupported = MSG_F_PARTIAL_LOCK | MSG_F_CEP_WARP | MSG_F_RES_BANK | MSG_F_WAVEGUIDE |
-                                 MSG_F_EVENT_FEEDBACK | MSG_F_IMPRINT | MSG_F_MULTIBAND;
-    if (p.flags & unsupported) { why = "preset uses a stage not yet on the GPU path (flags 0x" +
-                                       std::to_string(p.flags & unsupported) + ")"; return false; }
+// Presets whose grains run the float64 chain (kernels_grain64.h): the
+// generators outside the normal-driven closed forms, and every stage whose
+// reference result hinges on float64 magnitudes or noise floors.
+static bool is_precise(const msg_preset& p) {
+    const uint32_t f64_stages = MSG_F_PARTIAL_LOCK | MSG_F_CEP_WARP | MSG_F_RES_BANK | MSG_F_WAVEGUIDE |
+                                MSG_F_EVENT_FEEDBACK | MSG_F_IMPRINT | MSG_F_MULTIBAND;
+    if (p.flags & f64_stages) return true;
     switch (p.gen_mode) {
         case MSG_GEN_GAUSSIAN_CLICK: case MSG_GEN_NOISE_BURST: case MSG_GEN_SKEWED:
-        case MSG_GEN_RESONANT: case MSG_GEN_FALLBACK: break;
-        default: why = "generator mode " + std::to_string(p.gen_mode) + " not yet on the GPU path"; return false;
+        case MSG_GEN_RESONANT: case MSG_GEN_FALLBACK: return false;
+        default: return true;
     }
+}
+static bool normal_driven(int gen_mode) {
+    return gen_mode == MSG_GEN_GAUSSIAN_CLICK || gen_mode == MSG_GEN_NOISE_BURST || gen_mode == MSG_GEN_SKEWED ||
+           gen_mode == MSG_GEN_RESONANT || gen_mode == MSG_GEN_FALLBACK;
+}
+
+static bool supported(const msg_preset& p, std::string& why) {
+    if (!is_precise(p)) return true;
+    if (p.res_modes > G64_MAXPAR_HOST && (p.flags & MSG_F_RES_BANK)) { why = "res_modes above 256"; return false; }
+    if (p.wav_count > G64_MAXPAR_HOST && p.gen_mode == MSG_GEN_WAVELET) { why = "wav_count above 256"; return false; }
+    if (p.wg_lines > G64_MAXPAR_HOST && (p.flags & MSG_F_WAVEGUIDE)) { why = "wg_lines above 256"; return false; }
     return true;
+}
+
+// Stages of the float64 chain one event runs, with the reference's own
+// length / identity guards (MS:42, 105, 119-121, 132-134, 152, 372, 389).
+static int g64_ops(const msg_preset& p, const msg_event& e) {
+    int ops = 0;
+    const int n = e.n;
+    const bool stretch_id = std::fabs(e.stretch - 1.0) < 1e-9;
+    if ((p.flags & MSG_F_BANDLIMIT) && n >= 8) ops |= G64_LOWPASS;
+    if ((p.flags & MSG_F_NL_WARP) && n >= 16) ops |= G64_WARP;
+    if ((p.flags & MSG_F_CEP_WARP) && n >= 64) ops |= G64_CEP;
+    if (p.flags & MSG_F_PARTIAL_LOCK) {
+        if (n >= 64 && !stretch_id) ops |= G64_LOCK;
+    } else if (n >= 16 && !stretch_id) {
+        ops |= G64_STRETCH;
+    }
+    if ((p.flags & MSG_F_RES_BANK) && n >= 32) ops |= G64_RES;
+    if ((p.flags & MSG_F_WAVEGUIDE) && n >= 64) ops |= G64_WG;
+    if (p.flags & MSG_F_MULTIBAND) ops |= G64_MB;
+    if (p.flags & (MSG_F_EVENT_FEEDBACK | MSG_F_IMPRINT)) ops |= G64_CHAIN;
+    return ops;
 }
 
 static void stage_mark(msg_ctx* ctx, int i, hipStream_t s) {
@@ -318,6 +427,7 @@ msg_ctx* msg_create(int device_ordinal) {
     spectral_init_attrs();
     fir_init_attrs();
     fft_bench_init_attrs();
+    grain64_init_attrs();
     return ctx.release();
 }
 
@@ -344,6 +454,11 @@ void msg_destroy(msg_ctx* ctx) {
     ctx->mono_a.release(); ctx->mono_y.release(); ctx->hspec.release(); ctx->irspec.release();
     ctx->irjobs.release(); ctx->irbank.release();
     ctx->maxbits.release();
+    for (void* p : ctx->plans64.allocs) hipFree(p);
+    ctx->plans64.dev.release();
+    ctx->ev64.release(); ctx->g64_list.release(); ctx->gen64_list.release(); ctx->gen64_off.release();
+    ctx->micro64.release(); ctx->grain64.release(); ctx->state64.release(); ctx->save64.release();
+    ctx->chains.release(); ctx->imgbank.release();
     delete ctx;
 }
 
@@ -492,6 +607,27 @@ int msg_bench_fft(msg_ctx* ctx, int32_t n, int32_t reps, int32_t blocks, float* 
     return MSG_OK;
 }
 
+int msg_fft64(msg_ctx* ctx, int32_t n, int32_t inverse, const double* in, double* out) {
+    if (!ctx || !in || !out || n < 2) return MSG_E_ARG;
+    HIPCHK(ctx, hipSetDevice(ctx->device));
+    std::string why;
+    const int pi = real64_plan(ctx->plans64, n, why);
+    if (pi < 0) return fail(ctx, MSG_E_DEVICE, why);
+    const Real64Plan rp = ctx->plans64.host[pi];
+    if (rp.cap > G64_SLOTS) return fail(ctx, MSG_E_UNSUPPORTED, "transform exceeds the LDS float64 engine");
+    HIPCHK(ctx, sync_plans(ctx->plans64, nullptr));
+    const int K = n / 2 + 1;
+    const size_t cnt = (size_t)std::max(n, 2 * K);
+    double* io = nullptr;
+    HIPCHK(ctx, hipMalloc(&io, cnt * sizeof(double)));
+    hipError_t e = hipMemcpy(io, in, (inverse ? 2 * K : n) * sizeof(double), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = launch_fft64_one(rp.cap * 16, nullptr, ctx->plans64.dev.p, pi, inverse ? 1 : 0, io);
+    if (e == hipSuccess) e = hipMemcpy(out, io, (inverse ? n : 2 * K) * sizeof(double), hipMemcpyDeviceToHost);
+    hipFree(io);
+    HIPCHK(ctx, e);
+    return MSG_OK;
+}
+
 int msg_last_plan(msg_ctx* ctx, msg_plan_info* info, int32_t n_presets) {
     if (!ctx || !info) return MSG_E_ARG;
     if (n_presets > ctx->last_n) return fail(ctx, MSG_E_ARG, "n_presets exceeds last batch");
@@ -522,6 +658,14 @@ int msg_last_meta(msg_ctx* ctx, int32_t preset, double* micro, double* grain, in
     std::vector<float> tmp(e.n);
     const int64_t off = ctx->h_prt[preset].pool_base + e.pool_off;
     HIPCHK(ctx, hipDeviceSynchronize());
+    const int32_t l64 = ctx->h_last64.empty() ? -1 : ctx->h_last64[preset];
+    if (l64 >= 0) {   // float64 chain: micro_last / grain_last kept in float64
+        const int64_t o64 = ctx->h_ev64[l64].off64;
+        if (micro) HIPCHK(ctx, hipMemcpy(micro, ctx->micro64.p + o64, e.n * sizeof(double), hipMemcpyDeviceToHost));
+        if (grain) HIPCHK(ctx, hipMemcpy(grain, ctx->grain64.p + o64, e.n * sizeof(double), hipMemcpyDeviceToHost));
+        *n = e.n;
+        return MSG_OK;
+    }
     if (micro) {
         HIPCHK(ctx, hipMemcpy(tmp.data(), ctx->micro.p + off, e.n * sizeof(float), hipMemcpyDeviceToHost));
         for (int i = 0; i < e.n; ++i) micro[i] = tmp[i];
@@ -538,7 +682,6 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
                      const double* const* irs, const int64_t* ir_lens, int32_t n_irs,
                      const uint8_t* const* images, const int32_t* img_h, const int32_t* img_w,
                      int32_t n_images, float* out_dev, const int64_t* out_offsets, void* stream) {
-    (void)images; (void)img_h; (void)img_w; (void)n_images;
     if (!ctx || !presets || P <= 0 || !out_dev || !out_offsets) return fail(ctx, MSG_E_ARG, "bad arguments");
     hipStream_t s = (hipStream_t)stream;
     HIPCHK(ctx, hipSetDevice(ctx->device));
@@ -619,6 +762,20 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
     std::map<std::pair<int, int>, int64_t> ir_spec_of;   // (IR index, N) -> offset
     std::vector<int2> fjobs_by[5];                        // FIR output blocks per transform size
     std::vector<int64_t> ir_jobs;                         // [ir_off, ir_len, plan, out_off] per job
+    // float64 grain chain records
+    std::vector<Ev64> ev64;
+    std::vector<int32_t> gen64_list;                      // normal-driven float64 events (event slots)
+    std::vector<int64_t> gen64_off;                       // their raw-normal offsets in micro64
+    std::vector<Chain64> chains;
+    std::vector<int32_t> last64(P, -1);
+    std::vector<uint8_t> imgbank;
+    std::vector<int64_t> img_off(std::max(n_images, 1), 0);
+    for (int i = 0; i < n_images; ++i) {
+        img_off[i] = (int64_t)imgbank.size();
+        imgbank.insert(imgbank.end(), images[i], images[i] + (int64_t)img_h[i] * img_w[i]);
+    }
+    int64_t sum64 = 0, save_sum = 0, state_sum = 0;
+    int g64_cap = 0;
     for (int p = 0; p < P; ++p) {
         const msg_preset& pr = presets[p];
         const msg_plan_info& inf = info[p];
@@ -634,6 +791,16 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
         r.n_taps = (pr.flags & MSG_F_ER_CLOUD) ? std::max(1, pr.er_taps) : 0;
         r.tile_begin = tiles;
         r.max_n = inf.max_n;
+        // generator sources (MS:333-362)
+        r.frag_len = flen[p];
+        r.frag_off = (pr.ir_frag >= 0 && pr.ir_frag < n_irs) ? ir_off[pr.ir_frag] : 0;
+        if (pr.gen_mode == MSG_GEN_IMAGE && pr.image >= 0) {
+            if (pr.image >= n_images || !images) return fail(ctx, MSG_E_ARG, "bad image index");
+            r.img_off = img_off[pr.image];
+            r.img_h = img_h[pr.image];
+            r.img_w = img_w[pr.image];
+            if (r.img_h <= 0 || r.img_w <= 0) return fail(ctx, MSG_E_ARG, "empty image");
+        }
         // ADSR (MS:173-177); A > n raises ValueError in the reference (MS:182)
         const double sr = (double)pr.base_sr;
         const int64_t A = std::max<int64_t>(0, (int64_t)std::nearbyint(sr * pr.env_a / 1000.0));
@@ -721,6 +888,72 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
         pool += (inf.pool_len + 3) & ~int64_t(3);   // 16-byte aligned grain regions (float4 loads)
         ysum += (inf.out_n + 3) & ~int64_t(3);   // keep every mono region 16-byte aligned
         // events
+        const bool precise = is_precise(pr);
+        if (precise && inf.n_events > 0) {
+            const bool chained = (pr.flags & (MSG_F_EVENT_FEEDBACK | MSG_F_IMPRINT)) != 0;
+            if (chained) {
+                Chain64 c;
+                memset(&c, 0, sizeof(c));
+                c.preset = p;
+                c.ev_begin = (int32_t)ev64.size();
+                c.n_events = inf.n_events;
+                c.prev_off = state_sum;
+                c.mem_off = state_sum + ((inf.max_n + 1) & ~1);
+                state_sum += ((inf.max_n + 1) & ~1) + ((inf.max_n / 2 + 2) & ~1);
+                chains.push_back(c);
+            }
+            for (int k = 0; k < inf.n_events; ++k) {
+                const int ei = slot_base[p] + k;
+                const msg_event& e = ctx->h_events[ei];
+                memset(&ert[ei], 0, sizeof(EventRt));
+                Ev64 v;
+                memset(&v, 0, sizeof(v));
+                std::string why;
+                v.plan = real64_plan(ctx->plans64, e.n, why);
+                if (v.plan < 0) return fail(ctx, MSG_E_DEVICE, "float64 grain plan: " + why);
+                const Real64Plan& gp = ctx->plans64.host[v.plan];
+                if (gp.cap > G64_SLOTS)
+                    return fail(ctx, MSG_E_UNSUPPORTED, "grain of " + std::to_string(e.n) +
+                                " samples exceeds the LDS-resident float64 chain (8192 complex slots)");
+                g64_cap = std::max(g64_cap, gp.cap);
+                v.ops = g64_ops(pr, e);
+                v.n = e.n;
+                v.n0 = msgplan::grain_len(e.gen_sr, pr.micro_ms, 16);
+                v.gen_sr = e.gen_sr;
+                v.preset = p;
+                v.index = e.index;
+                v.ei = ei;
+                v.off64 = sum64;
+                v.grain_off = r.pool_base + e.pool_off;
+                v.cutoff_gen = e.cutoff_out * e.ufac;
+                v.stretch = e.stretch;
+                if (v.ops & G64_CEP) { v.save_off = save_sum; save_sum += e.n / 2 + 1; }
+                if (v.ops & G64_LOCK) {
+                    const int nb = e.n / 2;               // candidate bins 1..n/2
+                    const int cnt = pr.pl_top_n > 0 ? std::min(pr.pl_top_n, nb)
+                                                    : (pr.pl_top_n == 0 ? nb : std::max(0, nb + pr.pl_top_n));
+                    if (cnt > G64_MAXPAR_HOST)
+                        return fail(ctx, MSG_E_UNSUPPORTED, "partial lock of more than 256 peaks");
+                }
+                if (pr.gen_mode == MSG_GEN_WAVELET) {
+                    // morlet_atom is max(16, round(..)) long, the grain max(128, ..): shorter
+                    // atoms do not broadcast into the grain (MS:319, 166, 329)
+                    const int na = msgplan::grain_len(e.gen_sr, pr.micro_ms, 16);
+                    if (na < e.n)
+                        return fail(ctx, MSG_E_VALUE, "operands could not be broadcast together with shapes (" +
+                                                          std::to_string(e.n) + ",) (" + std::to_string(na) +
+                                                          ",) (" + std::to_string(e.n) + ",)");
+                }
+                if (normal_driven(pr.gen_mode)) {
+                    gen64_list.push_back(ei);
+                    gen64_off.push_back(sum64);
+                }
+                sum64 += (e.n + 1) & ~1;
+                last64[p] = (int32_t)ev64.size();
+                ev64.push_back(v);
+            }
+            continue;
+        }
         for (int k = 0; k < inf.n_events; ++k) {
             const int ei = slot_base[p] + k;
             const msg_event& e = ctx->h_events[ei];
@@ -763,6 +996,19 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
     }
     HIPCHK(ctx, sync_plans(ctx->grain_plans, s));
     HIPCHK(ctx, sync_plans(ctx->fir_plans, s));
+    HIPCHK(ctx, sync_plans(ctx->plans64, s));
+    std::vector<int32_t> g64_list(ev64.size());
+    for (size_t i = 0; i < ev64.size(); ++i) g64_list[i] = (int32_t)i;
+    HIPCHK(ctx, ctx->ev64.ensure(ev64.size()));
+    HIPCHK(ctx, ctx->g64_list.ensure(g64_list.size()));
+    HIPCHK(ctx, ctx->gen64_list.ensure(gen64_list.size()));
+    HIPCHK(ctx, ctx->gen64_off.ensure(gen64_off.size()));
+    HIPCHK(ctx, ctx->micro64.ensure(sum64));
+    HIPCHK(ctx, ctx->grain64.ensure(sum64));
+    HIPCHK(ctx, ctx->save64.ensure(save_sum));
+    HIPCHK(ctx, ctx->state64.ensure(state_sum));
+    HIPCHK(ctx, ctx->chains.ensure(chains.size()));
+    HIPCHK(ctx, ctx->imgbank.ensure(imgbank.size()));
     HIPCHK(ctx, ctx->ert.ensure(nslots));
     HIPCHK(ctx, ctx->prt.ensure(P));
     HIPCHK(ctx, ctx->gen_list.ensure(gen_list.size()));
@@ -817,13 +1063,24 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
     HIPCHK(ctx, h2d(ctx->irbank.p, irbank.data(), sizeof(double) * irbank.size()));
     HIPCHK(ctx, h2d(ctx->irjobs.p, ir_jobs.data(), sizeof(int64_t) * ir_jobs.size()));
     HIPCHK(ctx, hipMemsetAsync(ctx->maxbits.p, 0, sizeof(unsigned) * P, s));
+    HIPCHK(ctx, h2d(ctx->ev64.p, ev64.data(), sizeof(Ev64) * ev64.size()));
+    HIPCHK(ctx, h2d(ctx->g64_list.p, g64_list.data(), sizeof(int32_t) * g64_list.size()));
+    HIPCHK(ctx, h2d(ctx->gen64_list.p, gen64_list.data(), sizeof(int32_t) * gen64_list.size()));
+    HIPCHK(ctx, h2d(ctx->gen64_off.p, gen64_off.data(), sizeof(int64_t) * gen64_off.size()));
+    HIPCHK(ctx, h2d(ctx->chains.p, chains.data(), sizeof(Chain64) * chains.size()));
+    HIPCHK(ctx, h2d(ctx->imgbank.p, imgbank.data(), imgbank.size()));
 
     // ---- generate ----
     stage_mark(ctx, 2, s);
     if (!gen_list.empty())
         hipLaunchKernelGGL(k_gen_normal, dim3((unsigned)gen_list.size()), dim3(GEN_T), 0, s,
                            ctx->presets.p, ctx->events.p, ctx->prt.p, ctx->gen_list.p, (int)gen_list.size(),
-                           ctx->dzig, ctx->d_jump, ctx->micro.p);
+                           ctx->dzig, ctx->d_jump, ctx->micro.p, (double*)nullptr, (const int64_t*)nullptr);
+    HIPCHK(ctx, hipGetLastError());
+    if (!gen64_list.empty())   // raw normals of the float64 chain's normal-driven generators
+        hipLaunchKernelGGL(k_gen_normal, dim3((unsigned)gen64_list.size()), dim3(GEN_T), 0, s,
+                           ctx->presets.p, ctx->events.p, ctx->prt.p, ctx->gen64_list.p, (int)gen64_list.size(),
+                           ctx->dzig, ctx->d_jump, ctx->micro.p, ctx->micro64.p, (const int64_t*)ctx->gen64_off.p);
     HIPCHK(ctx, hipGetLastError());
     // ---- spectral chain ----
     stage_mark(ctx, 3, s);
@@ -840,6 +1097,15 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
         HIPCHK(ctx, launch_spectral(true, (unsigned)spec_big.size(), spec_big_lds, s, ctx->presets.p,
                                     ctx->events.p, ctx->ert.p, ctx->prt.p, ctx->grain_plans.dev.p, ctx->spec_big.p,
                                     (int)spec_big.size(), ctx->micro.p, ctx->grain.p));
+    if (!ev64.empty())
+        HIPCHK(ctx, launch_grain64((unsigned)ev64.size(), g64_cap * 16, s, ctx->presets.p, ctx->ev64.p, ctx->prt.p,
+                                   ctx->plans64.dev.p, ctx->g64_list.p, (int)ev64.size(), ctx->irbank.p,
+                                   ctx->imgbank.p, ctx->dzig, ctx->micro64.p, ctx->grain64.p, ctx->save64.p,
+                                   ctx->grain.p));
+    if (!chains.empty())
+        HIPCHK(ctx, launch_chain64((unsigned)chains.size(), g64_cap * 16, s, ctx->presets.p, ctx->ev64.p,
+                                   ctx->chains.p, (int)chains.size(), ctx->plans64.dev.p, ctx->grain64.p,
+                                   ctx->state64.p, ctx->grain.p));
     // ---- overlap-add x ADSR ----
     stage_mark(ctx, 4, s);
     hipLaunchKernelGGL(k_ola_env, dim3((unsigned)tiles), dim3(OLA_T), 0, s, ctx->events.p, ctx->prt.p,
@@ -882,6 +1148,8 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
     ctx->h_info = info;
     ctx->h_prt = prt;
     ctx->h_slot_base = slot_base;
+    ctx->h_ev64 = ev64;
+    ctx->h_last64 = last64;
     ctx->last_n = P;
     if (ctx->profiling) {
         HIPCHK(ctx, hipEventSynchronize(ctx->ev[7]));

@@ -56,6 +56,12 @@ MSG_HD int32_t event_grain_len(const msg_preset& p, int32_t gen_sr, int64_t ir_f
             return grain_len(gen_sr, p.micro_ms, 128);
         case MSG_GEN_IR_FRAGMENT:
             return grain_len(gen_sr, p.micro_ms, ir_frag_len < 32 ? 16 : 64);
+        case MSG_GEN_CRACKLE: {
+            // np.convolve(x, ker, "same") returns max(len(x), len(ker)) samples (MS:280-281)
+            const int32_t n0 = grain_len(gen_sr, p.micro_ms, 16);
+            const int32_t K = p.crackle_kernel > 8 ? p.crackle_kernel : 8;
+            return n0 > K ? n0 : K;
+        }
         default:
             return grain_len(gen_sr, p.micro_ms, 16);
     }

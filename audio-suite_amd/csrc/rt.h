@@ -44,6 +44,10 @@ struct PresetRt {
     float bess[25];        // J_m(0.9 w), m = -12..12
     float drive, peak;
     int32_t pad2;
+    // generator sources: IR fragment (float64 IR bank) and image (uint8 bank)
+    int64_t frag_off, frag_len;
+    int64_t img_off;
+    int32_t img_h, img_w;
 };
 
 // Per-event spectral work descriptor (host-built after planning).
@@ -59,6 +63,36 @@ struct EventRt {
 };
 enum : int32_t {
     SPEC_TILT_NOISE = 1, SPEC_TILT_SKEW = 2, SPEC_LOWPASS = 4, SPEC_STRETCH = 8, SPEC_WARP = 16,
+};
+
+// float64 grain chain (kernels_grain64.h): per-event and per-preset records
+struct Ev64 {
+    int32_t plan;          // Real64Plan index for n
+    int32_t ops;           // G64_* stages
+    int32_t n;             // grain length through the chain
+    int32_t n0;            // generator's own length (crackle: grain is max(n0, kernel))
+    int32_t gen_sr;
+    int32_t preset;        // batch index
+    int32_t index;         // event i (generator seed = seed + i)
+    int32_t ei;            // global event slot
+    int64_t off64;         // offset in the float64 micro/grain pools (doubles)
+    int64_t save_off;      // cepstral warp: saved spectrum (double2 slots)
+    int64_t grain_off;     // float grain pool offset (pool_base + pool_off)
+    double cutoff_gen;     // band-limit cutoff at the design rate (MS:691)
+    double stretch;        // stretch lane value (MS:637)
+};
+enum : int32_t {
+    G64_LOWPASS = 1, G64_WARP = 2, G64_CEP = 4, G64_LOCK = 8, G64_STRETCH = 16,
+    G64_RES = 32, G64_WG = 64, G64_MB = 128, G64_CHAIN = 256,
+    G64_SPEC = G64_LOWPASS | G64_WARP | G64_CEP | G64_LOCK | G64_STRETCH,
+};
+
+struct Chain64 {
+    int32_t preset;
+    int32_t ev_begin, n_events;   // Ev64 indices [ev_begin, ev_begin + n_events)
+    int32_t pad;
+    int64_t prev_off;             // previous grain (doubles, max_n)
+    int64_t mem_off;              // imprint memory (doubles, max_n/2 + 1)
 };
 
 constexpr int GEN_T = 64;          // one wave per event

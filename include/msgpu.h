@@ -157,6 +157,11 @@ int msg_stage_times(msg_ctx* ctx, float* ms, int32_t n);
  * forward+inverse real transforms of length n; *ms receives the device time. */
 int msg_bench_fft(msg_ctx* ctx, int32_t n, int32_t reps, int32_t blocks, float* ms);
 
+/* One float64 real transform on the device engine of the float64 grain chain
+ * (np.fft.rfft / irfft semantics, MS:46 ...): inverse = 0 maps n real samples
+ * to n/2+1 interleaved complex bins; inverse = 1 maps them back.  For tests. */
+int msg_fft64(msg_ctx* ctx, int32_t n, int32_t inverse, const double* in, double* out);
+
 /* ---- NumPy stream primitives on the host (tests pin them against NumPy) ---- */
 /* Raw PCG64 outputs of np.random.default_rng(seed).bit_generator.random_raw(n). */
 int msg_rng_raw(uint64_t seed, uint64_t* out, int64_t n);

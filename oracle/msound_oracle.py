@@ -629,7 +629,10 @@ def event_grain_len(p: dict, gen_sr: int) -> int:
     """Length every grain keeps through the chain, by generator mode (MS:650-686)."""
     mode = p["gen_mode"]
     micro_ms = float(p["micro_ms"])
-    if mode in BASIC_MODES or mode == "Crackle / corona":
+    if mode == "Crackle / corona":
+        # np.convolve(x, ker, "same") is max(len(x), len(ker)) long (MS:280-281)
+        return max(grain_len(gen_sr, micro_ms), max(8, int(p["crackle_kernel"])))
+    if mode in BASIC_MODES:
         return grain_len(gen_sr, micro_ms)
     if mode in ("Stick–slip friction", "Micro-chaos", "Image scanline"):
         return grain_len(gen_sr, micro_ms, 64)

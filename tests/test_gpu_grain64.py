@@ -1,0 +1,206 @@
+"""GPU parity of the float64 grain chain (kernels_grain64.h) against the oracle.
+
+Every generator outside the normal-driven closed forms, every tier-B spectral
+stage, the physics models, the multi-band unfold and the feedback/imprint
+chain, at grain lengths that exercise each FFT path: radix-only even lengths,
+radix-11/13 lengths, Bluestein even lengths (m = n/2 with a prime factor > 13)
+and odd lengths (Bluestein on n).  Tolerance: 1e-5 RMS over the (out_n, 2)
+buffer (north star), float32 output of a float64 chain.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+RMS_TOL = 1e-5
+
+
+def rms(a, b):
+    a = np.asarray(a, dtype=np.float64)
+    b = np.asarray(b, dtype=np.float64)
+    assert a.shape == b.shape, (a.shape, b.shape)
+    return float(np.sqrt(np.mean((a - b) ** 2)))
+
+
+@pytest.fixture(scope="module")
+def m():
+    import msgpu
+    return msgpu
+
+
+@pytest.fixture(scope="module")
+def O():
+    from oracle import msound_oracle
+    return msound_oracle
+
+
+def base(m, **kw):
+    p = m.merged(base_sr=48000, out_dur_s=0.2, event_process="Poisson", grains_per_sec=40.0, seed=77)
+    p.update(kw)
+    return p
+
+
+# micro_ms -> n at 48 kHz x unfold 25 (1.2 MHz): 1.25 -> 1500 (radix), 1.9 -> 2280 (m = 1140 = 4*3*5*19,
+# Bluestein), 1.0558333 -> 1267 (odd, 7*181), 1.1 -> 1320 (radix 11), 1.3 -> 1560 (radix 13)
+LENGTHS = {"radix": 1.25, "blue_even": 1.9, "odd": 1.0558333, "r11": 1.1, "r13": 1.3}
+
+GEN_MODES = ["Dust impulses", "Crackle / corona", "Stick–slip friction", "Micro-chaos",
+             "Wavelet atoms", "IR fragment", "Image scanline"]
+
+
+class fft_rounding:
+    """Evaluate every np.fft.rfft/irfft as F(s x) / s (s > 0: the same float64
+    transform with different rounding), or rfft as rfft(irfft(rfft(x)))
+    (s < 0: a ~1.4x larger rounding floor) -- to measure the reference
+    algorithm's own spread (tools/gen_spread.py does the same for the presets)."""
+
+    def __init__(self, s):
+        self.s = s
+
+    def __enter__(self):
+        self.r0, self.i0 = np.fft.rfft, np.fft.irfft
+        s, r0, i0 = self.s, self.r0, self.i0
+        if s < 0:
+            np.fft.rfft = lambda x, n=None: r0(i0(r0(x, n=n), n=(np.asarray(x).shape[-1] if n is None else n)), n=n)
+            return
+        np.fft.rfft = lambda x, n=None: r0(np.asarray(x) * s, n=n) / s
+        np.fft.irfft = lambda X, n=None: i0(np.asarray(X) * s, n=n) / s
+
+    def __exit__(self, *exc):
+        np.fft.rfft, np.fft.irfft = self.r0, self.i0
+
+
+def check(m, O, params, tol=RMS_TOL):
+    """Device vs oracle within 1e-5 RMS.  Presets with the cepstral warp are
+    held to the reference algorithm's own float64 rounding spread instead
+    (DESIGN.md section 2): its log(|X| + 1e-12) reads the ~1e-13 rounding floor
+    of band-limited bins, so any other float64 evaluation moves the output."""
+    outs = m.render_batch(params)
+    for i, (p, a) in enumerate(zip(params, outs)):
+        ref, _ = O.render(p)
+        err = rms(a, ref)
+        lim = tol
+        if p["cep_warp_on"]:
+            spread = 0.0
+            for sc in (3.0, 5.0, -1.0):
+                with fft_rounding(sc):
+                    alt, _ = O.render(p)
+                spread = max(spread, rms(alt, ref))
+            lim = max(tol, 1.5 * spread)
+        print(f"case {i}: {p['gen_mode']} n-ms {p['micro_ms']}: rms {err:.3e} (limit {lim:.3e})")
+        assert err <= lim, (i, p["gen_mode"], err, lim)
+
+
+@pytest.mark.parametrize("mode", GEN_MODES)
+def test_generators(m, O, irs, full_renders, mode):
+    params = [base(m, gen_mode=mode, micro_ms=ms, time_unfold=25.0, _ir_audio=irs["tiny_room_ir"],
+                   _img_gray=full_renders["image_gray"], seed=100 + i)
+              for i, ms in enumerate(LENGTHS.values())]
+    check(m, O, params)
+
+
+def test_generators_without_sources(m, O):
+    """IR fragment without an IR and image scanline without an image give zero grains (MS:335, 353)."""
+    check(m, O, [base(m, gen_mode="IR fragment", _ir_audio=None, er_cloud_on=False),
+                 base(m, gen_mode="Image scanline", _img_gray=None)])
+
+
+def test_crackle_kernel_longer_than_grain(m, O):
+    """n = 60 < kernel 64: np.convolve 'same' returns 64 samples and the offset draw uses
+    the 64-sample grain (MS:280, 750)."""
+    check(m, O, [base(m, gen_mode="Crackle / corona", time_unfold=1.0, crackle_kernel=64, seed=5),
+                 base(m, gen_mode="Crackle / corona", time_unfold=1.0, crackle_kernel=200, seed=6)])
+
+
+STAGES = {
+    "cep": dict(cep_warp_on=True, cep_factor=1.2),
+    "cep_down": dict(cep_warp_on=True, cep_factor=0.8),
+    "lock": dict(partial_lock_on=True, partial_stretch=1.7),
+    "lock_wide": dict(partial_lock_on=True, partial_stretch=0.6, pl_top_n=200, pl_neigh=16),
+    "lock_narrow": dict(partial_lock_on=True, partial_stretch=2.5, pl_top_n=4, pl_neigh=0),
+    "res": dict(res_bank_on=True),
+    "wg": dict(wg_on=True),
+    "mb": dict(unfold_mode="Multi-band"),
+    "mb_hard": dict(unfold_mode="Multi-band", mb_roll=0.0),
+    "warp_stretch": dict(nl_warp_on=True, nl_warp_power=0.8, partial_stretch=1.3),
+}
+
+
+@pytest.mark.parametrize("stage", sorted(STAGES))
+def test_spectral_and_physics_stages(m, O, stage):
+    params = [base(m, gen_mode=g, micro_ms=ms, time_unfold=25.0, seed=200 + i, **STAGES[stage])
+              for i, (g, ms) in enumerate(zip(["Noise burst", "Resonant strike", "Gaussian click",
+                                                "Skewed transient", "Wavelet atoms"], LENGTHS.values()))]
+    check(m, O, params)
+
+
+@pytest.mark.parametrize("chain", ["feedback", "imprint", "both"])
+def test_feedback_imprint_chain(m, O, chain):
+    kw = {"feedback": dict(event_feedback_on=True),
+          "imprint": dict(spectral_imprint_on=True),
+          "both": dict(event_feedback_on=True, spectral_imprint_on=True, cep_warp_on=True)}[chain]
+    params = [base(m, gen_mode=g, micro_ms=ms, time_unfold=25.0, grains_per_sec=80.0, seed=300 + i, **kw)
+              for i, (g, ms) in enumerate(zip(["Noise burst", "Crackle / corona", "Wavelet atoms"],
+                                              [1.25, 1.9, 1.0558333]))]
+    check(m, O, params)
+
+
+def test_chain_with_changing_grain_length(m, O):
+    """bp_unfold changes n per event: the imprint memory resets on a size change
+    and feedback mixes over the common prefix (MS:575-576, 733)."""
+    check(m, O, [base(m, gen_mode="Noise burst", time_unfold=20.0, grains_per_sec=60.0, bp_unfold="0:10, 0.2:30",
+                      event_feedback_on=True, spectral_imprint_on=True, seed=9)])
+
+
+def test_float64_chain_meta(m, O, irs):
+    """micro_last / grain_last of a float64-chain preset (MS:688, 729)."""
+    p = base(m, gen_mode="Wavelet atoms", partial_lock_on=True, partial_stretch=1.4, event_feedback_on=True,
+             seed=41)
+    _, meta = m.render(p)
+    _, ref = O.render(p)
+    for k in ("micro_last", "grain_last"):
+        assert meta[k].shape == ref[k].shape
+        assert rms(meta[k], ref[k]) <= 1e-9 * max(1.0, float(np.max(np.abs(ref[k]))))
+
+
+def test_float64_chain_errors(m):
+    with pytest.raises(ValueError):          # 60-sample atoms do not broadcast into a 128-sample grain
+        m.render(base(m, gen_mode="Wavelet atoms", time_unfold=1.0))
+    with pytest.raises(NotImplementedError):  # 24000-sample grain exceeds the LDS float64 chain
+        m.render(base(m, base_sr=192000, time_unfold=100.0, cep_warp_on=True, out_dur_s=0.05))
+
+
+def _fft64(m, n, inverse, data):
+    import ctypes as C
+    from msgpu import _lib as L
+    from msgpu.engine import default_engine
+    eng = default_engine(0)
+    src = np.ascontiguousarray(data, dtype=np.float64)
+    out = np.zeros(n if inverse else 2 * (n // 2 + 1), dtype=np.float64)
+    L.check(L.lib().msg_fft64(eng._ctx, n, 1 if inverse else 0, src.ctypes.data_as(C.POINTER(C.c_double)),
+                              out.ctypes.data_as(C.POINTER(C.c_double))), eng._ctx)
+    return out if inverse else out[0::2] + 1j * out[1::2]
+
+
+@pytest.mark.parametrize("n", [16, 60, 64, 1267, 1320, 1439, 1440, 1500, 1560, 2280, 2401, 4095, 5400, 8190, 8192])
+def test_fft64_engine_vs_numpy(m, n):
+    """The float64 engine's rfft / irfft against NumPy's pocketfft: radix-only,
+    radix 11/13, Bluestein even/odd and prime lengths.  Also reports the
+    rounding floor a masked-spectrum round trip leaves (what the cepstral warp
+    reads) next to NumPy's."""
+    rng = np.random.default_rng(n)
+    x = rng.standard_normal(n)
+    X = _fft64(m, n, False, x)
+    Xr = np.fft.rfft(x)
+    assert np.max(np.abs(X - Xr)) <= 1e-12 * np.max(np.abs(Xr)), n
+    y = _fft64(m, n, True, np.stack([Xr.real, Xr.imag], 1).ravel())
+    assert np.max(np.abs(y - x)) <= 1e-13 * np.max(np.abs(x)) * np.log2(n), n
+    # round-trip floor of a spectrum with its top quarter masked
+    Xm = Xr.copy()
+    Xm[3 * Xm.size // 4:] = 0
+    xm = np.fft.irfft(Xm, n)
+    ours = _fft64(m, n, False, _fft64(m, n, True, np.stack([Xm.real, Xm.imag], 1).ravel()))
+    ref = np.fft.rfft(xm)
+    fo = np.sqrt(np.mean(np.abs(ours[3 * Xm.size // 4:]) ** 2))
+    fr = np.sqrt(np.mean(np.abs(ref[3 * Xm.size // 4:]) ** 2))
+    print(f"n={n}: masked round-trip floor rms device {fo:.3e}  numpy {fr:.3e}  ratio {fo / max(fr, 1e-300):.2f}")

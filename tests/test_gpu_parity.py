@@ -67,22 +67,48 @@ def test_defaults_gaussian_click(msgpu, full_renders):
     assert rms(audio, full_renders["defaults_short_audio"]) <= RMS_TOL
 
 
-def test_supported_presets(msgpu, full_renders, irs, golden_info):
-    done = 0
+def test_all_shipped_presets(msgpu, full_renders, irs, golden_info):
+    """All 27 shipped presets (0.5 s, tiny-room IR, the golden image) against the
+    reference's renders — every generator, spectral stage, physics model,
+    multi-band unfold and feedback/imprint chain on the device path."""
+    import json
+    import os
+    spread = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "render_spread.json")))["spread"]
+    errs, lims = {}, {}
     for name in golden_info["presets"]:
         p = msgpu.merged(golden_info["preset_params"][name])
         p["out_dur_s"] = 0.5
         p["_ir_audio"] = irs["tiny_room_ir"]
         p["_img_gray"] = full_renders["image_gray"]
-        try:
-            audio, _ = msgpu.render(p)
-        except NotImplementedError:
-            continue       # stage not yet on the GPU path: must fail loudly, never approximate
-        err = rms(audio, full_renders[f"preset_{name}_audio"])
-        print(f"preset {name}: rms err {err:.3e}")
-        assert err <= RMS_TOL, name
-        done += 1
-    print("presets rendered on GPU:", done)
+        audio, _ = msgpu.render(p)
+        errs[name] = rms(audio, full_renders[f"preset_{name}_audio"])
+        # ill-conditioned presets (cepstral warp, imprint under a cutoff lane): the
+        # reference's own output moves by `spread` under
+        # float64 rounding changes (AVX2 vs AVX-512 NumPy, FFT rounding); hold the
+        # device to that band (tools/gen_spread.py, DESIGN.md section 2)
+        lims[name] = max(RMS_TOL, 1.5 * spread[name]) if name in spread else RMS_TOL
+        print(f"preset {name}: rms err {errs[name]:.3e} (limit {lims[name]:.3e})")
+    assert len(errs) == 27
+    bad = {k: v for k, v in errs.items() if not v <= lims[k]}
+    assert not bad, bad
+
+
+def test_all_presets_one_batch(msgpu, full_renders, irs, golden_info):
+    """The 27 presets as one device batch give the single-render results."""
+    params = []
+    for name in golden_info["presets"]:
+        p = msgpu.merged(golden_info["preset_params"][name])
+        p["out_dur_s"] = 0.5
+        p["_ir_audio"] = irs["tiny_room_ir"]
+        p["_img_gray"] = full_renders["image_gray"]
+        params.append(p)
+    import json
+    import os
+    spread = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "render_spread.json")))["spread"]
+    outs = msgpu.render_batch(params)
+    for name, a in zip(golden_info["presets"], outs):
+        lim = max(RMS_TOL, 1.5 * spread[name]) if name in spread else RMS_TOL
+        assert rms(a, full_renders[f"preset_{name}_audio"]) <= lim, name
 
 
 def test_batch_equals_single_and_oracle(msgpu, irs):
