@@ -297,7 +297,7 @@ MSG_DEV StereoTile stereo_stage(const PresetRt& r, const float* __restrict__ y, 
     st.t0 = (int)t0;
     st.cnt = (int)(t0 + ST_TILE < n ? ST_TILE : n - t0);
     st.lbase = mod_n(t0 - r.dl, n);
-    if (r.stereo_fir) {
+    if (r.stereo_fir == 1) {
         const int b0 = mod_n(t0 + r.dr - 24, n);
         float v[ST_WPER];
 #pragma unroll
@@ -327,7 +327,7 @@ MSG_DEV float stereo_r(const PresetRt& r, const float* w, int u) {
 
 __global__ void __launch_bounds__(ST_T)
 k_stereo_max(const PresetRt* __restrict__ rt, const int32_t* __restrict__ st_begin, int n_presets,
-             const float* __restrict__ ybuf, unsigned* __restrict__ maxbits) {
+             const float* __restrict__ ybuf, const float* __restrict__ rbuf, unsigned* __restrict__ maxbits) {
     __shared__ float w[ST_TILE + 48];
     __shared__ float wm[ST_T / 64];
     const int b = blockIdx.x;
@@ -347,7 +347,8 @@ k_stereo_max(const PresetRt* __restrict__ rt, const int32_t* __restrict__ st_beg
     for (int i = 0; i < ST_PER; ++i) {
         const int u = threadIdx.x + i * ST_T;
         m = fmaxf(m, fabsf(yv[i]));
-        if (r.stereo_fir && u < st.cnt) m = fmaxf(m, fabsf(stereo_r(r, w, u)));
+        if (r.stereo_fir == 1 && u < st.cnt) m = fmaxf(m, fabsf(stereo_r(r, w, u)));
+        if (r.stereo_fir == 2 && u < st.cnt) m = fmaxf(m, fabsf(rbuf[r.r2_off + st.t0 + u]));
     }
     for (int off = 32; off > 0; off >>= 1) m = fmaxf(m, __shfl_xor(m, off));
     if ((threadIdx.x & 63) == 0) wm[threadIdx.x >> 6] = m;
@@ -363,7 +364,8 @@ MSG_DEV float sat(float v, float d, float inv_td) { return d > 0.f ? tanhf(v * d
 
 __global__ void __launch_bounds__(ST_T)
 k_stereo_out(const PresetRt* __restrict__ rt, const int32_t* __restrict__ st_begin, int n_presets,
-             const float* __restrict__ ybuf, const unsigned* __restrict__ maxbits, float* __restrict__ out) {
+             const float* __restrict__ ybuf, const float* __restrict__ rbuf, const unsigned* __restrict__ maxbits,
+             float* __restrict__ out) {
     __shared__ float w[ST_TILE + 48];
     const int b = blockIdx.x;
     const int p = find_preset(st_begin, n_presets, b);
@@ -390,7 +392,8 @@ k_stereo_out(const PresetRt* __restrict__ rt, const int32_t* __restrict__ st_beg
         const int u = threadIdx.x + i * ST_T;
         if (u >= st.cnt) continue;
         const float L = lv[i];
-        const float R = r.stereo_fir ? stereo_r(r, w, u) : L;
+        const float R = r.stereo_fir == 1 ? stereo_r(r, w, u)
+                        : (r.stereo_fir == 2 ? rbuf[r.r2_off + st.t0 + u] : L);
         o[u] = make_float2(sat(L, d, inv_td) * scale, sat(R, d, inv_td) * scale);
     }
 }

@@ -57,3 +57,10 @@ hipError_t launch_chain64(unsigned grid, int lds_bytes, hipStream_t s, const msg
                           double* state, float* grain_pool);
 hipError_t launch_fft64_one(int lds_bytes, hipStream_t s, const Real64Plan* plans, int plan, int inverse,
                             double* io);
+
+// odd-length stereo rotation (kernels_stereo_odd.h): Bluestein through M = pow2 >= 2n-1
+void stereo_odd_init_attrs();
+int64_t stereo_odd_len(int64_t n);                  // M, or -1 when n is too long
+hipError_t launch_stereo_odd_kernel(int64_t n, float2* Bp, float2* A, hipStream_t s);
+hipError_t launch_stereo_odd(int64_t n, int dr, double width, const float* y, const float2* Bp, float2* A,
+                             float* r2, hipStream_t s);

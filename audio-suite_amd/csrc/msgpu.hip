@@ -104,6 +104,10 @@ struct msg_ctx {
     DevBuf<double2> save64;
     DevBuf<Chain64> chains;
     DevBuf<uint8_t> imgbank;
+    // odd-length stereo rotation (kernels_stereo_odd.h)
+    std::map<int64_t, DevBuf<float2>> so_bp;   // chirp kernel spectra by n
+    DevBuf<float2> so_A;
+    DevBuf<float> so_r2;
     // host mirrors of the last batch
     std::vector<msg_plan_info> h_info;
     std::vector<msg_event> h_events;
@@ -283,11 +287,14 @@ static double bessel_j(int m, double x) {
 }
 
 // Choose (N, P, Q) minimising FFT work for an M-tap FIR over n outputs.
-static void choose_fir(int64_t M, int64_t n, int& N, int& P, int& Q) {
+// need: with early reflections the whole kernel h is built in one transform
+// (k_fir_h), so only N >= need qualify (M - 1 with an IR, M without).
+static void choose_fir(int64_t M, int64_t n, int64_t need, int& N, int& P, int& Q) {
     double best = 1e300;
     N = FIR_NMAX; P = (int)std::min<int64_t>(M, FIR_NMAX / 2); Q = (int)((M + P - 1) / P);
     for (int lg = 11; lg <= 15; ++lg) {   // k_fir2 sizes: M = N/2 in 1024..16384
         const int NN = 1 << lg;
+        if (NN < need) continue;
         for (int q = 1; q <= 64; ++q) {
             const int64_t pp = (M + q - 1) / q;
             if (pp >= NN) continue;
@@ -428,6 +435,7 @@ msg_ctx* msg_create(int device_ordinal) {
     fir_init_attrs();
     fft_bench_init_attrs();
     grain64_init_attrs();
+    stereo_odd_init_attrs();
     return ctx.release();
 }
 
@@ -459,6 +467,8 @@ void msg_destroy(msg_ctx* ctx) {
     ctx->ev64.release(); ctx->g64_list.release(); ctx->gen64_list.release(); ctx->gen64_off.release();
     ctx->micro64.release(); ctx->grain64.release(); ctx->state64.release(); ctx->save64.release();
     ctx->chains.release(); ctx->imgbank.release();
+    for (auto& kv : ctx->so_bp) kv.second.release();
+    ctx->so_A.release(); ctx->so_r2.release();
     delete ctx;
 }
 
@@ -775,6 +785,8 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
         imgbank.insert(imgbank.end(), images[i], images[i] + (int64_t)img_h[i] * img_w[i]);
     }
     int64_t sum64 = 0, save_sum = 0, state_sum = 0;
+    int64_t r2_sum = 0, so_M = 0;
+    std::vector<int32_t> odd_presets;
     int g64_cap = 0;
     for (int p = 0; p < P; ++p) {
         const msg_preset& pr = presets[p];
@@ -836,7 +848,7 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
             const int64_t er_span = er ? (int64_t)std::nearbyint(pr.er_max_ms / 1000.0 * sr) + 1 : 0;
             const int64_t M = (ir ? r.ir_len : 1) + er_span;
             int N, Pp, Q;
-            choose_fir(M, inf.out_n, N, Pp, Q);
+            choose_fir(M, inf.out_n, er ? (ir ? M - 1 : M) : 0, N, Pp, Q);
             std::string why;
             const int fp = real_plan(ctx->fir_plans, N, why);
             if (fp < 0) return fail(ctx, MSG_E_DEVICE, "FIR plan: " + why);
@@ -871,9 +883,17 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
         // stereo (MS:423-436)
         const double w = std::min(std::max(pr.stereo_width, 0.0), 1.0);
         const bool stereo = (pr.flags & MSG_F_STEREO) && inf.out_n >= 64;
-        if (stereo && (inf.out_n % 2))
-            return fail(ctx, MSG_E_UNSUPPORTED, "stereo diffusion of an odd-length output is not yet on the GPU path");
         r.stereo_fir = stereo ? 1 : 0;
+        if (stereo && (inf.out_n % 2)) {      // full-length rotation through Bluestein (kernels_stereo_odd.h)
+            const int64_t M = stereo_odd_len(inf.out_n);
+            if (M < 0)
+                return fail(ctx, MSG_E_UNSUPPORTED, "stereo diffusion of an odd output longer than 4194304 frames");
+            r.stereo_fir = 2;
+            r.r2_off = r2_sum;
+            r2_sum += (inf.out_n + 3) & ~int64_t(3);
+            so_M = std::max(so_M, M);
+            odd_presets.push_back(p);
+        }
         r.dl = (int32_t)std::nearbyint((1 + 7 * w) * 0.0005 * sr);
         r.dr = (int32_t)std::nearbyint((1 + 9 * w) * 0.0007 * sr);
         for (int m = -12; m <= 12; ++m) {
@@ -1009,6 +1029,8 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
     HIPCHK(ctx, ctx->state64.ensure(state_sum));
     HIPCHK(ctx, ctx->chains.ensure(chains.size()));
     HIPCHK(ctx, ctx->imgbank.ensure(imgbank.size()));
+    HIPCHK(ctx, ctx->so_r2.ensure(r2_sum));
+    HIPCHK(ctx, ctx->so_A.ensure(so_M));
     HIPCHK(ctx, ctx->ert.ensure(nslots));
     HIPCHK(ctx, ctx->prt.ensure(P));
     HIPCHK(ctx, ctx->gen_list.ensure(gen_list.size()));
@@ -1138,11 +1160,23 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
     }
     // ---- stereo, tanh, normalise ----
     stage_mark(ctx, 6, s);
+    for (int p : odd_presets) {           // odd out_n: R = irfft(rfft(roll(y, -dr)) . rot) (MS:432-435)
+        const int64_t n = info[p].out_n;
+        auto it = ctx->so_bp.find(n);
+        if (it == ctx->so_bp.end()) {
+            it = ctx->so_bp.emplace(n, DevBuf<float2>()).first;
+            HIPCHK(ctx, it->second.ensure(stereo_odd_len(n)));
+            HIPCHK(ctx, launch_stereo_odd_kernel(n, it->second.p, ctx->so_A.p, s));
+        }
+        const double w = std::min(std::max(presets[p].stereo_width, 0.0), 1.0);
+        HIPCHK(ctx, launch_stereo_odd(n, prt[p].dr, w, yb + prt[p].y_off, it->second.p, ctx->so_A.p,
+                                      ctx->so_r2.p + prt[p].r2_off, s));
+    }
     hipLaunchKernelGGL(k_stereo_max, dim3((unsigned)stiles), dim3(ST_T), 0, s, ctx->prt.p, ctx->st_begin.p, P,
-                       yb, ctx->maxbits.p);
+                       yb, ctx->so_r2.p, ctx->maxbits.p);
     HIPCHK(ctx, hipGetLastError());
     hipLaunchKernelGGL(k_stereo_out, dim3((unsigned)stiles), dim3(ST_T), 0, s, ctx->prt.p, ctx->st_begin.p, P,
-                       yb, ctx->maxbits.p, out_dev);
+                       yb, ctx->so_r2.p, ctx->maxbits.p, out_dev);
     HIPCHK(ctx, hipGetLastError());
     stage_mark(ctx, 7, s);
     ctx->h_info = info;

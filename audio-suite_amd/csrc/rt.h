@@ -39,7 +39,7 @@ struct PresetRt {
     int64_t h_off;         // offset of the Q partition spectra (float2)
     int64_t irs_off;       // offset of the IR spectrum at size fir_N (float2)
     // stereo / saturation / normalisation
-    int32_t stereo_fir;    // 1: 25-tap Bessel FIR, 0: L = R = y
+    int32_t stereo_fir;    // 1: 25-tap Bessel FIR (even n), 2: precomputed R (odd n), 0: L = R = y
     int32_t dl, dr;
     float bess[25];        // J_m(0.9 w), m = -12..12
     float drive, peak;
@@ -48,6 +48,7 @@ struct PresetRt {
     int64_t frag_off, frag_len;
     int64_t img_off;
     int32_t img_h, img_w;
+    int64_t r2_off;        // stereo_fir == 2: rotated right channel in the odd-stereo buffer
 };
 
 // Per-event spectral work descriptor (host-built after planning).

@@ -35,6 +35,7 @@ def msgpu():
 
 CASES = [
     ("C1", "C1", {}), ("C2", "C2", {}), ("C3", "C3", {}),
+    ("C2odd", "C2", dict(seed=1002, out_dur_s=0.5 + 1 / 192000)),   # odd out_n: full-length rotation
     ("C3s1001", "C3", dict(seed=1001, out_dur_s=0.25)),
     ("C4s1000short", "C4", dict(out_dur_s=0.25)),
 ]
@@ -198,3 +199,25 @@ def test_spectral_runtime_and_compile_time_plans(msgpu, irs, full_renders, monke
         assert rms(audio, full_renders[f"{name}_audio"]) <= RMS_TOL, (name, ct)
     audio, _ = msgpu.render(msgpu.merged(out_dur_s=0.5))      # factory default: n = 1500
     assert rms(audio, full_renders["defaults_short_audio"]) <= RMS_TOL
+
+
+@pytest.mark.parametrize("frames", [65, 127, 4097, 48001, 240001])
+def test_odd_length_stereo(msgpu, irs, frames):
+    """Odd out_n: the stereo rotation as a full-length transform (Bluestein,
+    four-step M = 256 .. 2^20), against the oracle; mixed with an even preset
+    in one batch."""
+    from oracle import msound_oracle as O
+    sr = 48000
+    proc = "Single" if frames < 5000 else "Poisson"     # short outputs: one event at t = 0
+    params = [msgpu.merged(base_sr=sr, out_dur_s=frames / sr, gen_mode="Resonant strike", event_process=proc,
+                           grains_per_sec=30.0, env_a=0.0, env_r=1.0, seed=frames, stereo_width=w)
+              for w in (0.65, 1.0)]
+    params.append(msgpu.merged(base_sr=sr, out_dur_s=(frames + 1) / sr, env_a=0.0, env_r=1.0, seed=3))
+    outs = msgpu.render_batch(params)
+    for p, a in zip(params, outs):
+        assert a.shape[0] % 2 == (1 if p is not params[-1] else 0)
+        ref, _ = O.render(p)
+        err = rms(a, ref)
+        print(f"odd stereo n={a.shape[0]} w={p['stereo_width']}: rms {err:.3e}")
+        assert err <= RMS_TOL
+        assert np.max(np.abs(a)) > 0.5                 # a real signal, normalised to the peak
