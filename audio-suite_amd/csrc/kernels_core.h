@@ -40,7 +40,8 @@ __global__ void k_plan_events(const msg_preset* __restrict__ presets, int n_pres
 // report how many draws it consumed, which moves the parse position.  The
 // emitted sequence is exactly NumPy's standard_normal(n).
 // ---------------------------------------------------------------------------
-struct JumpTab { nprng::u128 a[GEN_T]; nprng::u128 s[GEN_T]; nprng::u128 a64, s64; };
+constexpr int GEN_G = 8;           // chunks of 64 draws classified per pass
+struct JumpTab { nprng::u128 a[GEN_T]; nprng::u128 s[GEN_T]; nprng::u128 a64, s64, aG, sG; };
 
 MSG_DEV double slow_normal(nprng::u128 st, nprng::u128 inc, uint64_t rabs, int idx, double x,
                            const nprng::Zig& z, int& consumed) {
@@ -142,51 +143,86 @@ k_gen_normal(const msg_preset* __restrict__ presets, const msg_event* __restrict
     const nprng::u128 inc = g0.inc;
     const nprng::u128 a64 = jt->a64;
     const nprng::u128 c64 = inc * jt->s64;
-    nprng::u128 st = jt->a[lane] * g0.state + inc * jt->s[lane];   // state after lane+1 steps
+
+    // Per group of GEN_G chunks of 64 draws: every lane classifies its GEN_G
+    // draws, then finishes its (rare) slow ziggurat draws in one divergent loop
+    // -- the wave runs that loop max-over-lanes times (usually once) instead of
+    // once per chunk that holds a slow draw.  A wave-uniform walk per chunk then
+    // marks the draws each slow normal consumed and all surviving lanes emit
+    // their sample at once (rank = popcount of the valid lanes below).
+    constexpr int G = GEN_G;
+    nprng::u128 st[G];
+    st[0] = jt->a[lane] * g0.state + inc * jt->s[lane];   // state after lane+1 steps
+#pragma unroll
+    for (int g = 1; g < G; ++g) st[g] = a64 * st[g - 1] + c64;
+    const nprng::u128 aG = jt->aG;
+    const nprng::u128 cG = inc * jt->sG;
     __syncthreads();
 
-    // Per chunk of 64 draws: every slow lane evaluates its rejection normal
-    // tentatively (in parallel); a wave-uniform walk over the slow lanes then
-    // marks the draws each one consumed, and all surviving lanes emit their
-    // sample at once (rank = popcount of the valid lanes below).
     int produced = 0;
-    int local = 0;   // first lane of this chunk that is not consumed by an earlier slow normal
+    int local = 0;   // first lane of the current chunk not consumed by an earlier slow normal
     while (produced < n) {
-        const uint64_t raw = nprng::xsl_rr(st);
-        const int idx = (int)(raw & 0xff);
-        const uint64_t rr = raw >> 8;
-        const uint64_t rabs = (rr >> 1) & 0x000fffffffffffffULL;
-        double x = (double)rabs * s_wi[idx];
-        if (rr & 1) x = -x;
-        const bool fast = rabs < s_ki[idx];
-        const uint64_t F = __ballot(fast);
-        int consumed = 1;
-        if (!fast && lane >= local) x = slow_normal(st, inc, rabs, idx, x, z, consumed);
-        uint64_t valid = ~0ULL << local;          // local < 64 here
-        uint64_t S = ~F & valid;
-        int pos = 64;
-        while (S) {                               // wave-uniform
-            const int q = __builtin_ctzll(S);
-            const int end = q + __builtin_amdgcn_readlane(consumed, q);
-            const uint64_t after_q = ~((2ULL << q) - 1);                  // lanes q+1..63
-            const uint64_t before_end = end >= 64 ? ~0ULL : ((1ULL << end) - 1);
-            valid &= ~(after_q & before_end);
-            if (end >= 64) { pos = end; break; }
-            S &= ~0ULL << end;
+        uint64_t rabs[G], F[G];
+        int idx[G], consumed[G];
+        double x[G];
+        unsigned slow = 0;
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            const uint64_t raw = nprng::xsl_rr(st[g]);
+            idx[g] = (int)(raw & 0xff);
+            const uint64_t rr = raw >> 8;
+            rabs[g] = (rr >> 1) & 0x000fffffffffffffULL;
+            x[g] = (double)rabs[g] * s_wi[idx[g]];
+            if (rr & 1) x[g] = -x[g];
+            const bool fast = rabs[g] < s_ki[idx[g]];
+            F[g] = __ballot(fast);
+            consumed[g] = 1;
+            if (!fast) slow |= 1u << g;
         }
-        if ((valid >> lane) & 1) {
-            const int j = produced + __popcll(valid & ((1ULL << lane) - 1));
-            if (j < n) {
-                if (out64) out64[j] = x;
-                else out[j] = gen_basic_sample(c, j, x);
+        while (slow) {                            // divergent: each lane walks its own slow draws
+            const int gs = __builtin_ctz(slow);
+            slow &= slow - 1;
+            nprng::u128 s0 = st[0];
+            uint64_t ra = rabs[0];
+            int id = idx[0];
+            double xv = x[0];
+#pragma unroll
+            for (int g = 1; g < G; ++g)
+                if (gs == g) { s0 = st[g]; ra = rabs[g]; id = idx[g]; xv = x[g]; }
+            int cn = 1;
+            const double v = slow_normal(s0, inc, ra, id, xv, z, cn);
+#pragma unroll
+            for (int g = 0; g < G; ++g)
+                if (gs == g) { x[g] = v; consumed[g] = cn; }
+        }
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            if (local >= 64) { local -= 64; continue; }   // chunk consumed by an earlier slow normal
+            if (produced >= n) continue;
+            uint64_t valid = ~0ULL << local;
+            uint64_t S = ~F[g] & valid;
+            int pos = 64;
+            while (S) {                               // wave-uniform
+                const int q = __builtin_ctzll(S);
+                const int end = q + __builtin_amdgcn_readlane(consumed[g], q);
+                const uint64_t after_q = ~((2ULL << q) - 1);                  // lanes q+1..63
+                const uint64_t before_end = end >= 64 ? ~0ULL : ((1ULL << end) - 1);
+                valid &= ~(after_q & before_end);
+                if (end >= 64) { pos = end; break; }
+                S &= ~0ULL << end;
             }
+            if ((valid >> lane) & 1) {
+                const int j = produced + __popcll(valid & ((1ULL << lane) - 1));
+                if (j < n) {
+                    if (out64) out64[j] = x[g];
+                    else out[j] = gen_basic_sample(c, j, x[g]);
+                }
+            }
+            produced += __popcll(valid);
+            local = pos - 64;
         }
-        produced += __popcll(valid);
-        local = pos;
-        do {   // advance all lanes by one chunk; skip chunks a slow normal consumed
-            st = a64 * st + c64;
-            local -= 64;
-        } while (local >= 64);
+#pragma unroll
+        for (int g = 0; g < G; ++g) st[g] = aG * st[g] + cG;   // next group of G chunks
     }
 }
 

@@ -67,7 +67,10 @@ struct msg_ctx {
     int device = 0;
     std::string err;
     bool profiling = false;
-    float stage_ms[10] = {0};
+    bool pending = false;         // events of the last profiled batch not yet read
+    bool pending_fir = false;
+    double stage_sum[10] = {0};   // accumulated stage times since msg_set_profiling(ctx, 1)
+    int64_t stage_cnt = 0;
     hipEvent_t ev[10] = {};
     // constant tables
     uint64_t* d_ki = nullptr; double* d_wi = nullptr; double* d_fi = nullptr;
@@ -412,6 +415,8 @@ msg_ctx* msg_create(int device_ordinal) {
     }
     const nprng::Jump j64 = nprng::jump_of(GEN_T);
     jt.a64 = j64.a; jt.s64 = j64.s;
+    const nprng::Jump jG = nprng::jump_of((uint64_t)GEN_T * GEN_G);
+    jt.aG = jG.a; jt.sG = jG.s;
     if (!up(ctx->d_jump, &jt, 1)) { g_err = "uploading jump table failed"; return nullptr; }
     for (int i = 0; i < 5; ++i) {
         std::vector<float> tab;
@@ -472,15 +477,40 @@ void msg_destroy(msg_ctx* ctx) {
     delete ctx;
 }
 
+// Fold the event times of the last profiled batch into the running sums.
+// The events are read lazily (here, at the next batch of the same context or
+// at msg_stage_times) so profiling never blocks the host between batches.
+static void collect_stage_times(msg_ctx* ctx) {
+    if (!ctx->pending) return;
+    hipEventSynchronize(ctx->ev[7]);
+    float ms[10] = {0};
+    for (int i = 0; i < 7; ++i) hipEventElapsedTime(&ms[i], ctx->ev[i], ctx->ev[i + 1]);
+    hipEventElapsedTime(&ms[7], ctx->ev[0], ctx->ev[7]);
+    if (ctx->pending_fir) {   // the FIR kernel alone, and the h build before it
+        hipEventElapsedTime(&ms[8], ctx->ev[8], ctx->ev[9]);
+        hipEventElapsedTime(&ms[9], ctx->ev[5], ctx->ev[8]);
+    }
+    for (int i = 0; i < 10; ++i) ctx->stage_sum[i] += ms[i];
+    ++ctx->stage_cnt;
+    ctx->pending = false;
+}
+
 int msg_set_profiling(msg_ctx* ctx, int32_t on) {
     if (!ctx) return MSG_E_ARG;
+    collect_stage_times(ctx);
     ctx->profiling = on != 0;
+    if (ctx->profiling) {
+        for (double& v : ctx->stage_sum) v = 0.0;
+        ctx->stage_cnt = 0;
+    }
     return MSG_OK;
 }
 
 int msg_stage_times(msg_ctx* ctx, float* ms, int32_t n) {
     if (!ctx || !ms) return MSG_E_ARG;
-    for (int i = 0; i < n && i < 10; ++i) ms[i] = ctx->stage_ms[i];
+    collect_stage_times(ctx);
+    for (int i = 0; i < n && i < 10; ++i)
+        ms[i] = ctx->stage_cnt ? (float)(ctx->stage_sum[i] / (double)ctx->stage_cnt) : 0.f;
     return MSG_OK;
 }
 
@@ -695,6 +725,7 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
     if (!ctx || !presets || P <= 0 || !out_dev || !out_offsets) return fail(ctx, MSG_E_ARG, "bad arguments");
     hipStream_t s = (hipStream_t)stream;
     HIPCHK(ctx, hipSetDevice(ctx->device));
+    collect_stage_times(ctx);
     for (int p = 0; p < P; ++p) {
         std::string why;
         if (!supported(presets[p], why)) return fail(ctx, MSG_E_UNSUPPORTED, "preset " + std::to_string(p) + ": " + why);
@@ -1186,14 +1217,8 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
     ctx->h_last64 = last64;
     ctx->last_n = P;
     if (ctx->profiling) {
-        HIPCHK(ctx, hipEventSynchronize(ctx->ev[7]));
-        for (int i = 0; i < 7; ++i) hipEventElapsedTime(&ctx->stage_ms[i], ctx->ev[i], ctx->ev[i + 1]);
-        hipEventElapsedTime(&ctx->stage_ms[7], ctx->ev[0], ctx->ev[7]);
-        ctx->stage_ms[8] = ctx->stage_ms[9] = 0.f;
-        if (hblocks > 0) {   // the FIR kernel alone, and the h build before it
-            hipEventElapsedTime(&ctx->stage_ms[8], ctx->ev[8], ctx->ev[9]);
-            hipEventElapsedTime(&ctx->stage_ms[9], ctx->ev[5], ctx->ev[8]);
-        }
+        ctx->pending = true;
+        ctx->pending_fir = hblocks > 0;
     }
     return MSG_OK;
 }

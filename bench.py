@@ -42,7 +42,7 @@ def load_irs():
     return {k: z[k] for k in z.files}
 
 
-def stage_bytes(infos, packed, params):
+def stage_bytes(infos, _packed, params):
     """Algorithmic (compulsory) HBM bytes per stage for one step."""
     sum_n = sum(int(i.pool_len) for i in infos)
     out_n = sum(int(i.out_n) for i in infos)
@@ -117,6 +117,8 @@ def main():
     ap.add_argument("--batch", type=int, default=1024)
     ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of CPU-baseline work")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--streams", type=int, default=2, help="in-flight sub-batches (contexts/streams) per GPU")
+    ap.add_argument("--iso-steps", type=int, default=3, help="single-stream renders for roofline_isolated")
     args = ap.parse_args()
 
     import torch
@@ -136,51 +138,88 @@ def main():
     irs = load_irs()
     seeds = rank_seeds(rank, args.batch)
     params = [msgpu.config_params(args.config, seed=s, irs=irs) for s in seeds]
-    packed = PackedBatch(params)
-    eng = Engine(dev)
-    out = eng.alloc_output(packed)
-    stream = torch.cuda.current_stream(dev)
+    S = max(1, min(args.streams, args.batch))
+    # S in-flight renders per GPU, one context + one HIP stream each (SURVEY
+    # section 8e: "one HIP stream per render"): the host plans one sub-batch
+    # while the device runs the other, and their kernels share the CUs.
+    cut = [len(params) * i // S for i in range(S + 1)]
+    subs = [PackedBatch(params[cut[i]:cut[i + 1]]) for i in range(S)]
+    engs = [Engine(dev) for _ in range(S)]
+    outs = [e.alloc_output(p) for e, p in zip(engs, subs)]
+    streams = [torch.cuda.Stream(device=dev) for _ in range(S)]
 
     def barrier():
         if world > 1:
             dist.barrier()
 
-    for _ in range(args.warmup):
-        eng.render_packed(packed, out, stream)
-    torch.cuda.synchronize(dev)
-    infos = eng.last_plan()
+    def step():
+        for e, p, o, st in zip(engs, subs, outs, streams):
+            e.render_packed(p, o, st)
 
-    eng.set_profiling(True)
-    stage_sum = np.zeros(10)
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    infos = [i for e in engs for i in e.last_plan()]
+
+    for e in engs:
+        e.set_profiling(True)
     barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        eng.render_packed(packed, out, stream)
-        stage_sum += np.array(eng.stage_times())
+        step()
     torch.cuda.synchronize(dev)
     barrier()
     elapsed = time.perf_counter() - t0
-    eng.set_profiling(False)
+    for e in engs:
+        e.set_profiling(False)
     elapsed = max_over_ranks(elapsed, world, f"cuda:{dev}")
+    names = ["plan", "host_prep", "generate", "spectral", "overlap_add", "fir", "stereo", "total",
+             "fir_kernel", "fir_h"]
+    # per-launch stage times in the timed region (each sub-batch on its own stream)
+    stage_ms = np.mean([np.array(e.stage_times()) for e in engs], axis=0)
+    stages = {n: round(float(v), 4) for n, v in zip(names, stage_ms)}
 
-    frames_rank = packed.total_frames
+    # isolated pass: the whole batch on one stream, kernels not sharing the GPU
+    iso = {}
+    if args.iso_steps > 0:
+        packed = PackedBatch(params)
+        e1 = engs[0]
+        o1 = e1.alloc_output(packed)
+        e1.render_packed(packed, o1, streams[0])
+        torch.cuda.synchronize(dev)
+        e1.set_profiling(True)
+        for _ in range(args.iso_steps):
+            e1.render_packed(packed, o1, streams[0])
+        torch.cuda.synchronize(dev)
+        e1.set_profiling(False)
+        iso = {n: round(float(v), 4) for n, v in zip(names, e1.stage_times())}
+        del o1
+
+    frames_rank = sum(p.total_frames for p in subs)
     total_frames = frames_rank * world * args.steps
     value = total_frames / elapsed / 1e6
     ms_step = elapsed / args.steps * 1e3
-    stage_ms = stage_sum / args.steps
-    names = ["plan", "host_prep", "generate", "spectral", "overlap_add", "fir", "stereo", "total",
-             "fir_kernel", "fir_h"]
-    stages = {n: round(float(v), 4) for n, v in zip(names, stage_ms)}
-    sb = stage_bytes(infos, packed, params)
-    stage_gbs = {k: round(sb[k] / (stages[k] * 1e-3) / 1e9, 1) for k in sb if stages.get(k, 0) > 0}
+    sb = stage_bytes(infos, None, params)
+    sb_launch = {k: v / S for k, v in sb.items()}
+    stage_gbs = {k: round(sb_launch[k] / (stages[k] * 1e-3) / 1e9, 1) for k in sb if stages.get(k, 0) > 0}
     # dominant single kernel (the FIR stage is timed without its h build)
     kernel_stages = ["generate", "spectral", "overlap_add", "fir_kernel", "stereo"]
     dom = max(kernel_stages, key=lambda k: stages[k])
-    achieved = sb[dom] / (stages[dom] * 1e-3) / 1e9
-    traffic = measured_traffic(STAGE_KERNEL[dom], args.config, args.batch)
+    achieved = sb_launch[dom] / (stages[dom] * 1e-3) / 1e9
+    traffic = measured_traffic(STAGE_KERNEL[dom], args.config, args.batch // S)
     sum_n = sum(int(i.pool_len) for i in infos)
     n_ev = sum(int(i.n_events) for i in infos)
+    roof_iso = None
+    if iso:
+        dom_i = max(kernel_stages, key=lambda k: iso[k])
+        ach_i = sb[dom_i] / (iso[dom_i] * 1e-3) / 1e9
+        roof_iso = {"kernel": STAGE_KERNEL[dom_i].rstrip("<"), "achieved": round(ach_i, 1),
+                    "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach_i / HBM_PEAK_GBS, 4),
+                    "algorithmic_bytes": sb[dom_i], "kernel_ms": iso[dom_i],
+                    "traffic": measured_traffic(STAGE_KERNEL[dom_i], args.config, args.batch),
+                    "stage_ms": iso, "note": f"whole batch on one stream, {args.iso_steps} renders after the "
+                                             f"timed region"}
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
@@ -197,11 +236,14 @@ def main():
                                    f"Poisson 18/s, 1 s, 16k-tap IR request (8192 cap), ER 320 taps, stereo",
                        "presets_per_gpu": args.batch, "frames_per_gpu_step": frames_rank,
                        "events_per_gpu_step": n_ev, "design_samples_per_gpu_step": sum_n,
-                       "parallelism": f"preset-sharded x{world}"},
+                       "parallelism": f"preset-sharded x{world}", "streams_per_gpu": S},
             "roofline": {"bound": "hbm", "kernel": STAGE_KERNEL[dom].rstrip("<"),
                          "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                         "algorithmic_bytes": sb[dom], "kernel_ms": stages[dom]},
+                         "algorithmic_bytes": sb_launch[dom], "kernel_ms": stages[dom],
+                         "note": f"per launch in the timed region ({S} sub-batches of {args.batch // S} presets "
+                                 f"on {S} streams sharing the GPU)"},
+            "roofline_isolated": roof_iso,
             "stage_ms": stages, "stage_algorithmic_GBs": stage_gbs,
             "design_msamples_per_s": round(sum_n * world * args.steps / elapsed / 1e6, 1),
             "cpu_baseline": cpu,

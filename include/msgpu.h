@@ -145,11 +145,13 @@ int msg_last_events(msg_ctx* ctx, int32_t preset, msg_event* events, int32_t cap
 int msg_last_meta(msg_ctx* ctx, int32_t preset, double* micro, double* grain,
                   int64_t cap, int64_t* n);
 
-/* Device time of each stage of the last batch in ms (HIP events):
+/* Device time of each stage in ms (HIP events on the batch's stream),
+ * averaged over the batches rendered since msg_set_profiling(ctx, 1):
  * [0] device plan + read-back, [1] host prep + uploads, [2] generate,
- * [3] spectral, [4] overlap-add x ADSR, [5] FIR (h build + FIR),
- * [6] stereo+clip+normalise, [7] total, [8] the FIR kernel alone,
- * [9] the h build (IR spectra + h spectra).  Needs msg_set_profiling(ctx, 1).  */
+ * [3] spectral (float32 and float64 chains), [4] overlap-add x ADSR,
+ * [5] FIR (h build + FIR), [6] stereo+clip+normalise, [7] total,
+ * [8] the FIR kernel alone, [9] the h build (IR spectra + h spectra).
+ * Events are read lazily, so profiling does not block the host.             */
 int msg_set_profiling(msg_ctx* ctx, int32_t on);
 int msg_stage_times(msg_ctx* ctx, float* ms, int32_t n);
 
