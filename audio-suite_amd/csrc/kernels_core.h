@@ -1,6 +1,7 @@
 // kernels_core.h — planner, generator, overlap-add and stereo kernels (TU: msgpu.hip).
 #pragma once
 #include "rt.h"
+#include <type_traits>
 
 // ---------------------------------------------------------------------------
 // Planner (one thread per preset).
@@ -40,7 +41,10 @@ __global__ void k_plan_events(const msg_preset* __restrict__ presets, int n_pres
 // report how many draws it consumed, which moves the parse position.  The
 // emitted sequence is exactly NumPy's standard_normal(n).
 // ---------------------------------------------------------------------------
-constexpr int GEN_G = 8;           // chunks of 64 draws classified per pass
+#ifndef MSG_GEN_G
+#define MSG_GEN_G 4
+#endif
+constexpr int GEN_G = MSG_GEN_G;   // chunks of 64 draws classified per pass
 struct JumpTab { nprng::u128 a[GEN_T]; nprng::u128 s[GEN_T]; nprng::u128 a64, s64, aG, sG; };
 
 MSG_DEV double slow_normal(nprng::u128 st, nprng::u128 inc, uint64_t rabs, int idx, double x,
@@ -76,36 +80,47 @@ MSG_DEV double slow_normal(nprng::u128 st, nprng::u128 inc, uint64_t rabs, int i
 }
 
 // Closed-form part of gen_basic for sample j given its normal N_j (MS:235-268).
-// The ring phase is reduced in float64 (f*t reaches ~150 cycles at 30 MHz);
-// the decays are exp2f of j times a float64-built coefficient.
+// The ring phase frac(j f / sr) is reduced exactly in float32 from a two-term
+// split of f / sr (j * fa with its fma rounding error, plus j * fb); the
+// decays are exp2f of j times a float64-built coefficient.
 struct GenBasicConst {
     int mode;            // MSG_GEN_*
     int n, fade;
     float inv_fade;
-    double f_over_sr;    // resonant: cycles per sample
+    float fa, fb;        // resonant: cycles per sample, fa + fb = f / sr
     float k_ring, k_exc; // resonant: log2 decay per sample
     float inv_sigma;     // gaussian click
 };
-MSG_DEV float gen_basic_sample(const GenBasicConst& c, int j, double nrm) {
+MSG_DEV float ring_phase(float jf, float fa, float fb) {
+    const float p = jf * fa;
+    const float e = fmaf(jf, fa, -p);                 // exact: j * fa = p + e
+    float ph = (p - floorf(p)) + (e + jf * fb);
+    return ph - floorf(ph);
+}
+MSG_DEV float gen_basic_sample(const GenBasicConst& c, int j, float nrm) {
     float x;
     const float jf = (float)j;
     if (c.mode == MSG_GEN_RESONANT) {
-        const double cyc = (double)j * c.f_over_sr;
-        const float ph = (float)(cyc - floor(cyc));
-        x = 0.9f * sinpif(2.0f * ph) * exp2f(jf * c.k_ring) + 0.25f * (float)nrm * exp2f(jf * c.k_exc);
+        const float ph = ring_phase(jf, c.fa, c.fb);
+        x = 0.9f * sinpif(2.0f * ph) * exp2f(jf * c.k_ring) + 0.25f * nrm * exp2f(jf * c.k_exc);
     } else if (c.mode == MSG_GEN_GAUSSIAN_CLICK) {
         const float u = jf * c.inv_sigma;
-        x = expf(-0.5f * (u * u)) * ((float)nrm * 0.12f + 1.0f);
+        x = expf(-0.5f * (u * u)) * (nrm * 0.12f + 1.0f);
     } else if (c.mode == MSG_GEN_NOISE_BURST || c.mode == MSG_GEN_SKEWED) {
-        return (float)nrm;                                    // raw normals; tilt/env in k_spectral
+        return nrm;                                           // raw normals; tilt/env in k_spectral
     } else {
-        x = (float)nrm * 0.1f;                                // gen_basic's last branch (MS:263)
+        x = nrm * 0.1f;                                       // gen_basic's last branch (MS:263)
     }
     if (j < c.fade) x *= jf * c.inv_fade;
     if (j >= c.n - c.fade) x *= (float)(j - (c.n - c.fade)) * -c.inv_fade + 1.0f;
     return x;
 }
 
+// RAW64: raw float64 normals for the float64 chain; else the float32 grain.
+// The float32 path forms the fast-path normal in float32 from the top 32 bits
+// of its 52-bit ziggurat integer (|error| <= 1 ulp of float32); slow draws and
+// RAW64 use the exact float64 product.
+template <bool RAW64>
 __global__ void __launch_bounds__(GEN_T)
 k_gen_normal(const msg_preset* __restrict__ presets, const msg_event* __restrict__ events,
              const PresetRt* __restrict__ rt, const int32_t* __restrict__ ev_list, int n_list,
@@ -113,17 +128,22 @@ k_gen_normal(const msg_preset* __restrict__ presets, const msg_event* __restrict
              double* __restrict__ pool64, const int64_t* __restrict__ off64) {
     __shared__ uint64_t s_ki[256];
     __shared__ double s_wi[256];
+    __shared__ float s_wf[256];          // wi * 2^20 in float32
     const int li = blockIdx.x;
     if (li >= n_list) return;
     const int lane = threadIdx.x;
-    for (int i = lane; i < 256; i += GEN_T) { s_ki[i] = z.ki[i]; s_wi[i] = z.wi[i]; }
+    for (int i = lane; i < 256; i += GEN_T) {
+        s_ki[i] = z.ki[i];
+        s_wi[i] = z.wi[i];
+        s_wf[i] = (float)(z.wi[i] * 1048576.0);
+    }
     const msg_event& e = events[ev_list[li]];
     const msg_preset& pr = presets[e.preset];
     const PresetRt& r = rt[e.preset];
     const int n = e.n;
     float* out = pool + r.pool_base + e.pool_off;
     // float64 grain chain (kernels_grain64.h): raw normals into its pool
-    double* out64 = off64 ? pool64 + off64[li] : nullptr;
+    double* out64 = RAW64 ? pool64 + off64[li] : nullptr;
 
     GenBasicConst c;
     c.mode = pr.gen_mode == MSG_GEN_FALLBACK ? MSG_GEN_NOISE_BURST : pr.gen_mode;   // MS:686
@@ -131,7 +151,9 @@ k_gen_normal(const msg_preset* __restrict__ presets, const msg_event* __restrict
     c.fade = (int)(0.01 * n) > 8 ? (int)(0.01 * n) : 8;
     c.inv_fade = (float)(1.0 / (double)c.fade);
     const double inv_sr = 1.0 / (double)e.gen_sr;
-    c.f_over_sr = fmax(10.0, pr.ring_hz) * inv_sr;
+    const double f_over_sr = fmax(10.0, pr.ring_hz) * inv_sr;
+    c.fa = (float)f_over_sr;
+    c.fb = (float)(f_over_sr - (double)c.fa);
     const double log2e = 1.4426950408889634;
     c.k_ring = (float)(-inv_sr / fmax(1e-6, pr.ring_decay_ms / 1000.0) * log2e);
     c.k_exc = (float)(-inv_sr / fmax(1e-6, (pr.micro_ms / 1000.0) * 0.15) * log2e);
@@ -162,19 +184,22 @@ k_gen_normal(const msg_preset* __restrict__ presets, const msg_event* __restrict
     int produced = 0;
     int local = 0;   // first lane of the current chunk not consumed by an earlier slow normal
     while (produced < n) {
+        using XT = typename std::conditional<RAW64, double, float>::type;
         uint64_t rabs[G], F[G];
         int idx[G], consumed[G];
-        double x[G];
+        XT x[G];
         unsigned slow = 0;
 #pragma unroll
         for (int g = 0; g < G; ++g) {
             const uint64_t raw = nprng::xsl_rr(st[g]);
-            idx[g] = (int)(raw & 0xff);
+            const int id = (int)(raw & 0xff);
             const uint64_t rr = raw >> 8;
             rabs[g] = (rr >> 1) & 0x000fffffffffffffULL;
-            x[g] = (double)rabs[g] * s_wi[idx[g]];
+            idx[g] = id | (int)((rr & 1) << 8);               // sign in bit 8
+            if constexpr (RAW64) x[g] = (double)rabs[g] * s_wi[id];
+            else x[g] = (float)(uint32_t)(rabs[g] >> 20) * s_wf[id];
             if (rr & 1) x[g] = -x[g];
-            const bool fast = rabs[g] < s_ki[idx[g]];
+            const bool fast = rabs[g] < s_ki[id];
             F[g] = __ballot(fast);
             consumed[g] = 1;
             if (!fast) slow |= 1u << g;
@@ -185,15 +210,16 @@ k_gen_normal(const msg_preset* __restrict__ presets, const msg_event* __restrict
             nprng::u128 s0 = st[0];
             uint64_t ra = rabs[0];
             int id = idx[0];
-            double xv = x[0];
 #pragma unroll
             for (int g = 1; g < G; ++g)
-                if (gs == g) { s0 = st[g]; ra = rabs[g]; id = idx[g]; xv = x[g]; }
+                if (gs == g) { s0 = st[g]; ra = rabs[g]; id = idx[g]; }
+            double xv = (double)ra * s_wi[id & 0xff];
+            if (id >> 8) xv = -xv;
             int cn = 1;
-            const double v = slow_normal(s0, inc, ra, id, xv, z, cn);
+            const double v = slow_normal(s0, inc, ra, id & 0xff, xv, z, cn);
 #pragma unroll
             for (int g = 0; g < G; ++g)
-                if (gs == g) { x[g] = v; consumed[g] = cn; }
+                if (gs == g) { x[g] = (XT)v; consumed[g] = cn; }
         }
 #pragma unroll
         for (int g = 0; g < G; ++g) {
@@ -214,8 +240,8 @@ k_gen_normal(const msg_preset* __restrict__ presets, const msg_event* __restrict
             if ((valid >> lane) & 1) {
                 const int j = produced + __popcll(valid & ((1ULL << lane) - 1));
                 if (j < n) {
-                    if (out64) out64[j] = x[g];
-                    else out[j] = gen_basic_sample(c, j, x[g]);
+                    if constexpr (RAW64) out64[j] = x[g];
+                    else out[j] = gen_basic_sample(c, j, (float)x[g]);
                 }
             }
             produced += __popcll(valid);

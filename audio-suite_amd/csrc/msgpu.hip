@@ -1126,12 +1126,12 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
     // ---- generate ----
     stage_mark(ctx, 2, s);
     if (!gen_list.empty())
-        hipLaunchKernelGGL(k_gen_normal, dim3((unsigned)gen_list.size()), dim3(GEN_T), 0, s,
+        hipLaunchKernelGGL(k_gen_normal<false>, dim3((unsigned)gen_list.size()), dim3(GEN_T), 0, s,
                            ctx->presets.p, ctx->events.p, ctx->prt.p, ctx->gen_list.p, (int)gen_list.size(),
                            ctx->dzig, ctx->d_jump, ctx->micro.p, (double*)nullptr, (const int64_t*)nullptr);
     HIPCHK(ctx, hipGetLastError());
     if (!gen64_list.empty())   // raw normals of the float64 chain's normal-driven generators
-        hipLaunchKernelGGL(k_gen_normal, dim3((unsigned)gen64_list.size()), dim3(GEN_T), 0, s,
+        hipLaunchKernelGGL(k_gen_normal<true>, dim3((unsigned)gen64_list.size()), dim3(GEN_T), 0, s,
                            ctx->presets.p, ctx->events.p, ctx->prt.p, ctx->gen64_list.p, (int)gen64_list.size(),
                            ctx->dzig, ctx->d_jump, ctx->micro.p, ctx->micro64.p, (const int64_t*)ctx->gen64_off.p);
     HIPCHK(ctx, hipGetLastError());
