@@ -157,6 +157,8 @@ template <bool INV> struct Dft<15, INV> { static MSG_DEV void run(float2* v) { D
 template <bool INV> struct Dft<16, INV> { static MSG_DEV void run(float2* v) { DftComp<4, 4, INV>::run(v); } };
 template <bool INV> struct Dft<20, INV> { static MSG_DEV void run(float2* v) { DftComp<4, 5, INV>::run(v); } };
 template <bool INV> struct Dft<25, INV> { static MSG_DEV void run(float2* v) { DftComp<5, 5, INV>::run(v); } };
+template <bool INV> struct Dft<24, INV> { static MSG_DEV void run(float2* v) { DftComp<4, 6, INV>::run(v); } };
+template <bool INV> struct Dft<30, INV> { static MSG_DEV void run(float2* v) { DftComp<5, 6, INV>::run(v); } };
 template <bool INV> struct Dft<32, INV> { static MSG_DEV void run(float2* v) { DftComp<4, 8, INV>::run(v); } };
 
 // LDS data layout: logical complex element i lives at lp(i) = i ^ ((i>>4)&15),

@@ -55,3 +55,15 @@ hipError_t launch_spectral_ct(int plan, unsigned grid, hipStream_t s, const msg_
         default: return hipErrorInvalidValue;
     }
 }
+
+#ifdef MSG_STAMPS
+// per-TU copy of the phase stamps (no relocatable device code): the
+// compile-time-plan kernels' own counters
+extern "C" int msg_debug_stamps_ct(unsigned long long* out, int n) {
+    unsigned long long h[16];
+    if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_spec_stamps), sizeof(h)) != hipSuccess) return 3;
+    for (int i = 0; i < n && i < 16; ++i) out[i] = h[i];
+    const unsigned long long z[16] = {};
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_spec_stamps), z, sizeof(z)) == hipSuccess ? 0 : 3;
+}
+#endif

@@ -99,18 +99,45 @@ struct Lowpass {
     }
 };
 
+// Smallest k in [0, K] with k * val >= x / > x (k * val as rfftfreq builds it).
+MSG_DEV int first_bin_at_least(double val, double x, int K) {
+    double g = floor(x / val);
+    int k = g < 0.0 ? 0 : (g > (double)K ? K : (int)g);
+    while (k > 0 && (double)(k - 1) * val >= x) --k;
+    while (k < K && (double)k * val < x) ++k;
+    return k;
+}
+MSG_DEV int first_bin_above(double val, double x, int K) {
+    double g = floor(x / val);
+    int k = g < 0.0 ? 0 : (g > (double)K ? K : (int)g);
+    while (k > 0 && (double)(k - 1) * val > x) --k;
+    while (k < K && (double)k * val <= x) ++k;
+    return k;
+}
+
 // Y[k] = interp(src(k), arange(K), X) for re/im, zero outside (np.interp, MS:112-127),
 // in place.  Every source lies on one side of its bin (ascending: src(k) >= k,
 // else src(k) <= k), so chunks of CH*T bins processed in that order -- read the
 // chunk's sources, barrier, write the chunk, barrier -- never read a bin that
-// was already overwritten.
+// was already overwritten.  Bins >= kz are zero (a band limit whose zeroing
+// was deferred): they are never read, and a chunk whose first (smallest,
+// src is increasing) source is >= kz is written as zeros without reading.
 template <class L, int T, int CH, class Src>
-MSG_DEV void spectral_gather(float2* buf, int K, bool ascending, Src src) {
+MSG_DEV void spectral_gather(float2* buf, int K, bool ascending, Src src, int kz) {
     constexpr int C = CH * T;
     const int nch = (K + C - 1) / C;
     const int tid = otid();
     for (int c = 0; c < nch; ++c) {
         const int base = (ascending ? c : nch - 1 - c) * C;
+        if (src(base) >= (double)kz) {             // chunk-uniform: all sources past the band
+#pragma unroll
+            for (int b = 0; b < CH; ++b) {
+                const int k = base + tid + b * T;
+                if (k < K) cxl<L>(buf, k) = make_float2(0.f, 0.f);
+            }
+            __syncthreads();
+            continue;
+        }
         float2 y[CH];
 #pragma unroll
         for (int b = 0; b < CH; ++b) {
@@ -118,13 +145,14 @@ MSG_DEV void spectral_gather(float2* buf, int K, bool ascending, Src src) {
             y[b] = make_float2(0.f, 0.f);
             if (k < K) {
                 const double xs = src(k);
-                if (xs >= 0.0 && xs <= (double)(K - 1)) {
+                if (xs >= 0.0 && xs <= (double)(K - 1) && xs < (double)kz) {
                     const int j = (int)xs;
                     if (j >= K - 1) {
                         y[b] = cxl<L>(buf, K - 1);
                     } else {
                         const float fr = (float)(xs - (double)j);
-                        const float2 a = cxl<L>(buf, j), e = cxl<L>(buf, j + 1);
+                        const float2 a = cxl<L>(buf, j);
+                        const float2 e = j + 1 < kz ? cxl<L>(buf, j + 1) : make_float2(0.f, 0.f);
                         y[b] = make_float2((e.x - a.x) * fr + a.x, (e.y - a.y) * fr + a.y);
                     }
                 }
@@ -219,11 +247,22 @@ MSG_DEV void spectral_chain(float2* lds, bool evn, const EventRt* __restrict__ e
             for (int j = tid; j < nn; j += T) mo[j] = rxl_get<L>(lds, evn, j);
         } else if (step == 2) {
             const int ops2 = ex.ops;
+            int kz = KK;          // bins >= kz are zero, zeroing deferred to the next gather
             if ((ops2 & SPEC_LOWPASS) && !SPEC_SKIP(0)) {
+                // lowpass_fft (MS:48-58): weight 1 below c, the cosine band [c, f1],
+                // zero above (f1 = c without roll); f = k * val is increasing in k,
+                // so the band and the zero range are index ranges
                 const Lowpass lpw(nn, ex.gen_sr, ex.cutoff_gen, ex.roll);
-                for (int k = tid; k < KK; k += T) {
+                const double lim = lpw.r <= 0 ? lpw.c : lpw.f1;
+                const int kb = first_bin_at_least(lpw.val, lpw.c, KK);          // f(kb) >= c
+                kz = first_bin_above(lpw.val, lim, KK);                         // f(kz) > lim
+                for (int k = kb + tid; k < kz; k += T) {
                     const float wk = lpw.w(k);
                     if (wk != 1.f) cxl<L>(lds, k) = cscale(cxl<L>(lds, k), wk);
+                }
+                if (!(ops2 & (SPEC_WARP | SPEC_STRETCH))) {
+                    for (int k = kz + tid; k < KK; k += T) cxl<L>(lds, k) = make_float2(0.f, 0.f);
+                    kz = KK;
                 }
                 __syncthreads();
             }
@@ -233,13 +272,14 @@ MSG_DEV void spectral_chain(float2* lds, bool evn, const EventRt* __restrict__ e
                 const double ikmax = 1.0 / kmax;
                 const double ip = 1.0 / fmax(1e-6, ex.warp_power);
                 spectral_gather<L, T, 8>(lds, KK, ip <= 1.0,
-                                         [&](int k) { return pow((double)k * ikmax, ip) * kmax; });
+                                         [&](int k) { return pow((double)k * ikmax, ip) * kmax; }, kz);
+                kz = KK;
             }
             if ((ops2 & SPEC_STRETCH) && !SPEC_SKIP(1)) {   // fft_partial_stretch (MS:117-128)
                 drop_edge_imag<L>(lds, evn, nn);
                 const double f = fmax(1e-12, ex.stretch);
                 const double inv_f = 1.0 / f;
-                spectral_gather<L, T, 8>(lds, KK, f < 1.0, [&](int k) { return (double)k * inv_f; });
+                spectral_gather<L, T, 8>(lds, KK, f < 1.0, [&](int k) { return (double)k * inv_f; }, kz);
             }
         }
         SPEC_STAMP(2 + step);

@@ -25,7 +25,8 @@ packed = PackedBatch([msgpu.config_params(cfg, seed=1000 + b, irs=irs) for b in 
 eng = Engine(0)
 out = eng.alloc_output(packed)
 lib = L.lib()
-fn = lib.msg_debug_stamps
+# the compile-time-plan kernels (hot lengths) keep their own counters
+fn = lib.msg_debug_stamps_ct if os.environ.get("MSGPU_SPEC_CT", "1") != "0" else lib.msg_debug_stamps
 fn.argtypes = [C.POINTER(C.c_uint64), C.c_int]
 buf = (C.c_uint64 * 16)()
 lib.msg_debug_skip.argtypes = [C.c_int]
