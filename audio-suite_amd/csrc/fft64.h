@@ -192,12 +192,66 @@ MSG_DEV void f64_pass(double2* buf, int N, int Ns, const double2* __restrict__ t
     __syncthreads();
 }
 
-// Unscaled DFT of buf[0..p.size) through the radix plan.
+// Global-memory variant of one pass (grains beyond the LDS engine): reads
+// src, writes dst (ping-pong), any number of butterflies per thread.
+template <int R, bool INV, int T>
+MSG_DEV void f64_pass_ping(const double2* src, double2* dst, int N, int Ns, const double2* __restrict__ tw) {
+    const int nb = N / R;
+    const int mul = N / (Ns * R);
+    for (int idx = threadIdx.x; idx < nb; idx += T) {
+        const int j = idx % Ns;
+        double2 v[R];
+#pragma unroll
+        for (int q = 0; q < R; ++q) v[q] = src[idx + q * nb];
+        if (Ns > 1) {
+#pragma unroll
+            for (int q = 1; q < R; ++q) {
+                double2 w = tw[(int64_t)j * q * mul];
+                if (INV) w.y = -w.y;
+                v[q] = dmul(v[q], w);
+            }
+        }
+        D64<R, INV>::run(v);
+        const int base = (idx - j) * R + j;
+#pragma unroll
+        for (int q = 0; q < R; ++q) dst[base + q * Ns] = v[q];
+    }
+    __syncthreads();
+}
+
+// Unscaled DFT of buf[0..p.size) through the radix plan.  scr == nullptr:
+// in place through registers (LDS buffers, MAXE >= size / T); otherwise
+// ping-pong through the global scratch scr (same size), result back in buf.
 template <bool INV, int T, int MAXE>
-MSG_DEV void f64_stockham(double2* buf, const Fft64& p) {
+MSG_DEV void f64_stockham(double2* buf, const Fft64& p, double2* scr = nullptr) {
     __syncthreads();
     const int N = p.size;
     int Ns = 1;
+    if (scr) {
+        double2* src = buf;
+        double2* dst = scr;
+        for (int s = 0; s < p.nrad; ++s) {
+            const int R = p.rad[s];
+            switch (R) {
+                case 2: f64_pass_ping<2, INV, T>(src, dst, N, Ns, p.tw); break;
+                case 3: f64_pass_ping<3, INV, T>(src, dst, N, Ns, p.tw); break;
+                case 4: f64_pass_ping<4, INV, T>(src, dst, N, Ns, p.tw); break;
+                case 5: f64_pass_ping<5, INV, T>(src, dst, N, Ns, p.tw); break;
+                case 7: f64_pass_ping<7, INV, T>(src, dst, N, Ns, p.tw); break;
+                case 8: f64_pass_ping<8, INV, T>(src, dst, N, Ns, p.tw); break;
+                case 11: f64_pass_ping<11, INV, T>(src, dst, N, Ns, p.tw); break;
+                case 13: f64_pass_ping<13, INV, T>(src, dst, N, Ns, p.tw); break;
+                default: f64_pass_ping<16, INV, T>(src, dst, N, Ns, p.tw); break;
+            }
+            Ns *= R;
+            double2* t = src; src = dst; dst = t;
+        }
+        if (src != buf) {
+            for (int j = threadIdx.x; j < N; j += T) buf[j] = src[j];
+            __syncthreads();
+        }
+        return;
+    }
     for (int s = 0; s < p.nrad; ++s) {
         const int R = p.rad[s];
         switch (R) {
@@ -218,8 +272,8 @@ MSG_DEV void f64_stockham(double2* buf, const Fft64& p) {
 // Unscaled complex DFT of length p.m in place (Bluestein when p.blue).
 // Ends with a barrier.
 template <bool INV, int T, int MAXE>
-MSG_DEV void f64_cfft(double2* buf, const Fft64& p) {
-    if (!p.blue) { f64_stockham<INV, T, MAXE>(buf, p); return; }
+MSG_DEV void f64_cfft(double2* buf, const Fft64& p, double2* scr = nullptr) {
+    if (!p.blue) { f64_stockham<INV, T, MAXE>(buf, p, scr); return; }
     const int m = p.m, M = p.size;
     const int tid = threadIdx.x;
     __syncthreads();
@@ -233,9 +287,9 @@ MSG_DEV void f64_cfft(double2* buf, const Fft64& p) {
         }
         buf[j] = a;
     }
-    f64_stockham<false, T, MAXE>(buf, p);
+    f64_stockham<false, T, MAXE>(buf, p, scr);
     for (int j = tid; j < M; j += T) buf[j] = dmul(buf[j], p.bspec[j]);
-    f64_stockham<true, T, MAXE>(buf, p);
+    f64_stockham<true, T, MAXE>(buf, p, scr);
     for (int k = tid; k < m; k += T) {
         double2 a = dmul(buf[k], p.chirp[k]);
         if (INV) a.y = -a.y;
@@ -244,12 +298,21 @@ MSG_DEV void f64_cfft(double2* buf, const Fft64& p) {
     __syncthreads();
 }
 
-// Real samples d[0..n) (contiguous doubles) <-> complex slots (x, 0), via registers.
+// Real samples d[0..n) (contiguous doubles) <-> complex slots (x, 0), via
+// registers (LDS) or through the global scratch scr.
 template <int T, int MAXE>
-MSG_DEV void f64_real_to_complex(double2* buf, int n) {
-    double v[MAXE];
+MSG_DEV void f64_real_to_complex(double2* buf, int n, double2* scr = nullptr) {
     const double* d = reinterpret_cast<const double*>(buf);
     __syncthreads();
+    if (scr) {
+        double* sd = reinterpret_cast<double*>(scr);
+        for (int j = threadIdx.x; j < n; j += T) sd[j] = d[j];
+        __syncthreads();
+        for (int j = threadIdx.x; j < n; j += T) buf[j] = d2(sd[j], 0.0);
+        __syncthreads();
+        return;
+    }
+    double v[MAXE];
 #pragma unroll
     for (int i = 0; i < MAXE; ++i) {
         const int j = threadIdx.x + i * T;
@@ -264,10 +327,18 @@ MSG_DEV void f64_real_to_complex(double2* buf, int n) {
     __syncthreads();
 }
 template <int T, int MAXE>
-MSG_DEV void f64_complex_to_real(double2* buf, int n, double scale) {
-    double v[MAXE];
+MSG_DEV void f64_complex_to_real(double2* buf, int n, double scale, double2* scr = nullptr) {
     double* d = reinterpret_cast<double*>(buf);
     __syncthreads();
+    if (scr) {
+        double* sd = reinterpret_cast<double*>(scr);
+        for (int j = threadIdx.x; j < n; j += T) sd[j] = buf[j].x * scale;
+        __syncthreads();
+        for (int j = threadIdx.x; j < n; j += T) d[j] = sd[j];
+        __syncthreads();
+        return;
+    }
+    double v[MAXE];
 #pragma unroll
     for (int i = 0; i < MAXE; ++i) {
         const int j = threadIdx.x + i * T;
@@ -284,14 +355,14 @@ MSG_DEV void f64_complex_to_real(double2* buf, int n, double scale) {
 
 // np.fft.rfft: real d[0..n) -> X[0..n/2] in buf.  Ends with a barrier.
 template <int T, int MAXE>
-MSG_DEV void f64_rfft(double2* buf, const Real64Plan& rp) {
+MSG_DEV void f64_rfft(double2* buf, const Real64Plan& rp, double2* scr = nullptr) {
     const int n = rp.n;
     if (!rp.even) {
-        f64_real_to_complex<T, MAXE>(buf, n);
-        f64_cfft<false, T, MAXE>(buf, rp.c);
+        f64_real_to_complex<T, MAXE>(buf, n, scr);
+        f64_cfft<false, T, MAXE>(buf, rp.c, scr);
         return;
     }
-    f64_cfft<false, T, MAXE>(buf, rp.c);   // packed z_j = x_2j + i x_2j+1, m = n/2
+    f64_cfft<false, T, MAXE>(buf, rp.c, scr);   // packed z_j = x_2j + i x_2j+1, m = n/2
     const int m = n / 2;
     for (int k = threadIdx.x; k <= m / 2; k += T) {
         if (k == 0) {
@@ -321,7 +392,7 @@ MSG_DEV void f64_rfft(double2* buf, const Real64Plan& rp) {
 // np.fft.irfft(X, n): X[0..n/2] in buf -> real d[0..n).  The imaginary parts
 // of X[0] (and X[n/2] for even n) are ignored, as pocketfft's c2r does.
 template <int T, int MAXE>
-MSG_DEV void f64_irfft(double2* buf, const Real64Plan& rp) {
+MSG_DEV void f64_irfft(double2* buf, const Real64Plan& rp, double2* scr = nullptr) {
     const int n = rp.n;
     __syncthreads();
     if (!rp.even) {
@@ -330,8 +401,8 @@ MSG_DEV void f64_irfft(double2* buf, const Real64Plan& rp) {
             if (k == 0) buf[0].y = 0.0;
             else buf[n - k] = dconj(buf[k]);
         }
-        f64_cfft<true, T, MAXE>(buf, rp.c);
-        f64_complex_to_real<T, MAXE>(buf, n, 1.0 / (double)n);
+        f64_cfft<true, T, MAXE>(buf, rp.c, scr);
+        f64_complex_to_real<T, MAXE>(buf, n, 1.0 / (double)n, scr);
         return;
     }
     const int m = n / 2;
@@ -355,7 +426,7 @@ MSG_DEV void f64_irfft(double2* buf, const Real64Plan& rp) {
         buf[k] = Zk;
         if (k2 != k) buf[k2] = Zk2;
     }
-    f64_cfft<true, T, MAXE>(buf, rp.c);
+    f64_cfft<true, T, MAXE>(buf, rp.c, scr);
     const double s = 1.0 / (double)m;
     double* d = reinterpret_cast<double*>(buf);
     for (int j = threadIdx.x; j < n; j += T) d[j] *= s;

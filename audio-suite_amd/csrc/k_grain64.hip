@@ -3,30 +3,42 @@
 #include "launch.h"
 
 void grain64_init_attrs() {
-    (void)hipFuncSetAttribute((const void*)k_grain64, hipFuncAttributeMaxDynamicSharedMemorySize, G64_CAP * 16);
-    (void)hipFuncSetAttribute((const void*)k_chain64, hipFuncAttributeMaxDynamicSharedMemorySize, G64_CAP * 16);
+    (void)hipFuncSetAttribute((const void*)k_grain64<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              G64_CAP * 16);
+    (void)hipFuncSetAttribute((const void*)k_chain64<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              G64_CAP * 16);
+    (void)hipFuncSetAttribute((const void*)k_fft64_one, hipFuncAttributeMaxDynamicSharedMemorySize, G64_CAP * 16);
 }
 
-hipError_t launch_grain64(unsigned grid, int lds_bytes, hipStream_t s, const msg_preset* presets, const Ev64* ev64,
-                          const PresetRt* rt, const Real64Plan* plans, const int32_t* list, int n_list,
-                          const double* irbank, const uint8_t* imgbank, nprng::Zig z, double* micro64,
+hipError_t launch_grain64(const G64Global* g, unsigned grid, int lds_bytes, hipStream_t s, const msg_preset* presets,
+                          const Ev64* ev64, const PresetRt* rt, const Real64Plan* plans, const int32_t* list,
+                          int n_list, const double* irbank, const uint8_t* imgbank, nprng::Zig z, double* micro64,
                           double* grain64, double2* save, float* grain_pool) {
-    hipLaunchKernelGGL(k_grain64, dim3(grid), dim3(G64_T), lds_bytes, s, presets, ev64, rt, plans, list, n_list,
-                       irbank, imgbank, z, micro64, grain64, save, grain_pool);
+    if (g)
+        hipLaunchKernelGGL(k_grain64<true>, dim3(grid), dim3(G64_T), 0, s, presets, ev64, rt, plans, list, n_list,
+                           irbank, imgbank, z, micro64, grain64, save, grain_pool, g->A, g->B, g->mask, g->slot_cap,
+                           g->mask_words);
+    else
+        hipLaunchKernelGGL(k_grain64<false>, dim3(grid), dim3(G64_T), lds_bytes, s, presets, ev64, rt, plans, list,
+                           n_list, irbank, imgbank, z, micro64, grain64, save, grain_pool, (double2*)nullptr,
+                           (double2*)nullptr, (uint32_t*)nullptr, (int64_t)0, (int64_t)0);
     return hipGetLastError();
 }
 
-hipError_t launch_chain64(unsigned grid, int lds_bytes, hipStream_t s, const msg_preset* presets, const Ev64* ev64,
-                          const Chain64* chains, int n_chains, const Real64Plan* plans, const double* grain64,
-                          double* state, float* grain_pool) {
-    hipLaunchKernelGGL(k_chain64, dim3(grid), dim3(G64_T), lds_bytes, s, presets, ev64, chains, n_chains, plans,
-                       grain64, state, grain_pool);
+hipError_t launch_chain64(const G64Global* g, unsigned grid, int lds_bytes, hipStream_t s, const msg_preset* presets,
+                          const Ev64* ev64, const Chain64* chains, int n_chains, const Real64Plan* plans,
+                          const double* grain64, double* state, float* grain_pool) {
+    if (g)
+        hipLaunchKernelGGL(k_chain64<true>, dim3(grid), dim3(G64_T), 0, s, presets, ev64, chains, n_chains, plans,
+                           grain64, state, grain_pool, g->A, g->B, g->slot_cap);
+    else
+        hipLaunchKernelGGL(k_chain64<false>, dim3(grid), dim3(G64_T), lds_bytes, s, presets, ev64, chains, n_chains,
+                           plans, grain64, state, grain_pool, (double2*)nullptr, (double2*)nullptr, (int64_t)0);
     return hipGetLastError();
 }
 
 hipError_t launch_fft64_one(int lds_bytes, hipStream_t s, const Real64Plan* plans, int plan, int inverse,
-                            double* io) {
-    (void)hipFuncSetAttribute((const void*)k_fft64_one, hipFuncAttributeMaxDynamicSharedMemorySize, G64_CAP * 16);
-    hipLaunchKernelGGL(k_fft64_one, dim3(1), dim3(G64_T), lds_bytes, s, plans, plan, inverse, io);
+                            double* io, double2* gA, double2* gB) {
+    hipLaunchKernelGGL(k_fft64_one, dim3(1), dim3(G64_T), gA ? 0 : lds_bytes, s, plans, plan, inverse, io, gA, gB);
     return hipGetLastError();
 }

@@ -120,7 +120,8 @@ MSG_DEV void copy_to(double* s, const double* d, int n) {
 // ---------------------------------------------------------------------------
 MSG_DEV void gen64(const msg_preset& pr, const PresetRt& r, const Ev64& ev, const Real64Plan& rp,
                    const double* __restrict__ normals, const double* __restrict__ irbank,
-                   const uint8_t* __restrict__ imgbank, const nprng::Zig& z, double2* buf, G64Shared& sh) {
+                   const uint8_t* __restrict__ imgbank, const nprng::Zig& z, double2* buf, double2* scr,
+                   G64Shared& sh) {
     double* d = reinterpret_cast<double*>(buf);
     const int n = ev.n;
     double* s = d + n;                      // scratch: n doubles after the signal
@@ -155,7 +156,7 @@ MSG_DEV void gen64(const msg_preset& pr, const PresetRt& r, const Ev64& ev, cons
     case MSG_GEN_NOISE_BURST: case MSG_GEN_SKEWED: {
         // tilted_noise (MS:224-233)
         for (int j = tid; j < n; j += G64_T) d[j] = normals[j];
-        f64_rfft<G64_T, G64_MAXE>(buf, rp);
+        f64_rfft<G64_T, G64_MAXE>(buf, rp, scr);
         const double val = 1.0 / ((double)n * (1.0 / sr));
         const double alpha = log(pow(10.0, tilt_db / 20.0)) / log(2.0);
         const int K = n / 2 + 1;
@@ -163,7 +164,7 @@ MSG_DEV void gen64(const msg_preset& pr, const PresetRt& r, const Ev64& ev, cons
             const double fk = (K > 1 && k == 0) ? val : (double)k * val;
             buf[k] = dscale(buf[k], pow(fk / fmax(1e-12, val), alpha));
         }
-        f64_irfft<G64_T, G64_MAXE>(buf, rp);
+        f64_irfft<G64_T, G64_MAXE>(buf, rp, scr);
         const bool skew = mode == MSG_GEN_SKEWED;
         const double tau = fmax(1e-6, (pr.micro_ms / 1000.0) * (skew ? 0.2 : 0.25));
         if (skew) copy_to(s, d, n);
@@ -467,20 +468,21 @@ MSG_DEV void gather64(C* buf, int K, bool ascending, Src src) {
     }
 }
 // partial_lock_stretch (MS:130-148) on the resident spectrum
-MSG_DEV void partial_lock64(double2* buf, int K, double factor, int top_n, int neigh, G64Shared& sh) {
+MSG_DEV void partial_lock64(double2* buf, int K, double factor, int top_n, int neigh, G64Shared& sh,
+                            uint32_t* mask) {
     const int nb = K - 1;                   // candidates: bins 1..K-1
     int cnt;
     if (top_n > 0) cnt = top_n < nb ? top_n : nb;
     else if (top_n == 0) cnt = nb;          // a[-0:] is the whole array
     else cnt = nb + top_n > 0 ? nb + top_n : 0;
-    for (int i = threadIdx.x; i < (int)(sizeof(sh.mask) / 4); i += G64_T) sh.mask[i] = 0u;
+    for (int i = threadIdx.x; i < (K + 31) / 32 + 1; i += G64_T) mask[i] = 0u;
     __syncthreads();
     // descending selection: pick the largest |X| not yet taken, cnt times
     for (int p = 0; p < cnt; ++p) {
         double bv = -1.0;
         int bk = -1;
         for (int k = 1 + threadIdx.x; k < K; k += G64_T) {
-            if ((sh.mask[k >> 5] >> (k & 31)) & 1u) continue;
+            if ((mask[k >> 5] >> (k & 31)) & 1u) continue;
             const double m = hypot(buf[k].x, buf[k].y);
             if (m > bv || (m == bv && k > bk)) { bv = m; bk = k; }
         }
@@ -500,7 +502,7 @@ MSG_DEV void partial_lock64(double2* buf, int K, double factor, int top_n, int n
             const int slot = cnt - 1 - p;
             sh.peak_x[slot] = buf[kk];
             sh.peak_k2[slot] = (int)rint((double)kk * factor);
-            sh.mask[kk >> 5] |= 1u << (kk & 31);
+            mask[kk >> 5] |= 1u << (kk & 31);
         }
         __syncthreads();
     }
@@ -526,18 +528,19 @@ MSG_DEV void partial_lock64(double2* buf, int K, double factor, int top_n, int n
 
 // cepstral_warp (MS:150-163): the spectrum X is saved per thread (same bins
 // read back by the same thread), the cepstrum round trip runs in the buffer.
-MSG_DEV void cepstral64(double2* buf, const Real64Plan& rp, double factor, double2* __restrict__ save) {
+MSG_DEV void cepstral64(double2* buf, const Real64Plan& rp, double factor, double2* __restrict__ save,
+                        double2* scr) {
     const int n = rp.n, K = n / 2 + 1;
     for (int k = threadIdx.x; k < K; k += G64_T) {
         const double2 x = buf[k];
         save[k] = x;
         buf[k] = d2(log(hypot(x.x, x.y) + 1e-12), 0.0);
     }
-    f64_irfft<G64_T, G64_MAXE>(buf, rp);                       // cep (n real)
+    f64_irfft<G64_T, G64_MAXE>(buf, rp, scr);                  // cep (n real)
     double* d = reinterpret_cast<double*>(buf);
     const double inv_f = 1.0 / fmax(1e-12, factor);
     gather64<double>(d, n, inv_f > 1.0, [&](int t) { return (double)t * inv_f; });
-    f64_rfft<G64_T, G64_MAXE>(buf, rp);
+    f64_rfft<G64_T, G64_MAXE>(buf, rp, scr);
     for (int k = threadIdx.x; k < K; k += G64_T) {
         const double mag2 = exp(buf[k].x);
         const double2 x = save[k];
@@ -624,16 +627,25 @@ MSG_DEV void waveguide64(double* d, int n, double sr, const msg_preset& pr, uint
 // ---------------------------------------------------------------------------
 // k_grain64: one event, generator -> spectral stages -> physics -> multi-band.
 // ---------------------------------------------------------------------------
+// GLOBAL = false: the grain in LDS, one event per workgroup.  GLOBAL = true:
+// grains beyond the LDS engine; each workgroup walks events li = blockIdx.x +
+// k gridDim.x with its own global slot (buffer gA, FFT ping-pong scratch gB,
+// partial-lock mask gmask).
+template <bool GLOBAL>
 __global__ void __launch_bounds__(G64_T)
 k_grain64(const msg_preset* __restrict__ presets, const Ev64* __restrict__ ev64, const PresetRt* __restrict__ rt,
           const Real64Plan* __restrict__ plans, const int32_t* __restrict__ list, int n_list,
           const double* __restrict__ irbank, const uint8_t* __restrict__ imgbank, nprng::Zig z,
           double* __restrict__ micro64, double* __restrict__ grain64, double2* __restrict__ save,
-          float* __restrict__ grain_pool) {
-    extern __shared__ __attribute__((aligned(16))) double2 buf[];
+          float* __restrict__ grain_pool, double2* gA, double2* gB, uint32_t* gmask, int64_t slot_cap,
+          int64_t mask_words) {
+    extern __shared__ __attribute__((aligned(16))) double2 lds_buf[];
     __shared__ G64Shared sh;
-    const int li = blockIdx.x;
-    if (li >= n_list) return;
+    double2* buf = GLOBAL ? gA + (int64_t)blockIdx.x * slot_cap : lds_buf;
+    double2* scr = GLOBAL ? gB + (int64_t)blockIdx.x * slot_cap : nullptr;
+    uint32_t* mask = GLOBAL ? gmask + (int64_t)blockIdx.x * mask_words : sh.mask;
+    for (int li = blockIdx.x; li < n_list; li += GLOBAL ? (int)gridDim.x : n_list) {
+    __syncthreads();
     const Ev64 ev = ev64[list[li]];
     const msg_preset& pr = presets[ev.preset];
     const PresetRt& r = rt[ev.preset];
@@ -643,13 +655,13 @@ k_grain64(const msg_preset* __restrict__ presets, const Ev64* __restrict__ ev64,
     const uint64_t seed = (uint64_t)(pr.seed + ev.index);
     const double sr = (double)ev.gen_sr;
 
-    gen64(pr, r, ev, rp, micro64 + ev.off64, irbank, imgbank, z, buf, sh);
+    gen64(pr, r, ev, rp, micro64 + ev.off64, irbank, imgbank, z, buf, scr, sh);
     for (int j = threadIdx.x; j < n; j += G64_T) micro64[ev.off64 + j] = d[j];   // micro_last (MS:688)
 
     const int ops = ev.ops;
     if (ops & G64_SPEC) {
         const int K = n / 2 + 1;
-        f64_rfft<G64_T, G64_MAXE>(buf, rp);
+        f64_rfft<G64_T, G64_MAXE>(buf, rp, scr);
         if (ops & G64_LOWPASS) {                                // MS:690-692
             const Freq64 fq(n, sr);
             const double nyq = 0.5 * sr;
@@ -671,8 +683,8 @@ k_grain64(const msg_preset* __restrict__ presets, const Ev64* __restrict__ ev64,
         const bool faithful = (ops & G64_CEP) || (pr.flags & MSG_F_IMPRINT);
         auto boundary = [&]() {
             if (faithful) {
-                f64_irfft<G64_T, G64_MAXE>(buf, rp);
-                f64_rfft<G64_T, G64_MAXE>(buf, rp);
+                f64_irfft<G64_T, G64_MAXE>(buf, rp, scr);
+                f64_rfft<G64_T, G64_MAXE>(buf, rp, scr);
             } else {
                 drop_edge_imag64(buf, rp);
             }
@@ -685,22 +697,22 @@ k_grain64(const msg_preset* __restrict__ presets, const Ev64* __restrict__ ev64,
         }
         if (ops & G64_CEP) {                                    // MS:696-697
             boundary();
-            cepstral64(buf, rp, pr.cep_factor, save + ev.save_off);
+            cepstral64(buf, rp, pr.cep_factor, save + ev.save_off, scr);
         }
         if (ops & G64_LOCK) {                                   // MS:699-700
             boundary();
-            partial_lock64(buf, K, ev.stretch, pr.pl_top_n, pr.pl_neigh, sh);
+            partial_lock64(buf, K, ev.stretch, pr.pl_top_n, pr.pl_neigh, sh, mask);
         } else if (ops & G64_STRETCH) {                         // MS:701-702
             boundary();
             const double inv_f = 1.0 / fmax(1e-12, ev.stretch);
             gather64<double2>(buf, K, inv_f > 1.0, [&](int k) { return (double)k * inv_f; });
         }
-        f64_irfft<G64_T, G64_MAXE>(buf, rp);
+        f64_irfft<G64_T, G64_MAXE>(buf, rp, scr);
     }
     if (ops & G64_RES) resonator64(d, n, sr, pr, seed, z, sh);  // MS:704-710
     if (ops & G64_WG) waveguide64(d, n, sr, pr, seed, sh);      // MS:712-717
     if (ops & G64_MB) {                                         // MS:722-727
-        f64_rfft<G64_T, G64_MAXE>(buf, rp);
+        f64_rfft<G64_T, G64_MAXE>(buf, rp, scr);
         const Freq64 fq(n, sr);
         const double nyq = 0.5 * sr;
         const int K = n / 2 + 1;
@@ -715,26 +727,30 @@ k_grain64(const msg_preset* __restrict__ presets, const Ev64* __restrict__ ev64,
             }
             buf[k] = dscale(buf[k], w);
         }
-        f64_irfft<G64_T, G64_MAXE>(buf, rp);
+        f64_irfft<G64_T, G64_MAXE>(buf, rp, scr);
     }
     __syncthreads();
     for (int j = threadIdx.x; j < n; j += G64_T) {
         grain64[ev.off64 + j] = d[j];                          // grain_last (MS:729)
         if (!(ops & G64_CHAIN)) grain_pool[ev.grain_off + j] = (float)d[j];
     }
+    }   // events
 }
 
 // ---------------------------------------------------------------------------
 // k_chain64: event feedback + spectral imprint, events of one preset in order.
 // ---------------------------------------------------------------------------
 
+template <bool GLOBAL>
 __global__ void __launch_bounds__(G64_T)
 k_chain64(const msg_preset* __restrict__ presets, const Ev64* __restrict__ ev64, const Chain64* __restrict__ chains,
           int n_chains, const Real64Plan* __restrict__ plans, const double* __restrict__ grain64,
-          double* __restrict__ state, float* __restrict__ grain_pool) {
-    extern __shared__ __attribute__((aligned(16))) double2 buf[];
-    const int ci = blockIdx.x;
-    if (ci >= n_chains) return;
+          double* __restrict__ state, float* __restrict__ grain_pool, double2* gA, double2* gB, int64_t slot_cap) {
+    extern __shared__ __attribute__((aligned(16))) double2 lds_buf[];
+    double2* buf = GLOBAL ? gA + (int64_t)blockIdx.x * slot_cap : lds_buf;
+    double2* scr = GLOBAL ? gB + (int64_t)blockIdx.x * slot_cap : nullptr;
+    for (int ci = blockIdx.x; ci < n_chains; ci += GLOBAL ? (int)gridDim.x : n_chains) {
+    __syncthreads();
     const Chain64 ch = chains[ci];
     const msg_preset& pr = presets[ch.preset];
     double* prev = state + ch.prev_off;
@@ -757,7 +773,7 @@ k_chain64(const msg_preset* __restrict__ presets, const Ev64* __restrict__ ev64,
         }
         if (imp_on && n >= 64 && amount > 0) {                 // MS:569-581
             const int K = n / 2 + 1;
-            f64_rfft<G64_T, G64_MAXE>(buf, rp);
+            f64_rfft<G64_T, G64_MAXE>(buf, rp, scr);
             const bool reset = (mem_k != K);
             for (int k = threadIdx.x; k < K; k += G64_T) {
                 const double2 x = buf[k];
@@ -771,7 +787,7 @@ k_chain64(const msg_preset* __restrict__ presets, const Ev64* __restrict__ ev64,
                 buf[k] = d2(mag2 * ca, mag2 * sa);
             }
             mem_k = K;
-            f64_irfft<G64_T, G64_MAXE>(buf, rp);
+            f64_irfft<G64_T, G64_MAXE>(buf, rp, scr);
         }
         __syncthreads();
         for (int j = threadIdx.x; j < n; j += G64_T) {
@@ -780,6 +796,7 @@ k_chain64(const msg_preset* __restrict__ presets, const Ev64* __restrict__ ev64,
         }
         prev_n = n;
     }
+    }   // chains
 }
 #endif  // __HIPCC__
 
@@ -787,16 +804,20 @@ k_chain64(const msg_preset* __restrict__ presets, const Ev64* __restrict__ ev64,
 // Single float64 real transform (tests / precision probes): inverse = 0 ->
 // io[0..n) real in, io[0..2K) = X[0..K) out; inverse = 1 -> X in, real out.
 __global__ void __launch_bounds__(G64_T)
-k_fft64_one(const Real64Plan* __restrict__ plans, int plan, int inverse, double* __restrict__ io) {
-    extern __shared__ __attribute__((aligned(16))) double2 buf[];
+k_fft64_one(const Real64Plan* __restrict__ plans, int plan, int inverse, double* __restrict__ io,
+            double2* gA, double2* gB) {
+    extern __shared__ __attribute__((aligned(16))) double2 lds_buf[];
+    double2* buf = gA ? gA : lds_buf;      // global buffers: the engine's ping-pong mode
+    double2* scr = gA ? gB : nullptr;
     const Real64Plan& rp = plans[plan];
     const int n = rp.n, K = n / 2 + 1;
     double* d = reinterpret_cast<double*>(buf);
     const int cnt = inverse ? 2 * K : n;
     for (int j = threadIdx.x; j < cnt; j += G64_T) d[j] = io[j];
     __syncthreads();
-    if (inverse) f64_irfft<G64_T, G64_MAXE>(buf, rp);
-    else f64_rfft<G64_T, G64_MAXE>(buf, rp);
+    if (inverse) f64_irfft<G64_T, G64_MAXE>(buf, rp, scr);
+    else f64_rfft<G64_T, G64_MAXE>(buf, rp, scr);
+    __syncthreads();
     const int cnt2 = inverse ? n : 2 * K;
     for (int j = threadIdx.x; j < cnt2; j += G64_T) io[j] = d[j];
 }

@@ -47,16 +47,23 @@ hipError_t launch_fft_bench(bool po2, unsigned grid, int lds_bytes, hipStream_t 
 
 // float64 grain chain (kernels_grain64.h): one workgroup per event / per chained preset
 constexpr int G64_THREADS = 512, G64_SLOTS = 8192, G64_MAXPAR_HOST = 256;   // must match kernels_grain64.h
+// global-memory slots for grains beyond the LDS engine (persistent workgroups)
+struct G64Global {
+    double2* A;           // grain buffers, slot_cap double2 per workgroup
+    double2* B;           // FFT ping-pong scratch, same size
+    uint32_t* mask;       // partial-lock selection bits, mask_words per workgroup
+    int64_t slot_cap, mask_words;
+};
 void grain64_init_attrs();
-hipError_t launch_grain64(unsigned grid, int lds_bytes, hipStream_t s, const msg_preset* presets, const Ev64* ev64,
-                          const PresetRt* rt, const Real64Plan* plans, const int32_t* list, int n_list,
-                          const double* irbank, const uint8_t* imgbank, nprng::Zig z, double* micro64,
+hipError_t launch_grain64(const G64Global* g, unsigned grid, int lds_bytes, hipStream_t s, const msg_preset* presets,
+                          const Ev64* ev64, const PresetRt* rt, const Real64Plan* plans, const int32_t* list,
+                          int n_list, const double* irbank, const uint8_t* imgbank, nprng::Zig z, double* micro64,
                           double* grain64, double2* save, float* grain_pool);
-hipError_t launch_chain64(unsigned grid, int lds_bytes, hipStream_t s, const msg_preset* presets, const Ev64* ev64,
-                          const Chain64* chains, int n_chains, const Real64Plan* plans, const double* grain64,
-                          double* state, float* grain_pool);
+hipError_t launch_chain64(const G64Global* g, unsigned grid, int lds_bytes, hipStream_t s, const msg_preset* presets,
+                          const Ev64* ev64, const Chain64* chains, int n_chains, const Real64Plan* plans,
+                          const double* grain64, double* state, float* grain_pool);
 hipError_t launch_fft64_one(int lds_bytes, hipStream_t s, const Real64Plan* plans, int plan, int inverse,
-                            double* io);
+                            double* io, double2* gA, double2* gB);
 
 // odd-length stereo rotation (kernels_stereo_odd.h): Bluestein through M = pow2 >= 2n-1
 void stereo_odd_init_attrs();

@@ -107,6 +107,8 @@ struct msg_ctx {
     DevBuf<double2> save64;
     DevBuf<Chain64> chains;
     DevBuf<uint8_t> imgbank;
+    DevBuf<double2> g64A, g64B;                 // global-class float64 grains (G64Global)
+    DevBuf<uint32_t> g64mask;
     // odd-length stereo rotation (kernels_stereo_odd.h)
     std::map<int64_t, DevBuf<float2>> so_bp;   // chirp kernel spectra by n
     DevBuf<float2> so_A;
@@ -472,6 +474,7 @@ void msg_destroy(msg_ctx* ctx) {
     ctx->ev64.release(); ctx->g64_list.release(); ctx->gen64_list.release(); ctx->gen64_off.release();
     ctx->micro64.release(); ctx->grain64.release(); ctx->state64.release(); ctx->save64.release();
     ctx->chains.release(); ctx->imgbank.release();
+    ctx->g64A.release(); ctx->g64B.release(); ctx->g64mask.release();
     for (auto& kv : ctx->so_bp) kv.second.release();
     ctx->so_A.release(); ctx->so_r2.release();
     delete ctx;
@@ -654,16 +657,23 @@ int msg_fft64(msg_ctx* ctx, int32_t n, int32_t inverse, const double* in, double
     const int pi = real64_plan(ctx->plans64, n, why);
     if (pi < 0) return fail(ctx, MSG_E_DEVICE, why);
     const Real64Plan rp = ctx->plans64.host[pi];
-    if (rp.cap > G64_SLOTS) return fail(ctx, MSG_E_UNSUPPORTED, "transform exceeds the LDS float64 engine");
     HIPCHK(ctx, sync_plans(ctx->plans64, nullptr));
     const int K = n / 2 + 1;
     const size_t cnt = (size_t)std::max(n, 2 * K);
     double* io = nullptr;
     HIPCHK(ctx, hipMalloc(&io, cnt * sizeof(double)));
     hipError_t e = hipMemcpy(io, in, (inverse ? 2 * K : n) * sizeof(double), hipMemcpyHostToDevice);
-    if (e == hipSuccess) e = launch_fft64_one(rp.cap * 16, nullptr, ctx->plans64.dev.p, pi, inverse ? 1 : 0, io);
+    double2* gA = nullptr;
+    double2* gB = nullptr;
+    if (e == hipSuccess && rp.cap > G64_SLOTS) {     // beyond LDS: the engine's global ping-pong mode
+        e = hipMalloc(&gA, (size_t)rp.cap * sizeof(double2));
+        if (e == hipSuccess) e = hipMalloc(&gB, (size_t)rp.cap * sizeof(double2));
+    }
+    if (e == hipSuccess) e = launch_fft64_one(rp.cap * 16, nullptr, ctx->plans64.dev.p, pi, inverse ? 1 : 0, io, gA, gB);
     if (e == hipSuccess) e = hipMemcpy(out, io, (inverse ? n : 2 * K) * sizeof(double), hipMemcpyDeviceToHost);
     hipFree(io);
+    if (gA) hipFree(gA);
+    if (gB) hipFree(gB);
     HIPCHK(ctx, e);
     return MSG_OK;
 }
@@ -818,7 +828,10 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
     int64_t sum64 = 0, save_sum = 0, state_sum = 0;
     int64_t r2_sum = 0, so_M = 0;
     std::vector<int32_t> odd_presets;
-    int g64_cap = 0;
+    int g64_cap = 0;                                      // LDS slots of the LDS-class float64 grains
+    int64_t g64_big_cap = 0;                              // slot size of the global-class grains
+    std::vector<int32_t> g64_lds, g64_glb;                // Ev64 indices by class
+    std::vector<Chain64> chains_glb;
     for (int p = 0; p < P; ++p) {
         const msg_preset& pr = presets[p];
         const msg_plan_info& inf = info[p];
@@ -939,9 +952,23 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
         pool += (inf.pool_len + 3) & ~int64_t(3);   // 16-byte aligned grain regions (float4 loads)
         ysum += (inf.out_n + 3) & ~int64_t(3);   // keep every mono region 16-byte aligned
         // events
-        const bool precise = is_precise(pr);
+        bool precise = is_precise(pr);
+        if (!precise) {
+            // grains beyond the LDS-resident float32 spectral kernels run the float64
+            // chain in global memory (micro_ms up to 80 ms at 30 MHz: 2.4 M samples)
+            for (int k = 0; k < inf.n_events && !precise; ++k) {
+                const msg_event& e = ctx->h_events[slot_base[p] + k];
+                if (!spec_ops(pr, e) || (use_ct && spectral_ct_plan(e.n) >= 0)) continue;
+                std::string why;
+                const int pi = real_plan(ctx->grain_plans, e.n, why);
+                if (pi < 0) return fail(ctx, MSG_E_DEVICE, "grain plan: " + why);
+                const RealPlan& gp = ctx->grain_plans.host[pi];
+                if (gp.lds_bytes > LDS_MAX || gp.c.size > SPEC_M_BIG) precise = true;
+            }
+        }
         if (precise && inf.n_events > 0) {
             const bool chained = (pr.flags & (MSG_F_EVENT_FEEDBACK | MSG_F_IMPRINT)) != 0;
+            bool chain_global = false;
             if (chained) {
                 Chain64 c;
                 memset(&c, 0, sizeof(c));
@@ -953,6 +980,7 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
                 state_sum += ((inf.max_n + 1) & ~1) + ((inf.max_n / 2 + 2) & ~1);
                 chains.push_back(c);
             }
+            const size_t ev_first = ev64.size();
             for (int k = 0; k < inf.n_events; ++k) {
                 const int ei = slot_base[p] + k;
                 const msg_event& e = ctx->h_events[ei];
@@ -963,10 +991,14 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
                 v.plan = real64_plan(ctx->plans64, e.n, why);
                 if (v.plan < 0) return fail(ctx, MSG_E_DEVICE, "float64 grain plan: " + why);
                 const Real64Plan& gp = ctx->plans64.host[v.plan];
-                if (gp.cap > G64_SLOTS)
-                    return fail(ctx, MSG_E_UNSUPPORTED, "grain of " + std::to_string(e.n) +
-                                " samples exceeds the LDS-resident float64 chain (8192 complex slots)");
-                g64_cap = std::max(g64_cap, gp.cap);
+                if (gp.cap > G64_SLOTS) {        // beyond the LDS engine: a global-memory slot
+                    g64_big_cap = std::max<int64_t>(g64_big_cap, gp.cap);
+                    g64_glb.push_back((int32_t)ev64.size());
+                    chain_global = true;
+                } else {
+                    g64_cap = std::max(g64_cap, gp.cap);
+                    g64_lds.push_back((int32_t)ev64.size());
+                }
                 v.ops = g64_ops(pr, e);
                 v.n = e.n;
                 v.n0 = msgplan::grain_len(e.gen_sr, pr.micro_ms, 16);
@@ -1002,6 +1034,11 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
                 sum64 += (e.n + 1) & ~1;
                 last64[p] = (int32_t)ev64.size();
                 ev64.push_back(v);
+            }
+            (void)ev_first;
+            if (chained && chain_global) {                  // the chain walks big grains too
+                chains_glb.push_back(chains.back());
+                chains.pop_back();
             }
             continue;
         }
@@ -1048,8 +1085,32 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
     HIPCHK(ctx, sync_plans(ctx->grain_plans, s));
     HIPCHK(ctx, sync_plans(ctx->fir_plans, s));
     HIPCHK(ctx, sync_plans(ctx->plans64, s));
-    std::vector<int32_t> g64_list(ev64.size());
-    for (size_t i = 0; i < ev64.size(); ++i) g64_list[i] = (int32_t)i;
+    std::vector<int32_t> g64_list(g64_lds);
+    g64_list.insert(g64_list.end(), g64_glb.begin(), g64_glb.end());
+    const size_t n_lds_chains = chains.size();
+    chains.insert(chains.end(), chains_glb.begin(), chains_glb.end());
+    // global slots: persistent workgroups, at most ~8 GB of grain + scratch buffers
+    G64Global gg{};
+    unsigned g_grid = 0, c_grid = 0;
+    if (!g64_glb.empty() || !chains_glb.empty()) {
+        int64_t cap = g64_big_cap;
+        for (const Chain64& c : chains_glb)
+            for (int q = 0; q < c.n_events; ++q)
+                cap = std::max<int64_t>(cap, ctx->plans64.host[ev64[c.ev_begin + q].plan].cap);
+        gg.slot_cap = (cap + 1) & ~int64_t(1);
+        gg.mask_words = gg.slot_cap / 32 + 2;
+        const int64_t per_slot = 2 * gg.slot_cap * 16 + gg.mask_words * 4;
+        const int64_t lim = std::max<int64_t>(1, std::min<int64_t>(1024, (int64_t(8) << 30) / per_slot));
+        g_grid = (unsigned)std::min<int64_t>((int64_t)g64_glb.size(), lim);
+        c_grid = (unsigned)std::min<int64_t>((int64_t)chains_glb.size(), lim);
+        const int64_t slots = std::max<int64_t>(std::max(g_grid, c_grid), 1);
+        HIPCHK(ctx, ctx->g64A.ensure(slots * gg.slot_cap));
+        HIPCHK(ctx, ctx->g64B.ensure(slots * gg.slot_cap));
+        HIPCHK(ctx, ctx->g64mask.ensure(slots * gg.mask_words));
+        gg.A = ctx->g64A.p;
+        gg.B = ctx->g64B.p;
+        gg.mask = ctx->g64mask.p;
+    }
     HIPCHK(ctx, ctx->ev64.ensure(ev64.size()));
     HIPCHK(ctx, ctx->g64_list.ensure(g64_list.size()));
     HIPCHK(ctx, ctx->gen64_list.ensure(gen64_list.size()));
@@ -1150,15 +1211,24 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
         HIPCHK(ctx, launch_spectral(true, (unsigned)spec_big.size(), spec_big_lds, s, ctx->presets.p,
                                     ctx->events.p, ctx->ert.p, ctx->prt.p, ctx->grain_plans.dev.p, ctx->spec_big.p,
                                     (int)spec_big.size(), ctx->micro.p, ctx->grain.p));
-    if (!ev64.empty())
-        HIPCHK(ctx, launch_grain64((unsigned)ev64.size(), g64_cap * 16, s, ctx->presets.p, ctx->ev64.p, ctx->prt.p,
-                                   ctx->plans64.dev.p, ctx->g64_list.p, (int)ev64.size(), ctx->irbank.p,
+    if (!g64_lds.empty())
+        HIPCHK(ctx, launch_grain64(nullptr, (unsigned)g64_lds.size(), g64_cap * 16, s, ctx->presets.p, ctx->ev64.p,
+                                   ctx->prt.p, ctx->plans64.dev.p, ctx->g64_list.p, (int)g64_lds.size(),
+                                   ctx->irbank.p, ctx->imgbank.p, ctx->dzig, ctx->micro64.p, ctx->grain64.p,
+                                   ctx->save64.p, ctx->grain.p));
+    if (!g64_glb.empty())
+        HIPCHK(ctx, launch_grain64(&gg, g_grid, 0, s, ctx->presets.p, ctx->ev64.p, ctx->prt.p, ctx->plans64.dev.p,
+                                   ctx->g64_list.p + g64_lds.size(), (int)g64_glb.size(), ctx->irbank.p,
                                    ctx->imgbank.p, ctx->dzig, ctx->micro64.p, ctx->grain64.p, ctx->save64.p,
                                    ctx->grain.p));
-    if (!chains.empty())
-        HIPCHK(ctx, launch_chain64((unsigned)chains.size(), g64_cap * 16, s, ctx->presets.p, ctx->ev64.p,
-                                   ctx->chains.p, (int)chains.size(), ctx->plans64.dev.p, ctx->grain64.p,
+    if (n_lds_chains > 0)
+        HIPCHK(ctx, launch_chain64(nullptr, (unsigned)n_lds_chains, g64_cap * 16, s, ctx->presets.p, ctx->ev64.p,
+                                   ctx->chains.p, (int)n_lds_chains, ctx->plans64.dev.p, ctx->grain64.p,
                                    ctx->state64.p, ctx->grain.p));
+    if (!chains_glb.empty())
+        HIPCHK(ctx, launch_chain64(&gg, c_grid, 0, s, ctx->presets.p, ctx->ev64.p, ctx->chains.p + n_lds_chains,
+                                   (int)chains_glb.size(), ctx->plans64.dev.p, ctx->grain64.p, ctx->state64.p,
+                                   ctx->grain.p));
     // ---- overlap-add x ADSR ----
     stage_mark(ctx, 4, s);
     hipLaunchKernelGGL(k_ola_env, dim3((unsigned)tiles), dim3(OLA_T), 0, s, ctx->events.p, ctx->prt.p,

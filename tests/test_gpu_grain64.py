@@ -166,8 +166,6 @@ def test_float64_chain_meta(m, O, irs):
 def test_float64_chain_errors(m):
     with pytest.raises(ValueError):          # 60-sample atoms do not broadcast into a 128-sample grain
         m.render(base(m, gen_mode="Wavelet atoms", time_unfold=1.0))
-    with pytest.raises(NotImplementedError):  # 24000-sample grain exceeds the LDS float64 chain
-        m.render(base(m, base_sr=192000, time_unfold=100.0, cep_warp_on=True, out_dur_s=0.05))
 
 
 def _fft64(m, n, inverse, data):
@@ -204,3 +202,32 @@ def test_fft64_engine_vs_numpy(m, n):
     fo = np.sqrt(np.mean(np.abs(ours[3 * Xm.size // 4:]) ** 2))
     fr = np.sqrt(np.mean(np.abs(ref[3 * Xm.size // 4:]) ** 2))
     print(f"n={n}: masked round-trip floor rms device {fo:.3e}  numpy {fr:.3e}  ratio {fo / max(fr, 1e-300):.2f}")
+
+
+@pytest.mark.parametrize("n", [12000, 10007, 20002, 65536])
+def test_fft64_engine_global_mode(m, n):
+    """Transforms beyond the LDS engine run the global ping-pong mode."""
+    rng = np.random.default_rng(n)
+    x = rng.standard_normal(n)
+    Xr = np.fft.rfft(x)
+    X = _fft64(m, n, False, x)
+    assert np.max(np.abs(X - Xr)) <= 1e-12 * np.max(np.abs(Xr)), n
+    y = _fft64(m, n, True, np.stack([Xr.real, Xr.imag], 1).ravel())
+    assert np.max(np.abs(y - x)) <= 1e-13 * np.max(np.abs(x)) * np.log2(n), n
+
+
+def test_long_grains_global_chain(m, O, irs):
+    """Grains beyond the LDS-resident engines (UI: micro_ms up to 80, unfold up to
+    200): a float32-chain preset at n = 48000 and 36001 (odd), float64-chain
+    presets at n = 12000 (cepstral + imprint + lock), 10007 (prime) and a
+    feedback chain, all against the oracle."""
+    params = [
+        base(m, gen_mode="Resonant strike", micro_ms=40.0, time_unfold=25.0, seed=401),           # n 48000
+        base(m, gen_mode="Noise burst", micro_ms=30.00083333, time_unfold=25.0, seed=402),         # n 36001
+        base(m, gen_mode="Wavelet atoms", time_unfold=200.0, partial_lock_on=True, partial_stretch=1.3,
+             spectral_imprint_on=True, seed=403),                                                   # n 12000
+        base(m, gen_mode="Crackle / corona", time_unfold=166.78333, unfold_mode="Multi-band", seed=404),  # n 10007
+        base(m, gen_mode="Dust impulses", time_unfold=200.0, event_feedback_on=True, res_bank_on=True, wg_on=True,
+             seed=405),
+    ]
+    check(m, O, params)
