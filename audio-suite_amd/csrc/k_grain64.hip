@@ -42,3 +42,19 @@ hipError_t launch_fft64_one(int lds_bytes, hipStream_t s, const Real64Plan* plan
     hipLaunchKernelGGL(k_fft64_one, dim3(1), dim3(G64_T), gA ? 0 : lds_bytes, s, plans, plan, inverse, io, gA, gB);
     return hipGetLastError();
 }
+
+hipError_t launch_stft64(unsigned frames, int lds_bytes, hipStream_t s, const Real64Plan* plans, int plan,
+                         const void* x, int elem_bytes, int64_t n, int channels, int win, int hop, double* S) {
+    if (elem_bytes == 8) {
+        (void)hipFuncSetAttribute((const void*)k_stft64<double>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  G64_CAP * 16);
+        hipLaunchKernelGGL(k_stft64<double>, dim3(frames), dim3(G64_T), lds_bytes, s, plans, plan,
+                           (const double*)x, n, channels, win, hop, S);
+    } else {
+        (void)hipFuncSetAttribute((const void*)k_stft64<float>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  G64_CAP * 16);
+        hipLaunchKernelGGL(k_stft64<float>, dim3(frames), dim3(G64_T), lds_bytes, s, plans, plan,
+                           (const float*)x, n, channels, win, hop, S);
+    }
+    return hipGetLastError();
+}

@@ -822,3 +822,38 @@ k_fft64_one(const Real64Plan* __restrict__ plans, int plan, int inverse, double*
     for (int j = threadIdx.x; j < cnt2; j += G64_T) io[j] = d[j];
 }
 #endif
+
+#if defined(__HIPCC__)
+// ---------------------------------------------------------------------------
+// k_stft64: the app's spectrogram, stft_mag_db (MS:197-212), one workgroup per
+// frame: (mono or the L/R mean of an interleaved buffer) x hann(win) -> rfft
+// (float64 engine in LDS) -> 20 log10(max(|X|, 1e-12)).  A signal shorter
+// than win is one frame of x * hann(n), zero-padded to win (MS:199-202).
+// x is float32 (render output) or float64; S is frames x (win/2 + 1), row-major.
+// ---------------------------------------------------------------------------
+template <typename TX>
+__global__ void __launch_bounds__(G64_T)
+k_stft64(const Real64Plan* __restrict__ plans, int plan, const TX* __restrict__ x, int64_t n, int channels,
+         int win, int hop, double* __restrict__ S) {
+    extern __shared__ __attribute__((aligned(16))) double2 buf[];
+    const Real64Plan& rp = plans[plan];
+    double* d = reinterpret_cast<double*>(buf);
+    const int f = blockIdx.x;
+    const int64_t a = (int64_t)f * hop;
+    const int nseg = n < win ? (int)n : win;
+    for (int j = threadIdx.x; j < win; j += G64_T) {
+        double v = 0.0;
+        if (j < nseg) {
+            const int64_t i = a + j;
+            const double s = channels == 2 ? ((double)x[2 * i] + (double)x[2 * i + 1]) / 2.0 : (double)x[i];
+            v = s * hann64(j, nseg);
+        }
+        d[j] = v;
+    }
+    __syncthreads();
+    f64_rfft<G64_T, G64_MAXE>(buf, rp);
+    const int K = win / 2 + 1;
+    for (int k = threadIdx.x; k < K; k += G64_T)
+        S[(int64_t)f * K + k] = 20.0 * log10(fmax(hypot(buf[k].x, buf[k].y), 1e-12));
+}
+#endif

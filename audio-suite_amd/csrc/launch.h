@@ -71,3 +71,6 @@ int64_t stereo_odd_len(int64_t n);                  // M, or -1 when n is too lo
 hipError_t launch_stereo_odd_kernel(int64_t n, float2* Bp, float2* A, hipStream_t s);
 hipError_t launch_stereo_odd(int64_t n, int dr, double width, const float* y, const float2* Bp, float2* A,
                              float* r2, hipStream_t s);
+// the app's spectrogram (stft_mag_db, MS:197-212) on the float64 engine
+hipError_t launch_stft64(unsigned frames, int lds_bytes, hipStream_t s, const Real64Plan* plans, int plan,
+                         const void* x, int elem_bytes, int64_t n, int channels, int win, int hop, double* S);

@@ -678,6 +678,28 @@ int msg_fft64(msg_ctx* ctx, int32_t n, int32_t inverse, const double* in, double
     return MSG_OK;
 }
 
+int msg_stft_mag_db(msg_ctx* ctx, const void* x_dev, int32_t elem_bytes, int64_t n, int32_t channels, int32_t win,
+                    int32_t hop, int32_t max_frames, double* S_dev, int32_t* frames, void* stream) {
+    if (!ctx || !frames || n < 1 || win < 2 || hop < 1 || (channels != 1 && channels != 2) ||
+        (elem_bytes != 4 && elem_bytes != 8))
+        return fail(ctx, MSG_E_ARG, "bad arguments");
+    const int64_t fr = n < win ? 1 : std::min<int64_t>(1 + (n - win) / hop, std::max(max_frames, 0));
+    *frames = (int32_t)fr;
+    if (!S_dev || fr <= 0) return MSG_OK;                 // size query
+    if (!x_dev) return fail(ctx, MSG_E_ARG, "null input");
+    HIPCHK(ctx, hipSetDevice(ctx->device));
+    std::string why;
+    const int pi = real64_plan(ctx->plans64, win, why);
+    if (pi < 0) return fail(ctx, MSG_E_DEVICE, why);
+    const int cap = ctx->plans64.host[pi].cap;
+    if (cap > G64_SLOTS) return fail(ctx, MSG_E_UNSUPPORTED, "STFT window beyond the LDS float64 engine");
+    hipStream_t s = (hipStream_t)stream;
+    HIPCHK(ctx, sync_plans(ctx->plans64, s));
+    HIPCHK(ctx, launch_stft64((unsigned)fr, cap * 16, s, ctx->plans64.dev.p, pi, x_dev, elem_bytes, n, channels, win,
+                                     hop, S_dev));
+    return MSG_OK;
+}
+
 int msg_last_plan(msg_ctx* ctx, msg_plan_info* info, int32_t n_presets) {
     if (!ctx || !info) return MSG_E_ARG;
     if (n_presets > ctx->last_n) return fail(ctx, MSG_E_ARG, "n_presets exceeds last batch");

@@ -19,3 +19,15 @@ def render(params, progress=None, device: int = 0):
 def render_batch(params_list, device: int = 0):
     from .dropin import render_batch as _rb
     return _rb(params_list, device)
+
+
+def stft_mag_db(x, sr=None, win=2048, hop=256, max_frames=3000, device: int = 0):
+    """The app's spectrogram (MS:197-212) on the device; see spectrum.py."""
+    from .spectrum import stft_mag_db as _s
+    return _s(x, sr, win, hop, max_frames, device)
+
+
+def render_variations(base_params, seeds, unfolds, stretches, folder=None, device: int = 0, **kw):
+    """The app's batch render (on_batch, MS:1524-1596); see batch.py."""
+    from .batch import render_variations as _rv
+    return _rv(base_params, seeds, unfolds, stretches, folder, device, **kw)

@@ -80,6 +80,32 @@ class Engine:
         packed = PackedBatch(params_list)
         return self.render_packed(packed, out), packed
 
+    def stft_mag_db(self, x, win=2048, hop=256, max_frames=3000, stream=None):
+        """Spectrogram of a device float32/float64 tensor (n,) mono or (n, 2) stereo (L/R
+        mean): returns a device float64 tensor (frames, win//2 + 1), enqueued on ``stream``."""
+        torch = self.torch
+        if x.dtype not in (torch.float32, torch.float64) or not x.is_contiguous() or x.device.type != "cuda":
+            raise ValueError("x must be a contiguous float32 or float64 device tensor")
+        eb = x.element_size()
+        channels = 1 if x.dim() == 1 else int(x.shape[1])
+        if x.dim() > 2 or channels not in (1, 2):
+            raise ValueError("x must be (n,) or (n, 2)")
+        n = int(x.shape[0])
+        frames = C.c_int32(0)
+        lib = L.lib()
+        L.check(lib.msg_stft_mag_db(self._ctx, None, eb, n, channels, int(win), int(hop), int(max_frames),
+                                    None, C.byref(frames), None), self._ctx)
+        S = torch.empty((frames.value, int(win) // 2 + 1), dtype=torch.float64, device=x.device)
+        if frames.value == 0:
+            return S
+        if stream is None:
+            stream = torch.cuda.current_stream(x.device)
+        with self._lock:
+            L.check(lib.msg_stft_mag_db(self._ctx, C.c_void_p(x.data_ptr()), eb, n, channels, int(win), int(hop),
+                                        int(max_frames), C.c_void_p(S.data_ptr()), C.byref(frames),
+                                        C.c_void_p(stream.cuda_stream)), self._ctx)
+        return S
+
     # ---- last-batch inspection -----------------------------------------
     def last_plan(self):
         arr = (L.MsgPlanInfo * self._last_n)()

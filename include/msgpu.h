@@ -164,6 +164,15 @@ int msg_bench_fft(msg_ctx* ctx, int32_t n, int32_t reps, int32_t blocks, float* 
  * to n/2+1 interleaved complex bins; inverse = 1 maps them back.  For tests. */
 int msg_fft64(msg_ctx* ctx, int32_t n, int32_t inverse, const double* in, double* out);
 
+/* The app's spectrogram stft_mag_db (MS:197-212) of a device buffer: x_dev is
+ * n mono samples (channels = 1) or n interleaved L/R frames (channels = 2, the
+ * L/R mean is analysed, as MS:1500 does), float32 (elem_bytes = 4, the render
+ * output) or float64 (elem_bytes = 8).  S_dev receives frames x (win/2+1)
+ * doubles, row-major (S_dev = NULL: only *frames is set).  Enqueued on stream.
+ * Windows up to 16384 samples (the float64 LDS engine). */
+int msg_stft_mag_db(msg_ctx* ctx, const void* x_dev, int32_t elem_bytes, int64_t n, int32_t channels, int32_t win,
+                    int32_t hop, int32_t max_frames, double* S_dev, int32_t* frames, void* stream);
+
 /* ---- NumPy stream primitives on the host (tests pin them against NumPy) ---- */
 /* Raw PCG64 outputs of np.random.default_rng(seed).bit_generator.random_raw(n). */
 int msg_rng_raw(uint64_t seed, uint64_t* out, int64_t n);

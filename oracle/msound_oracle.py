@@ -800,3 +800,26 @@ def render(p: dict, progress=None):
     meta = {"out_sr": plan.base_sr, "design_sr_base": plan.gen_sr,
             "micro_last": micro_last, "grain_last": grain_last}
     return st.astype(np.float64), meta
+
+
+# ---------------------------------------------------------------------------
+# UI analysis helpers (MS:23-24, 197-212): the spectrogram the app draws
+# ---------------------------------------------------------------------------
+def db(x, eps=1e-12):
+    """20 log10(max(|x|, eps)) (MS:23-24)."""
+    return 20 * np.log10(np.maximum(np.abs(x), eps))
+
+
+def stft_mag_db(x, sr, win=2048, hop=256, max_frames=3000):
+    """Hann-windowed STFT magnitude in dB, (win//2+1, frames) (MS:197-212)."""
+    n = len(x)
+    if n < win:
+        X = np.fft.rfft(x * hann(n), n=win)
+        return db(X)[:, None]
+    frames = min(1 + (n - win) // hop, max_frames)
+    w = hann(win)
+    S = np.empty((win // 2 + 1, frames), dtype=np.float64)
+    for i in range(frames):
+        a = i * hop
+        S[:, i] = db(np.fft.rfft(x[a:a + win] * w))
+    return S

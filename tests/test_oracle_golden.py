@@ -158,3 +158,14 @@ def test_c4_c5_decimated(irs, large_renders, golden_info):
         close(a[-8192:].astype(np.float32), large_renders[f"{name}_tail"], 2e-7)
         s = golden_info["summaries"][f"{name}_1000"]
         assert abs(float(np.sqrt(np.mean(a ** 2))) - s["rms"]) < 1e-12
+
+
+def test_stft_mag_db_pinned():
+    """The oracle's spectrogram helper against the reference's (MS:197-212)."""
+    import os
+    z = np.load(os.path.join(os.path.dirname(__file__), "golden", "stft.npz"))
+    for name in ("c2", "defaults", "capped", "short", "odd"):
+        sr, win, hop, mf = (int(v) for v in z[f"{name}_cfg"])
+        S = O.stft_mag_db(z[f"{name}_x"], sr, win=win, hop=hop, max_frames=mf)
+        assert S.shape == z[f"{name}_S"].shape
+        assert np.max(np.abs(S.astype(np.float32) - z[f"{name}_S"])) <= 1e-3, name
