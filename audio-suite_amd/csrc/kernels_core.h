@@ -335,12 +335,16 @@ k_ola_env(const msg_event* __restrict__ events, const PresetRt* __restrict__ rt,
 // Stereo (even n: exact 25-tap Bessel FIR form of the spectral rotation),
 // tanh saturation and peak normalisation.
 // ---------------------------------------------------------------------------
-// A block handles ST_TILE frames [t0, t0+ST_TILE) of one preset.  The
-// right-channel window y[(t0 + dr - 24 + u) mod n], u < ST_TILE + 48, is staged
-// in LDS (all loads of a thread in flight at once), so each output is 25 LDS
-// reads + FMAs.  L[t] = y[(t - dl) mod n] is a shifted coalesced read.
-constexpr int ST_PER = ST_TILE / ST_T;
-constexpr int ST_WPER = (ST_TILE + 48 + ST_T - 1) / ST_T;
+// A block handles ST_TILE frames [t0, t0+ST_TILE) of one preset; each thread
+// owns runs of 4 consecutive frames.  The right-channel window
+// y[(t0 + dr - 24 + u) mod n], u < ST_TILE + 48, is staged in LDS with
+// coalesced loads; a run's 25-tap outputs then need 13 ds_read_b128 of the
+// window instead of 100 scalar reads (the kernels were LDS-issue bound).
+// L[t] = y[(t - dl) mod n] is staged the same way in k_stereo_out.
+constexpr int ST_RUNS = ST_TILE / (4 * ST_T);     // runs of 4 frames per thread
+constexpr int ST_WIN = ST_TILE + 48;
+constexpr int ST_WPER = (ST_WIN + ST_T - 1) / ST_T;
+constexpr int ST_LPER = ST_TILE / ST_T;
 
 struct StereoTile {
     int t0, cnt;             // first frame, frames in this tile
@@ -352,65 +356,98 @@ MSG_DEV int mod_n(int64_t i, int64_t n) {
     return (int)(i < 0 ? i + n : i);
 }
 
-// Stage the R window into w[0 .. ST_TILE+48); returns the tile bounds.
-MSG_DEV StereoTile stereo_stage(const PresetRt& r, const float* __restrict__ y, int64_t t0, float* w) {
+// Stage len floats y[(b0 + u) mod n] into w[0 .. len) (coalesced, all loads in flight).
+template <int PER>
+MSG_DEV void stereo_window(const float* __restrict__ y, int n, int b0, int len, float* w) {
+    float v[PER];
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+        const int u = threadIdx.x + i * ST_T;
+        int j = b0 + u;
+        if (n >= len) { if (j >= n) j -= n; }   // one wrap at most
+        else j %= n;
+        v[i] = u < len ? y[j] : 0.f;
+    }
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+        const int u = threadIdx.x + i * ST_T;
+        if (u < len) w[u] = v[i];
+    }
+}
+
+MSG_DEV StereoTile stereo_tile(const PresetRt& r, int64_t t0) {
     const int n = (int)r.out_n;
     StereoTile st;
     st.t0 = (int)t0;
     st.cnt = (int)(t0 + ST_TILE < n ? ST_TILE : n - t0);
     st.lbase = mod_n(t0 - r.dl, n);
-    if (r.stereo_fir == 1) {
-        const int b0 = mod_n(t0 + r.dr - 24, n);
-        float v[ST_WPER];
-#pragma unroll
-        for (int i = 0; i < ST_WPER; ++i) {
-            const int u = threadIdx.x + i * ST_T;
-            int j = b0 + u;
-            if (n >= ST_TILE + 48) { if (j >= n) j -= n; }   // one wrap at most
-            else j %= n;
-            v[i] = u < ST_TILE + 48 ? y[j] : 0.f;
-        }
-#pragma unroll
-        for (int i = 0; i < ST_WPER; ++i) {
-            const int u = threadIdx.x + i * ST_T;
-            if (u < ST_TILE + 48) w[u] = v[i];
-        }
-    }
-    __syncthreads();
     return st;
 }
 
-MSG_DEV float stereo_r(const PresetRt& r, const float* w, int u) {
-    float acc = 0.f;
+// R[u + k] = sum_m J_m w[u + k + 2m], k < 4, u a multiple of 4 (same fma order as the
+// reference-checked scalar form: m = 0 .. 24).
+MSG_DEV void stereo_r4(const PresetRt& r, const float* w, int u, float (&R)[4]) {
+    float x[52];
+    const float4* w4 = reinterpret_cast<const float4*>(w + u);
 #pragma unroll
-    for (int m = 0; m < 25; ++m) acc = fmaf(r.bess[m], w[u + 2 * m], acc);
-    return acc;
+    for (int i = 0; i < 13; ++i) {
+        const float4 q = w4[i];
+        x[4 * i] = q.x; x[4 * i + 1] = q.y; x[4 * i + 2] = q.z; x[4 * i + 3] = q.w;
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        float acc = 0.f;
+#pragma unroll
+        for (int m = 0; m < 25; ++m) acc = fmaf(r.bess[m], x[k + 2 * m], acc);
+        R[k] = acc;
+    }
 }
 
 __global__ void __launch_bounds__(ST_T)
 k_stereo_max(const PresetRt* __restrict__ rt, const int32_t* __restrict__ st_begin, int n_presets,
              const float* __restrict__ ybuf, const float* __restrict__ rbuf, unsigned* __restrict__ maxbits) {
-    __shared__ float w[ST_TILE + 48];
+    __shared__ __attribute__((aligned(16))) float w[ST_WIN];
     __shared__ float wm[ST_T / 64];
     const int b = blockIdx.x;
     const int p = find_preset(st_begin, n_presets, b);
     const PresetRt& r = rt[p];
     const float* y = ybuf + r.y_off;
-    const StereoTile st = stereo_stage(r, y, (int64_t)(b - st_begin[p]) * ST_TILE, w);
-    float m = 0.f;
+    const int n = (int)r.out_n;
+    const StereoTile st = stereo_tile(r, (int64_t)(b - st_begin[p]) * ST_TILE);
+    if (r.stereo_fir == 1) stereo_window<ST_WPER>(y, n, mod_n((int64_t)st.t0 + r.dr - 24, n), ST_WIN, w);
     // max|L| over all frames equals max|y| (L is a rotation of y): read y directly
-    float yv[ST_PER];
+    // (y regions are 16-byte aligned and t0 is a multiple of ST_TILE)
+    float4 yv[ST_RUNS];
 #pragma unroll
-    for (int i = 0; i < ST_PER; ++i) {
-        const int u = threadIdx.x + i * ST_T;
-        yv[i] = u < st.cnt ? y[st.t0 + u] : 0.f;
+    for (int i = 0; i < ST_RUNS; ++i) {
+        const int u = 4 * (threadIdx.x + i * ST_T);
+        if (u + 4 <= st.cnt) {
+            yv[i] = *reinterpret_cast<const float4*>(y + st.t0 + u);
+        } else {
+            yv[i].x = u < st.cnt ? y[st.t0 + u] : 0.f;
+            yv[i].y = u + 1 < st.cnt ? y[st.t0 + u + 1] : 0.f;
+            yv[i].z = u + 2 < st.cnt ? y[st.t0 + u + 2] : 0.f;
+            yv[i].w = 0.f;
+        }
     }
+    __syncthreads();
+    float m = 0.f;
 #pragma unroll
-    for (int i = 0; i < ST_PER; ++i) {
-        const int u = threadIdx.x + i * ST_T;
-        m = fmaxf(m, fabsf(yv[i]));
-        if (r.stereo_fir == 1 && u < st.cnt) m = fmaxf(m, fabsf(stereo_r(r, w, u)));
-        if (r.stereo_fir == 2 && u < st.cnt) m = fmaxf(m, fabsf(rbuf[r.r2_off + st.t0 + u]));
+    for (int i = 0; i < ST_RUNS; ++i) {
+        const int u = 4 * (threadIdx.x + i * ST_T);
+        m = fmaxf(m, fmaxf(fmaxf(fabsf(yv[i].x), fabsf(yv[i].y)), fmaxf(fabsf(yv[i].z), fabsf(yv[i].w))));
+        if (r.stereo_fir == 1 && u < st.cnt) {
+            float R[4];
+            stereo_r4(r, w, u, R);
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                if (u + k < st.cnt) m = fmaxf(m, fabsf(R[k]));
+        }
+        if (r.stereo_fir == 2) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                if (u + k < st.cnt) m = fmaxf(m, fabsf(rbuf[r.r2_off + st.t0 + u + k]));
+        }
     }
     for (int off = 32; off > 0; off >>= 1) m = fmaxf(m, __shfl_xor(m, off));
     if ((threadIdx.x & 63) == 0) wm[threadIdx.x >> 6] = m;
@@ -428,34 +465,49 @@ __global__ void __launch_bounds__(ST_T)
 k_stereo_out(const PresetRt* __restrict__ rt, const int32_t* __restrict__ st_begin, int n_presets,
              const float* __restrict__ ybuf, const float* __restrict__ rbuf, const unsigned* __restrict__ maxbits,
              float* __restrict__ out) {
-    __shared__ float w[ST_TILE + 48];
+    __shared__ __attribute__((aligned(16))) float w[ST_WIN];
+    __shared__ __attribute__((aligned(16))) float lw[ST_TILE];
     const int b = blockIdx.x;
     const int p = find_preset(st_begin, n_presets, b);
     const PresetRt& r = rt[p];
     const float* y = ybuf + r.y_off;
-    const StereoTile st = stereo_stage(r, y, (int64_t)(b - st_begin[p]) * ST_TILE, w);
+    const int n = (int)r.out_n;
+    const StereoTile st = stereo_tile(r, (int64_t)(b - st_begin[p]) * ST_TILE);
+    if (r.stereo_fir == 1) stereo_window<ST_WPER>(y, n, mod_n((int64_t)st.t0 + r.dr - 24, n), ST_WIN, w);
+    stereo_window<ST_LPER>(y, n, r.stereo_fir ? st.lbase : st.t0, st.cnt, lw);
     const float d = r.drive;
     const float inv_td = d > 0.f ? 1.0f / tanhf(d) : 1.f;
     const float M = __uint_as_float(maxbits[p]);
     const float mc = sat(M, d, inv_td);
     const float scale = mc > 0.f ? r.peak / mc : 1.f;
-    const int n = (int)r.out_n;
     float2* o = reinterpret_cast<float2*>(out) + r.out_off + st.t0;
-    float lv[ST_PER];
+    const bool o16 = ((r.out_off + st.t0) & 1) == 0;      // float4 stores of two frames
+    __syncthreads();
 #pragma unroll
-    for (int i = 0; i < ST_PER; ++i) {
-        const int u = threadIdx.x + i * ST_T;
-        int il = r.stereo_fir ? st.lbase + u : st.t0 + u;
-        if (il >= n) il -= n;
-        lv[i] = u < st.cnt ? y[il] : 0.f;
-    }
-#pragma unroll
-    for (int i = 0; i < ST_PER; ++i) {
-        const int u = threadIdx.x + i * ST_T;
+    for (int i = 0; i < ST_RUNS; ++i) {
+        const int u = 4 * (threadIdx.x + i * ST_T);
         if (u >= st.cnt) continue;
-        const float L = lv[i];
-        const float R = r.stereo_fir == 1 ? stereo_r(r, w, u)
-                        : (r.stereo_fir == 2 ? rbuf[r.r2_off + st.t0 + u] : L);
-        o[u] = make_float2(sat(L, d, inv_td) * scale, sat(R, d, inv_td) * scale);
+        const float4 l4 = *reinterpret_cast<const float4*>(lw + u);
+        const float L[4] = {l4.x, l4.y, l4.z, l4.w};
+        float R[4];
+        if (r.stereo_fir == 1) {
+            stereo_r4(r, w, u, R);
+        } else {
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                R[k] = r.stereo_fir == 2 ? (u + k < st.cnt ? rbuf[r.r2_off + st.t0 + u + k] : 0.f) : L[k];
+        }
+        float2 v[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v[k] = make_float2(sat(L[k], d, inv_td) * scale, sat(R[k], d, inv_td) * scale);
+        if (o16 && u + 4 <= st.cnt) {
+            float4* o4 = reinterpret_cast<float4*>(o + u);
+            o4[0] = make_float4(v[0].x, v[0].y, v[1].x, v[1].y);
+            o4[1] = make_float4(v[2].x, v[2].y, v[3].x, v[3].y);
+        } else {
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                if (u + k < st.cnt) o[u + k] = v[k];
+        }
     }
 }

@@ -109,6 +109,12 @@ struct msg_ctx {
     DevBuf<uint8_t> imgbank;
     DevBuf<double2> g64A, g64B;                 // global-class float64 grains (G64Global)
     DevBuf<uint32_t> g64mask;
+    // standalone FIR (msg_fir): its own buffers, so it never touches a render batch's
+    DevBuf<PresetRt> sf_prt;
+    DevBuf<int2> sf_jobs;
+    DevBuf<int64_t> sf_irjobs;
+    DevBuf<double> sf_h;
+    DevBuf<float2> sf_hspec;
     // odd-length stereo rotation (kernels_stereo_odd.h)
     std::map<int64_t, DevBuf<float2>> so_bp;   // chirp kernel spectra by n
     DevBuf<float2> so_A;
@@ -460,6 +466,8 @@ void msg_destroy(msg_ctx* ctx) {
     for (float2* t : ctx->d_spec_ct_tab) hipFree(t);
     ctx->spec_ct_list.release();
     ctx->fir_jobs.release();
+    ctx->sf_prt.release(); ctx->sf_jobs.release(); ctx->sf_irjobs.release(); ctx->sf_h.release();
+    ctx->sf_hspec.release();
     for (auto& ev : ctx->ev) hipEventDestroy(ev);
     ctx->presets.release(); ctx->frag_len.release(); ctx->info.release(); ctx->slot_base.release();
     ctx->tap_base.release(); ctx->events.release(); ctx->er_off.release(); ctx->er_gain.release();
@@ -697,6 +705,63 @@ int msg_stft_mag_db(msg_ctx* ctx, const void* x_dev, int32_t elem_bytes, int64_t
     HIPCHK(ctx, sync_plans(ctx->plans64, s));
     HIPCHK(ctx, launch_stft64((unsigned)fr, cap * 16, s, ctx->plans64.dev.p, pi, x_dev, elem_bytes, n, channels, win,
                                      hop, S_dev));
+    return MSG_OK;
+}
+
+int msg_fir(msg_ctx* ctx, const float* x_dev, float* y_dev, int64_t n, int32_t n_signals, const double* h,
+            int64_t M, int32_t* fir_shape, void* stream) {
+    if (!ctx || !x_dev || !y_dev || !h || n < 1 || n_signals < 1 || M < 1)
+        return fail(ctx, MSG_E_ARG, "bad arguments");
+    if ((const void*)x_dev == (const void*)y_dev) return fail(ctx, MSG_E_ARG, "x and y must not alias");
+    if (M > (int64_t)64 * (FIR_NMAX - 1)) return fail(ctx, MSG_E_UNSUPPORTED, "FIR longer than 64 partitions");
+    HIPCHK(ctx, hipSetDevice(ctx->device));
+    hipStream_t s = (hipStream_t)stream;
+    int N = 0, Pp = 0, Q = 0;
+    choose_fir(M, n, 0, N, Pp, Q);
+    const int64_t B = N - Pp + 1;
+    const int64_t blocks = (n + B - 1) / B;
+    if (blocks * n_signals > INT32_MAX) return fail(ctx, MSG_E_UNSUPPORTED, "too many output blocks");
+    if (fir_shape) { fir_shape[0] = N; fir_shape[1] = Pp; fir_shape[2] = Q; }
+    std::string why;
+    const int fp = real_plan(ctx->fir_plans, N, why);
+    if (fp < 0) return fail(ctx, MSG_E_DEVICE, "FIR plan: " + why);
+    HIPCHK(ctx, sync_plans(ctx->fir_plans, s));
+    const int K = N / 2 + 1;
+    // partition spectra H_q = FFT_N(h[qP, qP + P)) by the IR-spectrum kernel
+    std::vector<int64_t> jobs;
+    for (int q = 0; q < Q; ++q)
+        jobs.insert(jobs.end(), {(int64_t)q * Pp, std::min<int64_t>(Pp, M - (int64_t)q * Pp), (int64_t)fp,
+                                 (int64_t)q * K});
+    std::vector<PresetRt> prt((size_t)n_signals);
+    std::vector<int2> fj;
+    fj.reserve((size_t)(blocks * n_signals));
+    for (int i = 0; i < n_signals; ++i) {
+        PresetRt& r = prt[i];
+        memset(&r, 0, sizeof(r));
+        r.out_n = n;
+        r.y_off = (int64_t)i * n;
+        r.fir_on = 1; r.fir_N = N; r.fir_P = Pp; r.fir_Q = Q; r.fir_B = (int32_t)B;
+        r.h_off = 0;
+        for (int64_t b = 0; b < blocks; ++b) fj.push_back(make_int2(i, (int)b));
+    }
+    HIPCHK(ctx, ctx->sf_prt.ensure(prt.size()));
+    HIPCHK(ctx, ctx->sf_jobs.ensure(fj.size()));
+    HIPCHK(ctx, ctx->sf_irjobs.ensure(jobs.size()));
+    HIPCHK(ctx, ctx->sf_h.ensure((size_t)M));
+    HIPCHK(ctx, ctx->sf_hspec.ensure((size_t)Q * K));
+    HIPCHK(ctx, hipMemcpyAsync(ctx->sf_prt.p, prt.data(), sizeof(PresetRt) * prt.size(), hipMemcpyHostToDevice, s));
+    HIPCHK(ctx, hipMemcpyAsync(ctx->sf_jobs.p, fj.data(), sizeof(int2) * fj.size(), hipMemcpyHostToDevice, s));
+    HIPCHK(ctx, hipMemcpyAsync(ctx->sf_irjobs.p, jobs.data(), sizeof(int64_t) * jobs.size(), hipMemcpyHostToDevice,
+                               s));
+    HIPCHK(ctx, hipMemcpyAsync(ctx->sf_h.p, h, sizeof(double) * (size_t)M, hipMemcpyHostToDevice, s));
+    HIPCHK(ctx, launch_ir_spec((unsigned)Q, ctx->fir_plans.host[fp].lds_bytes, s, ctx->sf_irjobs.p, Q,
+                               ctx->fir_plans.dev.p, ctx->sf_h.p, ctx->sf_hspec.p));
+    int ti = 0;
+    while ((1024 << ti) != N / 2) ++ti;
+    HIPCHK(ctx, launch_fir2(N / 2, (unsigned)fj.size(), s, ctx->sf_prt.p, ctx->sf_jobs.p, ctx->d_fir2tab[ti],
+                            ctx->sf_hspec.p, x_dev, y_dev));
+    // pageable-host H2D copies are staged before hipMemcpyAsync returns (as in
+    // msg_render_batch), so the host vectors may go; the FIR runs asynchronously.
     return MSG_OK;
 }
 

@@ -27,6 +27,20 @@ def stft_mag_db(x, sr=None, win=2048, hop=256, max_frames=3000, device: int = 0)
     return _s(x, sr, win, hop, max_frames, device)
 
 
+def fir(x, h, device: int = 0):
+    """Standalone causal FIR np.convolve(x, h)[:len(x)] on the device (MS:444 arithmetic, any tap count)."""
+    from .engine import default_engine
+    import numpy as np
+    eng = default_engine(device)
+    torch = eng.torch
+    if isinstance(x, torch.Tensor):
+        return eng.fir(x.contiguous(), h)[0]
+    a = np.ascontiguousarray(x, dtype=np.float32)
+    y, _ = eng.fir(torch.from_numpy(a).to(f"cuda:{eng.device}"), h)
+    torch.cuda.synchronize(eng.device)
+    return y.cpu().numpy()
+
+
 def render_variations(base_params, seeds, unfolds, stretches, folder=None, device: int = 0, **kw):
     """The app's batch render (on_batch, MS:1524-1596); see batch.py."""
     from .batch import render_variations as _rv

@@ -103,6 +103,8 @@ _PROTOS = {
     "msg_stage_times": (C.c_int, [C.c_void_p, C.POINTER(C.c_float), C.c_int32]),
     "msg_bench_fft": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32, C.c_int32, C.POINTER(C.c_float)]),
     "msg_fft64": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32, C.POINTER(C.c_double), C.POINTER(C.c_double)]),
+    "msg_fir": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64, C.c_int32, C.c_void_p, C.c_int64,
+                          C.POINTER(C.c_int32), C.c_void_p]),
     "msg_stft_mag_db": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.c_int64, C.c_int32, C.c_int32, C.c_int32, C.c_int32,
                                   C.c_void_p, C.POINTER(C.c_int32), C.c_void_p]),
     "msg_rng_raw": (C.c_int, [C.c_uint64, C.POINTER(C.c_uint64), C.c_int64]),

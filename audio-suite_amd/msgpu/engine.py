@@ -106,6 +106,29 @@ class Engine:
                                         C.c_void_p(stream.cuda_stream)), self._ctx)
         return S
 
+    def fir(self, x, h, out=None, stream=None):
+        """Causal FIR y = np.convolve(x, h)[:n] of each row of a device float32 tensor
+        (S, n) or (n,), h float64 taps (host); returns (y, (N, P, Q)) enqueued on ``stream``."""
+        torch = self.torch
+        if x.dtype != torch.float32 or not x.is_contiguous() or x.device.type != "cuda" or x.dim() > 2:
+            raise ValueError("x must be a contiguous float32 device tensor (n,) or (S, n)")
+        S, n = (1, int(x.shape[0])) if x.dim() == 1 else (int(x.shape[0]), int(x.shape[1]))
+        hh = np.ascontiguousarray(h, dtype=np.float64)
+        if hh.ndim != 1 or hh.size < 1:
+            raise ValueError("h must be a non-empty 1-D array")
+        if out is None:
+            out = torch.empty_like(x)
+        if out.shape != x.shape or out.dtype != torch.float32 or not out.is_contiguous():
+            raise ValueError("out must match x")
+        if stream is None:
+            stream = torch.cuda.current_stream(x.device)
+        shape = (C.c_int32 * 3)()
+        with self._lock:
+            L.check(L.lib().msg_fir(self._ctx, C.c_void_p(x.data_ptr()), C.c_void_p(out.data_ptr()), n, S,
+                                    hh.ctypes.data_as(C.c_void_p), int(hh.size), shape,
+                                    C.c_void_p(stream.cuda_stream)), self._ctx)
+        return out, tuple(shape)
+
     # ---- last-batch inspection -----------------------------------------
     def last_plan(self):
         arr = (L.MsgPlanInfo * self._last_n)()

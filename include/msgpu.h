@@ -164,6 +164,16 @@ int msg_bench_fft(msg_ctx* ctx, int32_t n, int32_t reps, int32_t blocks, float* 
  * to n/2+1 interleaved complex bins; inverse = 1 maps them back.  For tests. */
 int msg_fft64(msg_ctx* ctx, int32_t n, int32_t inverse, const double* in, double* out);
 
+/* Standalone causal FIR, y = np.convolve(x, h)[:n] per signal (the arithmetic of
+ * convolve_ir_short, MS:438-445, without its 8192-tap cap; SURVEY §8 "16 k / 64 k
+ * taps"), on the render path's partitioned FFT overlap-save kernels (float32).
+ * x_dev / y_dev: n_signals contiguous signals of n floats (device, not aliased);
+ * h: M float64 taps in host memory, shared by every signal.  fir_shape (or NULL)
+ * receives the transform N, partition P and partition count Q chosen.
+ * Enqueued on stream; one call in flight per context. */
+int msg_fir(msg_ctx* ctx, const float* x_dev, float* y_dev, int64_t n, int32_t n_signals, const double* h,
+            int64_t M, int32_t* fir_shape, void* stream);
+
 /* The app's spectrogram stft_mag_db (MS:197-212) of a device buffer: x_dev is
  * n mono samples (channels = 1) or n interleaved L/R frames (channels = 2, the
  * L/R mean is analysed, as MS:1500 does), float32 (elem_bytes = 4, the render

@@ -487,6 +487,19 @@ def convolve_ir_short(x, ir):
     return np.convolve(x, h, mode="full")[:len(x)].astype(np.float64)
 
 
+def fir_causal(x, h):
+    """The arithmetic of MS:444 without the 8192-tap cap of MS:443: the standalone
+    FIR of SURVEY §8 (16 k / 64 k taps), np.convolve(x, h)[:len(x)] in float64."""
+    x = np.asarray(x, dtype=np.float64)
+    return np.convolve(x, np.asarray(h, dtype=np.float64), mode="full")[:len(x)]
+
+
+def synthetic_fir_taps(M, seed=7):
+    """SURVEY §8(d)'s standalone-FIR taps: default_rng(7).standard_normal(M) exp(-6t/M), peak 0.9."""
+    h = np.random.default_rng(seed).standard_normal(M) * np.exp(-6.0 * np.arange(M) / M)
+    return peak_normalize(h, 0.9)
+
+
 # ---------------------------------------------------------------------------
 # Breakpoint lanes (MS:452-482), unfold (MS:489-500), event fields (MS:507-558)
 # ---------------------------------------------------------------------------

@@ -1,0 +1,70 @@
+"""Standalone FIR (msg_fir): y = np.convolve(x, h)[:n] at 16 k / 64 k taps (SURVEY §8 config
+remarks and §8(d)), on the render path's partitioned FFT kernels (k_ir_spec, k_fir2).
+
+The oracle is oracle.fir_causal (np.convolve, MS:444 without the 8192 cap).  At
+these sizes np.convolve takes minutes, so the float64 reference is
+scipy.signal.fftconvolve, itself checked against fir_causal on a short case here.
+The bar is float32 FFT convolution accuracy relative to the output RMS: 1e-5.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+REL = 1e-5
+
+
+def _ref(x, h):
+    from scipy.signal import fftconvolve
+    return fftconvolve(np.asarray(x, np.float64), h)[:len(x)]
+
+
+def _rel_rms(y, r):
+    return float(np.sqrt(np.mean((y - r) ** 2)) / max(np.sqrt(np.mean(r ** 2)), 1e-30))
+
+
+def test_fftconvolve_matches_oracle():
+    from oracle import msound_oracle as O
+    rng = np.random.default_rng(1)
+    x, h = rng.standard_normal(5000), O.synthetic_fir_taps(3000)
+    np.testing.assert_allclose(_ref(x, h), O.fir_causal(x, h), rtol=0, atol=1e-9)
+
+
+@pytest.mark.parametrize("M,n,S", [(16384, 60000, 3), (65536, 200000, 2), (8192, 384000, 1)])
+def test_fir_long_taps(M, n, S):
+    import torch
+    from msgpu.engine import default_engine
+    from oracle import msound_oracle as O
+    h = O.synthetic_fir_taps(M)
+    x = np.stack([np.random.default_rng(b).standard_normal(n).astype(np.float32) for b in range(S)])
+    eng = default_engine(0)
+    y, (N, P, Q) = eng.fir(torch.from_numpy(x).cuda(), h)
+    torch.cuda.synchronize()
+    assert P * Q >= M and N <= 32768
+    y = y.cpu().numpy()
+    for b in range(S):
+        assert _rel_rms(y[b], _ref(x[b], h)) <= REL, (b, N, P, Q)
+
+
+@pytest.mark.parametrize("M,n", [(1, 1000), (5, 1), (300, 7), (20000, 9000), (70000, 30000), (4097, 4096)])
+def test_fir_edges(M, n):
+    import msgpu
+    from oracle import msound_oracle as O
+    rng = np.random.default_rng(M + n)
+    h = rng.standard_normal(M)
+    x = rng.standard_normal(n).astype(np.float32)
+    y = msgpu.fir(x, h)
+    r = O.fir_causal(x, h)
+    assert y.shape == (n,)
+    assert _rel_rms(y, r) <= REL
+
+
+def test_fir_errors():
+    import torch
+    from msgpu.engine import default_engine
+    eng = default_engine(0)
+    x = torch.zeros(1000, device="cuda")
+    with pytest.raises(RuntimeError):
+        eng.fir(x, np.ones(10), out=x)
+    with pytest.raises(NotImplementedError):
+        eng.fir(x, np.ones(64 * 32768))

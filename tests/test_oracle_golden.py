@@ -169,3 +169,13 @@ def test_stft_mag_db_pinned():
         S = O.stft_mag_db(z[f"{name}_x"], sr, win=win, hop=hop, max_frames=mf)
         assert S.shape == z[f"{name}_S"].shape
         assert np.max(np.abs(S.astype(np.float32) - z[f"{name}_S"])) <= 1e-3, name
+
+
+def test_fir_causal_is_the_capped_ir_convolution():
+    """fir_causal is convolve_ir_short's arithmetic (MS:438-445) for IRs inside the 8192 cap."""
+    rng = np.random.default_rng(5)
+    x = rng.standard_normal(3000)
+    ir = O.peak_normalize(rng.standard_normal(700), 0.9)
+    np.testing.assert_array_equal(O.fir_causal(x, O.ir_kernel(ir)), O.convolve_ir_short(x, ir))
+    h = O.synthetic_fir_taps(16384)
+    assert h.shape == (16384,) and abs(np.max(np.abs(h)) - 0.9) < 1e-12
