@@ -175,7 +175,7 @@ k_fir2(const PresetRt* __restrict__ rt, const int2* __restrict__ jobs, const flo
     extern __shared__ __attribute__((aligned(16))) float2 lds[];
     float2* tab = lds;
     float2* buf = lds + G::TAB;
-    const int2 job = jobs[blockIdx.x];
+    const int2 job = jobs[xcd_block(blockIdx.x, gridDim.x)];
     const PresetRt& pr = rt[job.x];
     const int P = pr.fir_P, Q = pr.fir_Q;
     const int64_t n = pr.out_n;

@@ -273,7 +273,7 @@ __global__ void __launch_bounds__(OLA_T)
 k_ola_env(const msg_event* __restrict__ events, const PresetRt* __restrict__ rt,
           const int32_t* __restrict__ tile_begin, int n_presets,
           const float* __restrict__ grain_pool, float* __restrict__ mono) {
-    const int b = blockIdx.x;
+    const int b = xcd_block(blockIdx.x, gridDim.x);
     const int p = find_preset(tile_begin, n_presets, b);
     const PresetRt& r = rt[p];
     const int64_t t0 = (int64_t)(b - r.tile_begin) * OLA_TILE;
@@ -408,7 +408,7 @@ k_stereo_max(const PresetRt* __restrict__ rt, const int32_t* __restrict__ st_beg
              const float* __restrict__ ybuf, const float* __restrict__ rbuf, unsigned* __restrict__ maxbits) {
     __shared__ __attribute__((aligned(16))) float w[ST_WIN];
     __shared__ float wm[ST_T / 64];
-    const int b = blockIdx.x;
+    const int b = xcd_block(blockIdx.x, gridDim.x);
     const int p = find_preset(st_begin, n_presets, b);
     const PresetRt& r = rt[p];
     const float* y = ybuf + r.y_off;
@@ -467,7 +467,7 @@ k_stereo_out(const PresetRt* __restrict__ rt, const int32_t* __restrict__ st_beg
              float* __restrict__ out) {
     __shared__ __attribute__((aligned(16))) float w[ST_WIN];
     __shared__ __attribute__((aligned(16))) float lw[ST_TILE];
-    const int b = blockIdx.x;
+    const int b = xcd_block(blockIdx.x, gridDim.x);
     const int p = find_preset(st_begin, n_presets, b);
     const PresetRt& r = rt[p];
     const float* y = ybuf + r.y_off;

@@ -103,11 +103,36 @@ constexpr int ST_T = 256;
 constexpr int ST_TILE = 4096;
 
 // shared helpers
+//
+// XCD-aware block order.  Workgroups are dispatched round-robin over the 8
+// XCDs (block b -> XCD b % 8), and each XCD has its own L2.  Kernels whose
+// neighbouring jobs share input (FIR blocks of one preset re-read the same
+// partition spectra and overlapping input segments; overlap-add tiles read the
+// same grains; stereo tiles overlap by their halo) remap b so that each XCD
+// takes one contiguous range of jobs: the shared lines then stay in one L2.
+constexpr int MSG_XCDS = 8;
+__device__ __forceinline__ int xcd_block(int b, int grid) {
+    const int x = b % MSG_XCDS, i = b / MSG_XCDS;
+    const int per = grid / MSG_XCDS, rem = grid % MSG_XCDS;
+    return x < rem ? x * (per + 1) + i : rem * (per + 1) + (x - rem) * per + i;
+}
+
+// Largest p with begin[p] <= b (begin non-decreasing, begin[0] = 0): a 64-ary
+// search, one candidate per lane and a ballot per level, so a block finds its
+// preset in ceil(log64 n) dependent loads (2 for 1024 presets) instead of
+// log2 n.  Short-lived blocks (a 4096-frame tile) were latency-bound on the
+// binary search.  Call from every lane of a wave (uniform control flow).
 __device__ __forceinline__ int find_preset(const int32_t* __restrict__ begin, int n_presets, int b) {
-    int lo = 0, hi = n_presets - 1;
-    while (lo < hi) {
-        const int mid = (lo + hi + 1) >> 1;
-        if (begin[mid] <= b) lo = mid; else hi = mid - 1;
+    const int lane = (int)(threadIdx.x & 63);
+    int lo = 0, len = n_presets;
+    while (len > 1) {
+        const int step = (len + 63) >> 6;
+        const int off = lane * step;
+        const bool ok = off < len && begin[lo + off] <= b;
+        const unsigned long long m = __ballot(ok);
+        const int c = 63 - __clzll(m);      // lane 0 always holds (begin[lo] <= b)
+        lo += c * step;
+        len = min(step, len - c * step);
     }
     return lo;
 }

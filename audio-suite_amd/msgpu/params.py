@@ -131,6 +131,11 @@ CONFIGS: dict = {
     "C2": dict(base_sr=192000, out_dur_s=1.0, gen_mode="Resonant strike",
                time_unfold=10.0, partial_stretch=1.0, event_process="Poisson",
                space_ir_on=True, space_ir_max_samps=4096, _ir_name="ir_metallic_ping_180ms"),
+    # H48: the metric label's "384 kHz -> 48 kHz" read literally:
+    # design SR 384 kHz (unfold x8) rendered to a 48 kHz output, C2's IR.
+    "H48": dict(base_sr=48000, out_dur_s=1.0, gen_mode="Resonant strike",
+                time_unfold=8.0, partial_stretch=1.0, event_process="Poisson",
+                space_ir_on=True, space_ir_max_samps=4096, _ir_name="ir_metallic_ping_180ms"),
     # C3: 384 kHz, unfold x100 (design SR clamps to 30 MHz, MS:597), stretch x2,
     # IR request 16384 taps (capped to 8192 by MS:443).
     "C3": dict(base_sr=384000, out_dur_s=1.0, gen_mode="Resonant strike",

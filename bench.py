@@ -34,7 +34,9 @@ HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: 8.0 TB/s spec
 TRAFFIC_JSON = os.path.join(REPO, "profiles", "traffic.json")
 # bench stage -> the kernel it times (rocprofv3 kernel-name prefix)
 STAGE_KERNEL = {"generate": "k_gen_normal", "spectral": "k_spectral", "overlap_add": "k_ola_env",
-                "fir_kernel": "k_fir<", "stereo": "k_stereo_out"}
+                "fir_kernel": "k_fir2<", "stereo": "k_stereo_out"}
+# host cores of the GPU box available to one job (its CPU share; nproc shows the machine)
+BOX_CORES = 16
 
 
 def load_irs():
@@ -72,24 +74,45 @@ def measured_traffic(kernel, cfg, batch):
     return None
 
 
-def cpu_baseline(cfg, irs, budget_s):
+def _cpu_worker(job):
+    """Render presets seed0, seed0 + stride, ... with the oracle for budget_s seconds."""
+    cfg, seed0, stride, budget_s = job
     from oracle import msound_oracle as O   # CPU baseline only
     import msgpu
-    done = 0
-    frames = 0
+    irs = load_irs()
+    done = frames = 0
     t0 = time.perf_counter()
     while True:
-        p = msgpu.config_params(cfg, seed=1000 + done, irs=irs)
+        p = msgpu.config_params(cfg, seed=seed0 + done * stride, irs=irs)
         a, _ = O.render(p)
         frames += a.shape[0]
         done += 1
         if time.perf_counter() - t0 >= budget_s or done >= 256:
             break
-    dt = time.perf_counter() - t0
-    return {"value": frames / dt / 1e6, "unit": "Msamples/s", "cores": 1, "kind": "port",
-            "sample": f"{done} {cfg} presets (seeds 1000..{999 + done}) rendered sequentially by "
-                      f"oracle/msound_oracle.py (NumPy restatement of main_v2.render) on 1 host core "
-                      f"in {dt:.1f} s"}
+    return done, frames, time.perf_counter() - t0
+
+
+def cpu_baseline(cfg, budget_s):
+    """The NumPy restatement of render() on the host: one core,
+    then one process per core of the box's share.  Runs before the GPU is touched
+    (the pool forks)."""
+    import multiprocessing as mp
+    done, frames, dt = _cpu_worker((cfg, 1000, 1, budget_s))
+    single = frames / dt / 1e6
+    procs = max(1, min(BOX_CORES, len(os.sched_getaffinity(0))))
+    ctx = mp.get_context("fork")
+    t0 = time.perf_counter()
+    with ctx.Pool(procs) as pool:
+        res = pool.map(_cpu_worker, [(cfg, 1000 + i, procs, budget_s) for i in range(procs)])
+    wall = time.perf_counter() - t0
+    pdone = sum(r[0] for r in res)
+    pframes = sum(r[1] for r in res)
+    return {"value": pframes / wall / 1e6, "unit": "Msamples/s", "cores": procs, "kind": "port",
+            "single_core": round(single, 4),
+            "sample": f"{cfg} presets rendered by oracle/msound_oracle.py (NumPy restatement of "
+                      f"main_v2.render): {done} presets on 1 core in {dt:.1f} s "
+                      f"({single:.3f} Msamples/s), then {pdone} presets on {procs} processes in "
+                      f"{wall:.1f} s"}
 
 
 def rank_seeds(rank, batch):
@@ -119,12 +142,18 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--streams", type=int, default=2, help="in-flight sub-batches (contexts/streams) per GPU")
     ap.add_argument("--iso-steps", type=int, default=3, help="single-stream renders for roofline_isolated")
+    ap.add_argument("--h48-steps", type=int, default=5,
+                    help="steps of the 384 kHz -> 48 kHz point (config H48, same batch), 0 = skip")
     args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        cpu = cpu_baseline(args.config, args.cpu_budget)
 
     import torch
     import torch.distributed as dist
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         torch.cuda.set_device(local)
@@ -221,9 +250,27 @@ def main():
                     "stage_ms": iso, "note": f"whole batch on one stream, {args.iso_steps} renders after the "
                                              f"timed region"}
 
-    cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu:
-        cpu = cpu_baseline(args.config, irs, args.cpu_budget)
+    # the metric label's "384 kHz -> 48 kHz" read literally: H48 presets, same batch
+    h48 = None
+    if args.h48_steps > 0 and args.config != "H48":
+        hp = [msgpu.config_params("H48", seed=s, irs=irs) for s in seeds]
+        hpk = PackedBatch(hp)
+        ho = engs[0].alloc_output(hpk)
+        engs[0].render_packed(hpk, ho, streams[0])
+        torch.cuda.synchronize(dev)
+        barrier()
+        t1 = time.perf_counter()
+        for _ in range(args.h48_steps):
+            engs[0].render_packed(hpk, ho, streams[0])
+        torch.cuda.synchronize(dev)
+        barrier()
+        he = max_over_ranks(time.perf_counter() - t1, world, f"cuda:{dev}")
+        h48 = {"config": "H48: 48 kHz out, unfold x8 (384 kHz design SR), Poisson 18/s, 1 s, 4096-tap IR, "
+                         "ER 320 taps, stereo",
+               "value": round(hpk.total_frames * world * args.h48_steps / he / 1e6, 3), "unit": "Msamples/s",
+               "ms_per_step": round(he / args.h48_steps * 1e3, 3), "steps": args.h48_steps,
+               "presets_per_gpu": args.batch, "streams_per_gpu": 1}
+        del ho
 
     if rank == 0:
         line = {
@@ -247,6 +294,7 @@ def main():
             "stage_ms": stages, "stage_algorithmic_GBs": stage_gbs,
             "design_msamples_per_s": round(sum_n * world * args.steps / elapsed / 1e6, 1),
             "cpu_baseline": cpu,
+            "point_384k_to_48k": h48,
         }
         print(json.dumps(line), flush=True)
     if world > 1:
