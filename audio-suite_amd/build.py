@@ -28,7 +28,9 @@ def _newest_header():
     return max(os.path.getmtime(h) for h in HEADERS)
 
 
-VARIANTS = {"": ([], "build", "libmsgpu.so"), "stamps": (["-DMSG_STAMPS"], "build_stamps", "libmsgpu_stamps.so")}
+VARIANTS = {"": ([], "build", "libmsgpu.so"), "stamps": (["-DMSG_STAMPS"], "build_stamps", "libmsgpu_stamps.so"),
+            # tuning experiments: python build.py --exp with MSGPU_EXP_DEFS="-DNAME=V ..."
+            "exp": (os.environ.get("MSGPU_EXP_DEFS", "").split(), "build_exp", "libmsgpu_exp.so")}
 
 
 def _compile(tu, variant=""):
@@ -65,4 +67,5 @@ def build(force: bool = False, variant: str = "") -> str:
 
 
 if __name__ == "__main__":
-    print(build(force="--force" in sys.argv, variant="stamps" if "--stamps" in sys.argv else ""))
+    var = "stamps" if "--stamps" in sys.argv else ("exp" if "--exp" in sys.argv else "")
+    print(build(force="--force" in sys.argv, variant=var))

@@ -11,6 +11,8 @@ template <int M> static void fir2_attr() {
 void fir_init_attrs() {
     fir2_attr<1024>(); fir2_attr<2048>(); fir2_attr<4096>(); fir2_attr<8192>(); fir2_attr<16384>();
     (void)hipFuncSetAttribute((const void*)k_fir_h<FIR_T, FIR_M>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
+    (void)hipFuncSetAttribute((const void*)k_fir_hconv<FIR_T, FIR_M>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              LDS_MAX);
     (void)hipFuncSetAttribute((const void*)k_ir_spec<FIR_T, FIR_M>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               LDS_MAX);
 }
@@ -22,12 +24,20 @@ hipError_t launch_ir_spec(unsigned grid, int lds_bytes, hipStream_t s, const int
     return hipGetLastError();
 }
 
+hipError_t launch_fir_hconv(unsigned grid, int lds_bytes, hipStream_t s, const PresetRt* rt, const int32_t* conv_list,
+                            const RealPlan* fir_plans, const int32_t* fir_plan_of, const int32_t* er_off,
+                            const double* er_gain, const float2* ir_spec, float* hs) {
+    hipLaunchKernelGGL((k_fir_hconv<FIR_T, FIR_M>), dim3(grid), dim3(FIR_T), lds_bytes, s, rt, conv_list, fir_plans,
+                       fir_plan_of, er_off, er_gain, ir_spec, hs);
+    return hipGetLastError();
+}
+
 hipError_t launch_fir_h(unsigned grid, int lds_bytes, hipStream_t s, const PresetRt* rt, const int32_t* hblk_begin,
                         int n_presets, const RealPlan* fir_plans, const int32_t* fir_plan_of,
                         const int32_t* er_off, const double* er_gain, const double* ir_bank,
-                        const float2* ir_spec, float2* hspec) {
+                        const float* hs, float2* hspec) {
     hipLaunchKernelGGL((k_fir_h<FIR_T, FIR_M>), dim3(grid), dim3(FIR_T), lds_bytes, s, rt, hblk_begin, n_presets,
-                       fir_plans, fir_plan_of, er_off, er_gain, ir_bank, ir_spec, hspec);
+                       fir_plans, fir_plan_of, er_off, er_gain, ir_bank, hs, hspec);
     return hipGetLastError();
 }
 

@@ -120,8 +120,11 @@ MSG_DEV float gen_basic_sample(const GenBasicConst& c, int j, float nrm) {
 // The float32 path forms the fast-path normal in float32 from the top 32 bits
 // of its 52-bit ziggurat integer (|error| <= 1 ulp of float32); slow draws and
 // RAW64 use the exact float64 product.
+#ifndef MSG_GEN_WAVES
+#define MSG_GEN_WAVES 1
+#endif
 template <bool RAW64>
-__global__ void __launch_bounds__(GEN_T)
+__global__ void __launch_bounds__(GEN_T, MSG_GEN_WAVES)
 k_gen_normal(const msg_preset* __restrict__ presets, const msg_event* __restrict__ events,
              const PresetRt* __restrict__ rt, const int32_t* __restrict__ ev_list, int n_list,
              nprng::Zig z, const JumpTab* __restrict__ jt, float* __restrict__ pool,
@@ -269,6 +272,26 @@ MSG_DEV float adsr_at(const PresetRt& r, int t) {
     return S * (1.0f - env_pow(u, c));
 }
 
+// Number of events (sorted by start) with start <= lim: a 64-ary ballot search,
+// one dependent load for up to 64 events instead of a log2 n binary search.
+// Call from every lane of a wave.
+MSG_DEV int events_starting_by(const msg_event* __restrict__ ev, int n, int64_t lim) {
+    const int lane = (int)(threadIdx.x & 63);
+    int lo = 0, len = n;
+    while (len > 0) {
+        const int step = (len + 63) >> 6;
+        const int nseg = (len + step - 1) / step;
+        const int last = min((lane + 1) * step, len) - 1;       // last element of this lane's segment
+        const bool ok = lane < nseg && (int64_t)ev[lo + last].start <= lim;
+        const int c = __popcll(__ballot(ok));                   // sorted: a prefix of the segments
+        if (c == nseg) { lo += len; break; }
+        lo += c * step;
+        if (step == 1) break;
+        len = min(step, len - c * step) - 1;                    // segment c ends above lim
+    }
+    return lo;
+}
+
 __global__ void __launch_bounds__(OLA_T)
 k_ola_env(const msg_event* __restrict__ events, const PresetRt* __restrict__ rt,
           const int32_t* __restrict__ tile_begin, int n_presets,
@@ -285,12 +308,7 @@ k_ola_env(const msg_event* __restrict__ events, const PresetRt* __restrict__ rt,
     for (int u = 0; u < PER; ++u) acc[u] = 0.f;
     // events are sorted by start: the first one that can reach t0 starts after t0 - max_n
     const msg_event* ev = events + r.ev_begin;
-    int lo = 0, hi = r.n_events;
-    const int64_t lim = t0 - (int64_t)r.max_n;
-    while (lo < hi) {
-        const int mid = (lo + hi) >> 1;
-        if ((int64_t)ev[mid].start <= lim) lo = mid + 1; else hi = mid;
-    }
+    const int lo = events_starting_by(ev, r.n_events, t0 - (int64_t)r.max_n);
     // 64 events per round: lane k fetches event lo+k, then the wave walks them
     // from registers (readlane) so all their grain reads are in flight together
     for (int k0 = lo; k0 < r.n_events; k0 += 64) {

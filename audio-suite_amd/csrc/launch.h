@@ -32,10 +32,13 @@ hipError_t launch_spectral_ct(int plan, unsigned grid, hipStream_t s, const msg_
 void fir_init_attrs();
 hipError_t launch_ir_spec(unsigned grid, int lds_bytes, hipStream_t s, const int64_t* jobs, int n_jobs,
                           const RealPlan* fir_plans, const double* ir_bank, float2* ir_spec);
+hipError_t launch_fir_hconv(unsigned grid, int lds_bytes, hipStream_t s, const PresetRt* rt, const int32_t* conv_list,
+                            const RealPlan* fir_plans, const int32_t* fir_plan_of, const int32_t* er_off,
+                            const double* er_gain, const float2* ir_spec, float* hs);
 hipError_t launch_fir_h(unsigned grid, int lds_bytes, hipStream_t s, const PresetRt* rt, const int32_t* hblk_begin,
                         int n_presets, const RealPlan* fir_plans, const int32_t* fir_plan_of,
                         const int32_t* er_off, const double* er_gain, const double* ir_bank,
-                        const float2* ir_spec, float2* hspec);
+                        const float* hs, float2* hspec);
 // register-resident FIR with compile-time transform size M = N/2 in {1024..16384}
 bool fir2_tables_host(int M, std::vector<float>& out);
 hipError_t launch_fir2(int M, unsigned grid, hipStream_t s, const PresetRt* rt, const int2* jobs,

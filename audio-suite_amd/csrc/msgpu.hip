@@ -93,6 +93,8 @@ struct msg_ctx {
     DevBuf<int32_t> gen_list, spec_small, spec_big, tile_begin, fir_begin, h_begin, st_begin, fir_plan_of;
     DevBuf<float> micro, grain, mono_a, mono_y;
     DevBuf<float2> hspec, irspec;
+    DevBuf<float> hscratch;                     // h of ER + IR presets (k_fir_hconv -> k_fir_h)
+    DevBuf<int32_t> conv_list;
     DevBuf<int2> fir_jobs;
     DevBuf<int32_t> spec_ct_list;
     DevBuf<int64_t> irjobs;
@@ -475,6 +477,7 @@ void msg_destroy(msg_ctx* ctx) {
     ctx->spec_big.release(); ctx->tile_begin.release(); ctx->fir_begin.release(); ctx->h_begin.release();
     ctx->st_begin.release(); ctx->fir_plan_of.release(); ctx->micro.release(); ctx->grain.release();
     ctx->mono_a.release(); ctx->mono_y.release(); ctx->hspec.release(); ctx->irspec.release();
+    ctx->hscratch.release(); ctx->conv_list.release();
     ctx->irjobs.release(); ctx->irbank.release();
     ctx->maxbits.release();
     for (void* p : ctx->plans64.allocs) hipFree(p);
@@ -893,6 +896,8 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
     }
     int64_t pool = 0, ysum = 0, hsum = 0, irs_sum = 0;
     int32_t tiles = 0, fblocks = 0, hblocks = 0, stiles = 0;
+    std::vector<int32_t> conv_list;
+    int64_t hs_sum = 0;
     int spec_small_lds = 0, spec_big_lds = 0, fir_lds = 0;
     std::vector<int32_t> spec_ct[SPEC_CT_PLANS];           // events of the compile-time spectral plans
     const char* ct_env = getenv("MSGPU_SPEC_CT");         // "0": runtime-plan kernels only (tests)
@@ -999,6 +1004,9 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
                     irs_sum += N / 2 + 1;
                 }
                 r.irs_off = it->second;
+                r.hs_off = hs_sum;
+                hs_sum += N;
+                conv_list.push_back(p);
             } else if (er && M > N) {
                 return fail(ctx, MSG_E_UNSUPPORTED, "early-reflection span exceeds the FIR transform");
             }
@@ -1234,6 +1242,8 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
     HIPCHK(ctx, ctx->mono_y.ensure(ysum));
     HIPCHK(ctx, ctx->hspec.ensure(hsum));
     HIPCHK(ctx, ctx->irspec.ensure(irs_sum));
+    HIPCHK(ctx, ctx->hscratch.ensure(hs_sum));
+    HIPCHK(ctx, ctx->conv_list.ensure(conv_list.size()));
     HIPCHK(ctx, ctx->irjobs.ensure(ir_jobs.size()));
     HIPCHK(ctx, ctx->irbank.ensure(irbank.size()));
     HIPCHK(ctx, ctx->maxbits.ensure(P));
@@ -1263,6 +1273,7 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
     HIPCHK(ctx, h2d(ctx->fir_plan_of.p, fir_plan_of.data(), sizeof(int32_t) * P));
     HIPCHK(ctx, h2d(ctx->irbank.p, irbank.data(), sizeof(double) * irbank.size()));
     HIPCHK(ctx, h2d(ctx->irjobs.p, ir_jobs.data(), sizeof(int64_t) * ir_jobs.size()));
+    HIPCHK(ctx, h2d(ctx->conv_list.p, conv_list.data(), sizeof(int32_t) * conv_list.size()));
     HIPCHK(ctx, hipMemsetAsync(ctx->maxbits.p, 0, sizeof(unsigned) * P, s));
     HIPCHK(ctx, h2d(ctx->ev64.p, ev64.data(), sizeof(Ev64) * ev64.size()));
     HIPCHK(ctx, h2d(ctx->g64_list.p, g64_list.data(), sizeof(int32_t) * g64_list.size()));
@@ -1329,9 +1340,13 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
             HIPCHK(ctx, launch_ir_spec((unsigned)(ir_jobs.size() / 4), fir_lds, s, ctx->irjobs.p,
                                        (int)(ir_jobs.size() / 4), ctx->fir_plans.dev.p, ctx->irbank.p, ctx->irspec.p));
         }
+        if (!conv_list.empty())
+            HIPCHK(ctx, launch_fir_hconv((unsigned)conv_list.size(), fir_lds, s, ctx->prt.p, ctx->conv_list.p,
+                                         ctx->fir_plans.dev.p, ctx->fir_plan_of.p, ctx->er_off.p, ctx->er_gain.p,
+                                         ctx->irspec.p, ctx->hscratch.p));
         HIPCHK(ctx, launch_fir_h((unsigned)hblocks, fir_lds, s, ctx->prt.p, ctx->h_begin.p, P,
                                  ctx->fir_plans.dev.p, ctx->fir_plan_of.p, ctx->er_off.p, ctx->er_gain.p,
-                                 ctx->irbank.p, ctx->irspec.p, ctx->hspec.p));
+                                 ctx->irbank.p, ctx->hscratch.p, ctx->hspec.p));
         stage_mark(ctx, 8, s);
         for (int i = 0; i < 5; ++i)
             if (fjob_off[i + 1] > fjob_off[i])

@@ -49,6 +49,7 @@ struct PresetRt {
     int64_t img_off;
     int32_t img_h, img_w;
     int64_t r2_off;        // stereo_fir == 2: rotated right channel in the odd-stereo buffer
+    int64_t hs_off;        // ER + IR presets: h in the FIR scratch (fir_N floats, k_fir_hconv)
 };
 
 // Per-event spectral work descriptor (host-built after planning).
