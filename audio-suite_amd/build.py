@@ -9,6 +9,7 @@ MSGPU_LIB=.../libmsgpu_stamps.so.  Never the product library.
 """
 import concurrent.futures as cf
 import os
+import re
 import subprocess
 import sys
 
@@ -24,8 +25,24 @@ FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC",
          "-Wall", "-Wno-unused-function", "-Wno-unused-value", "-Wno-unused-result"]
 
 
-def _newest_header():
-    return max(os.path.getmtime(h) for h in HEADERS)
+_INC = re.compile(r'^\s*#\s*include\s+"([^"]+)"', re.M)
+
+
+def _deps(path, seen=None):
+    """Local headers a source includes, transitively (quoted includes only)."""
+    seen = set() if seen is None else seen
+    with open(path) as f:
+        text = f.read()
+    for inc in _INC.findall(text):
+        h = os.path.normpath(os.path.join(os.path.dirname(path), inc))
+        if os.path.exists(h) and h not in seen:
+            seen.add(h)
+            _deps(h, seen)
+    return seen
+
+
+def _newest_dep(src):
+    return max([os.path.getmtime(src)] + [os.path.getmtime(h) for h in _deps(src)])
 
 
 VARIANTS = {"": ([], "build", "libmsgpu.so"), "stamps": (["-DMSG_STAMPS"], "build_stamps", "libmsgpu_stamps.so"),
@@ -37,7 +54,7 @@ def _compile(tu, variant=""):
     defs, objdir, _ = VARIANTS[variant]
     src = os.path.join(CSRC, tu)
     obj = os.path.join(HERE, objdir, tu.replace(".hip", ".o"))
-    if os.path.exists(obj) and os.path.getmtime(obj) >= max(os.path.getmtime(src), _newest_header()):
+    if os.path.exists(obj) and os.path.getmtime(obj) >= _newest_dep(src):
         return obj
     cmd = [HIPCC, *FLAGS, *defs, "-c", "-o", obj + ".tmp", src]
     print("[msgpu build]", " ".join(cmd), flush=True)

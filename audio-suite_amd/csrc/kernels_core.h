@@ -81,8 +81,10 @@ MSG_DEV double slow_normal(nprng::u128 st, nprng::u128 inc, uint64_t rabs, int i
 
 // Closed-form part of gen_basic for sample j given its normal N_j (MS:235-268).
 // The ring phase frac(j f / sr) is reduced exactly in float32 from a two-term
-// split of f / sr (j * fa with its fma rounding error, plus j * fb); the
-// decays are exp2f of j times a float64-built coefficient.
+// split of f / sr (j * fa with its fma rounding error, plus j * fb), so the
+// hardware sine (v_sin_f32 takes revolutions: one transcendental instead of a
+// software sinpi) only ever sees [0, 1); the decays are the hardware exp2 of j
+// times a float64-built coefficient (arguments >= -126: no denormal path).
 struct GenBasicConst {
     int mode;            // MSG_GEN_*
     int n, fade;
@@ -102,7 +104,8 @@ MSG_DEV float gen_basic_sample(const GenBasicConst& c, int j, float nrm) {
     const float jf = (float)j;
     if (c.mode == MSG_GEN_RESONANT) {
         const float ph = ring_phase(jf, c.fa, c.fb);
-        x = 0.9f * sinpif(2.0f * ph) * exp2f(jf * c.k_ring) + 0.25f * nrm * exp2f(jf * c.k_exc);
+        x = 0.9f * __builtin_amdgcn_sinf(ph) * __builtin_amdgcn_exp2f(fmaxf(jf * c.k_ring, -126.f)) +
+            0.25f * nrm * __builtin_amdgcn_exp2f(fmaxf(jf * c.k_exc, -126.f));
     } else if (c.mode == MSG_GEN_GAUSSIAN_CLICK) {
         const float u = jf * c.inv_sigma;
         x = expf(-0.5f * (u * u)) * (nrm * 0.12f + 1.0f);
