@@ -198,7 +198,7 @@ k_fir2(const PresetRt* __restrict__ rt, const int2* __restrict__ jobs, const flo
         const int js[2] = {t, t0z ? NB3 / 2 : NB3 - t};
         // ---- pass 1: x segment (zero outside [0, n)) -> DFT_R1 -> LDS A
         const int64_t s0 = t0 - (int64_t)q * P - (P - 1);
-        const bool fast = s0 >= 0 && s0 + 2 * M <= n && (s0 & 1) == 0;
+        const bool fast = s0 >= 0 && s0 + 2 * M <= n && (((uintptr_t)(x + s0)) & 7) == 0;
 #pragma unroll
         for (int b = 0; b < BP1; ++b) {
             const int j = t + b * T;
@@ -316,6 +316,201 @@ k_fir2(const PresetRt* __restrict__ rt, const int2* __restrict__ jobs, const flo
             const int64_t o = t0 + u - (P - 1);
             if (u >= P - 1 && o < n) y[(uint32_t)o] = v[r].x * s;
             if (u + 1 >= P - 1 && o + 1 < n) y[(uint32_t)(o + 1)] = -v[r].y * s;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Frequency-domain delay line (standalone FIR with many partitions, msg_fir).
+// Partitions and blocks are both P = M samples (N = 2M): segment b is
+// x[bM - M, bM + M), its spectrum X_b is computed once (k_fdl_fwd) and reused
+// by the Q blocks b .. b+Q-1, so a block costs two transforms instead of Q+1:
+//     y[bM, bM + M) = samples [M, 2M) of IFFT_N( sum_q X_{b-q} . H_q ).
+// Spectra are stored at natural bins (M+1 float2 per segment, H's layout);
+// PresetRt.fir_block_begin is the signal's first segment index.
+// ---------------------------------------------------------------------------
+// real-FFT split of bins k, M-k from the packed Z (the first half of fir_pair_mac)
+MSG_DEV void fir_pair_split(float2 zk, float2 zm, float2 wk, float2& xk, float2& xm) {
+    const float2 e = make_float2(0.5f * (zk.x + zm.x), 0.5f * (zk.y - zm.y));
+    const float2 d = make_float2(zk.x - zm.x, zk.y + zm.y);
+    const float2 o = make_float2(0.5f * d.y, -0.5f * d.x);
+    const float2 wo = cmul(wk, o);
+    xk = cadd(e, wo);
+    xm = make_float2(e.x - wo.x, wo.y - e.y);
+}
+
+template <int M>
+__global__ void __launch_bounds__(FirGeo<M>::T)
+k_fdl_fwd(const PresetRt* __restrict__ rt, const int2* __restrict__ jobs, const float2* __restrict__ tables,
+          const float* __restrict__ x_in, float2* __restrict__ xspec) {
+    using G = FirGeo<M>;
+    constexpr int T = G::T, R1 = G::R1, R2 = G::R2, R3 = G::R3;
+    constexpr int NB1 = G::NB1, NB3 = G::NB3, BP1 = G::BP1, BP2 = G::BP2;
+    extern __shared__ __attribute__((aligned(16))) float2 lds[];
+    float2* tab = lds;
+    float2* buf = lds + G::TAB;
+    const int2 job = jobs[xcd_block(blockIdx.x, gridDim.x)];
+    const PresetRt& pr = rt[job.x];
+    const int64_t n = pr.out_n;
+    const float* x = x_in + pr.y_off;
+    const int t = threadIdx.x;
+    for (int i = t; i < G::TAB_USED; i += T) tab[i] = tables[i];
+    const bool t0z = (t == 0);
+    const int js[2] = {t, t0z ? NB3 / 2 : NB3 - t};
+    const int64_t s0 = (int64_t)job.y * M - M;
+    const bool fast = s0 >= 0 && s0 + 2 * M <= n && (((uintptr_t)(x + s0)) & 7) == 0;
+#pragma unroll
+    for (int b = 0; b < BP1; ++b) {
+        const int j = t + b * T;
+        float2 v[R1];
+        if (fast) {
+            const float2* z = reinterpret_cast<const float2*>(x + s0);
+#pragma unroll
+            for (int r = 0; r < R1; ++r) v[r] = z[(uint32_t)(j + r * NB1)];
+        } else {
+#pragma unroll
+            for (int r = 0; r < R1; ++r) {
+                const int64_t a = s0 + 2 * (int64_t)(j + r * NB1);
+                const bool in0 = a >= 0 && a < n, in1 = a + 1 >= 0 && a + 1 < n;
+                const float x0 = x[(uint32_t)(in0 ? a : 0)], x1 = x[(uint32_t)(in1 ? a + 1 : 0)];
+                v[r] = make_float2(in0 ? x0 : 0.f, in1 ? x1 : 0.f);
+            }
+        }
+        Dft<R1, false>::run(v);
+        const int base = padx<G::SA>(j * R1);
+#pragma unroll
+        for (int r = 0; r < R1; ++r) buf[base + r] = v[r];
+    }
+    __syncthreads();
+    fir_pass_lds<M, R2, R1, BP2, G::SA, G::SB>(buf, tab, t);
+    __syncthreads();
+    float2 v[2][R3];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const int base = padx<G::SB>(js[h]);
+#pragma unroll
+        for (int r = 0; r < R3; ++r) v[h][r] = buf[base + padx<G::SB>(r * NB3)];
+    }
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        twiddle_pow<R3>(v[h], fir_wM(tab, G::OFF_MLO, G::OFF_MHI, js[h]));
+        Dft<R3, false>::run(v[h]);
+    }
+    float2 a[R3], bb[R3];
+    fir_slots<R3>(v, a, bb, t0z);
+    const float2 wA = fir_wM(tab, G::OFF_PLO, G::OFF_PHI, js[0]);
+    float2* X = xspec + (int64_t)(pr.fir_block_begin + job.y) * (M + 1);
+#pragma unroll
+    for (int r = 0; r < R3; ++r) {
+        const int kA = t0z ? fir_k0<M, R3>(r) : js[0] + r * NB3;
+        const float2 wk = t0z ? fir_w0<M, R3>(r) : cmul(wA, fir_cr<R3>(r));
+        if (t0z && r == R3 - 1) {          // DC and Nyquist (packed in z0), bin M/2
+            const float2 z0 = a[r];
+            X[0] = make_float2(z0.x + z0.y, 0.f);
+            X[M] = make_float2(z0.x - z0.y, 0.f);
+            X[M / 2] = cconj(bb[0]);
+        } else {
+            float2 xk, xm;
+            fir_pair_split(a[r], bb[R3 - 1 - r], wk, xk, xm);
+            X[(uint32_t)kA] = xk;
+            X[(uint32_t)(M - kA)] = xm;
+        }
+    }
+}
+
+template <int M>
+__global__ void __launch_bounds__(FirGeo<M>::T)
+k_fdl_mac(const PresetRt* __restrict__ rt, const int2* __restrict__ jobs, const float2* __restrict__ tables,
+          const float2* __restrict__ hspec, const float2* __restrict__ xspec, float* __restrict__ y_out) {
+    using G = FirGeo<M>;
+    constexpr int T = G::T, R1 = G::R1, R2 = G::R2, R3 = G::R3;
+    constexpr int NB1 = G::NB1, NB3 = G::NB3, BP1 = G::BP1, BP2 = G::BP2;
+    extern __shared__ __attribute__((aligned(16))) float2 lds[];
+    float2* tab = lds;
+    float2* buf = lds + G::TAB;
+    const int2 job = jobs[xcd_block(blockIdx.x, gridDim.x)];
+    const PresetRt& pr = rt[job.x];
+    const int Q = pr.fir_Q;
+    const int64_t n = pr.out_n;
+    const int t = threadIdx.x;
+    for (int i = t; i < G::TAB_USED; i += T) tab[i] = tables[i];
+    float2 acc[2][R3];
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int r = 0; r < R3; ++r) acc[h][r] = make_float2(0.f, 0.f);
+    {
+        const bool t0z = (t == 0);
+        const int j0 = t;
+        const int nq = Q < job.y + 1 ? Q : job.y + 1;   // X_{b-q} of segments before the signal are zero
+        for (int q = 0; q < nq; ++q) {
+            const float2* X = xspec + (int64_t)(pr.fir_block_begin + job.y - q) * (M + 1);
+            const float2* H = hspec + pr.h_off + (int64_t)q * (M + 1);
+#pragma unroll
+            for (int r = 0; r < R3; ++r) {
+                const int kA = t0z ? fir_k0<M, R3>(r) : j0 + r * NB3;
+                if (t0z && r == R3 - 1) {
+                    const float2 x0 = X[0], xM = X[M], h0 = H[0], hM = H[M];
+                    acc[0][r] = cadd(acc[0][r], make_float2(x0.x * h0.x, xM.x * hM.x));   // (Y[0], Y[M]) packed
+                    acc[1][0] = cadd(acc[1][0], cmul(X[M / 2], H[M / 2]));
+                } else {
+                    acc[0][r] = cadd(acc[0][r], cmul(X[(uint32_t)kA], H[(uint32_t)kA]));
+                    acc[1][R3 - 1 - r] = cadd(acc[1][R3 - 1 - r], cmul(X[(uint32_t)(M - kA)], H[(uint32_t)(M - kA)]));
+                }
+            }
+        }
+    }
+    __syncthreads();   // twiddle table visible
+    // ---- inverse: as k_fir2
+    {
+        const int tt = otid();
+        const bool t0z = (tt == 0);
+        const float2 wA = fir_wM(tab, G::OFF_PLO, G::OFF_PHI, tt);
+#pragma unroll
+        for (int r = 0; r < R3; ++r) {
+            const float2 wk = t0z ? fir_w0<M, R3>(r) : cmul(wA, fir_cr<R3>(r));
+            if (r < R3 - 1) {
+                fir_pair_pre(acc[0][r], acc[1][R3 - 1 - r], wk);
+            } else {
+                float2 yk = acc[0][r], ym = acc[1][0];
+                fir_pair_pre(yk, ym, wk);
+                const float y0 = acc[0][r].x, yN = acc[0][r].y;
+                const float2 dc = make_float2(0.5f * (y0 + yN), -0.5f * (y0 - yN));
+                acc[0][r] = t0z ? dc : yk;
+                acc[1][0] = t0z ? acc[1][0] : ym;
+            }
+        }
+        fir_unslots<R3>(acc, t0z);
+    }
+    const int js[2] = {t, t == 0 ? NB3 / 2 : NB3 - t};
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        Dft<R3, false>::run(acc[h]);
+        const int base = padx<G::SC>(js[h] * R3);
+#pragma unroll
+        for (int r = 0; r < R3; ++r) buf[base + r] = acc[h][r];
+    }
+    __syncthreads();
+    fir_pass_lds<M, R2, R3, BP2, G::SC, G::SD>(buf, tab, t);
+    __syncthreads();
+    float* y = y_out + pr.y_off;
+    const float s = 1.0f / (float)M;
+    const int64_t t0 = (int64_t)job.y * M - M;       // segment start
+#pragma unroll
+    for (int b = 0; b < BP1; ++b) {
+        const int j = t + b * T;
+        float2 v[R1];
+        const int base = padx<G::SD>(j);
+#pragma unroll
+        for (int r = 0; r < R1; ++r) v[r] = buf[base + padx<G::SD>(r * NB1)];
+        twiddle_pow<R1>(v, fir_wM(tab, G::OFF_MLO, G::OFF_MHI, j));
+        Dft<R1, false>::run(v);
+#pragma unroll
+        for (int r = 0; r < R1; ++r) {
+            const int u = 2 * (j + r * NB1);
+            const int64_t o = t0 + u;
+            if (u >= M && o < n) y[(uint32_t)o] = v[r].x * s;
+            if (u + 1 >= M && o + 1 < n) y[(uint32_t)(o + 1)] = -v[r].y * s;
         }
     }
 }

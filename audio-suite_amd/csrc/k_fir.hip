@@ -6,6 +6,10 @@
 template <int M> static void fir2_attr() {
     (void)hipFuncSetAttribute((const void*)k_fir2<M>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               FirGeo<M>::LDS_BYTES);
+    (void)hipFuncSetAttribute((const void*)k_fdl_fwd<M>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              FirGeo<M>::LDS_BYTES);
+    (void)hipFuncSetAttribute((const void*)k_fdl_mac<M>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              FirGeo<M>::LDS_BYTES);
 }
 
 void fir_init_attrs() {
@@ -68,6 +72,27 @@ hipError_t launch_fir2(int M, unsigned grid, hipStream_t s, const PresetRt* rt, 
         case 4096: return fir2_go<4096>(grid, s, rt, jobs, tables, hspec, x_in, y_out);
         case 8192: return fir2_go<8192>(grid, s, rt, jobs, tables, hspec, x_in, y_out);
         case 16384: return fir2_go<16384>(grid, s, rt, jobs, tables, hspec, x_in, y_out);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+template <int M>
+static hipError_t fdl_go(unsigned grid, hipStream_t s, const PresetRt* rt, const int2* jobs, const float2* tables,
+                         const float2* hspec, float2* xspec, const float* x_in, float* y_out) {
+    hipLaunchKernelGGL((k_fdl_fwd<M>), dim3(grid), dim3(FirGeo<M>::T), FirGeo<M>::LDS_BYTES, s, rt, jobs, tables,
+                       x_in, xspec);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL((k_fdl_mac<M>), dim3(grid), dim3(FirGeo<M>::T), FirGeo<M>::LDS_BYTES, s, rt, jobs, tables,
+                       hspec, (const float2*)xspec, y_out);
+    return hipGetLastError();
+}
+
+hipError_t launch_fdl(int M, unsigned grid, hipStream_t s, const PresetRt* rt, const int2* jobs, const float2* tables,
+                      const float2* hspec, float2* xspec, const float* x_in, float* y_out) {
+    switch (M) {
+        case 8192: return fdl_go<8192>(grid, s, rt, jobs, tables, hspec, xspec, x_in, y_out);
+        case 16384: return fdl_go<16384>(grid, s, rt, jobs, tables, hspec, xspec, x_in, y_out);
         default: return hipErrorInvalidValue;
     }
 }

@@ -41,6 +41,9 @@ hipError_t launch_fir_h(unsigned grid, int lds_bytes, hipStream_t s, const Prese
                         const float* hs, float2* hspec);
 // register-resident FIR with compile-time transform size M = N/2 in {1024..16384}
 bool fir2_tables_host(int M, std::vector<float>& out);
+// frequency-domain delay line (msg_fir with many partitions): segment spectra, then MAC + inverse
+hipError_t launch_fdl(int M, unsigned grid, hipStream_t s, const PresetRt* rt, const int2* jobs, const float2* tables,
+                      const float2* hspec, float2* xspec, const float* x_in, float* y_out);
 hipError_t launch_fir2(int M, unsigned grid, hipStream_t s, const PresetRt* rt, const int2* jobs,
                        const float2* tables, const float2* hspec, const float* x_in, float* y_out);
 

@@ -116,7 +116,7 @@ struct msg_ctx {
     DevBuf<int2> sf_jobs;
     DevBuf<int64_t> sf_irjobs;
     DevBuf<double> sf_h;
-    DevBuf<float2> sf_hspec;
+    DevBuf<float2> sf_hspec, sf_xspec;
     // odd-length stereo rotation (kernels_stereo_odd.h)
     std::map<int64_t, DevBuf<float2>> so_bp;   // chirp kernel spectra by n
     DevBuf<float2> so_A;
@@ -469,7 +469,7 @@ void msg_destroy(msg_ctx* ctx) {
     ctx->spec_ct_list.release();
     ctx->fir_jobs.release();
     ctx->sf_prt.release(); ctx->sf_jobs.release(); ctx->sf_irjobs.release(); ctx->sf_h.release();
-    ctx->sf_hspec.release();
+    ctx->sf_hspec.release(); ctx->sf_xspec.release();
     for (auto& ev : ctx->ev) hipEventDestroy(ev);
     ctx->presets.release(); ctx->frag_len.release(); ctx->info.release(); ctx->slot_base.release();
     ctx->tap_base.release(); ctx->events.release(); ctx->er_off.release(); ctx->er_gain.release();
@@ -721,7 +721,19 @@ int msg_fir(msg_ctx* ctx, const float* x_dev, float* y_dev, int64_t n, int32_t n
     hipStream_t s = (hipStream_t)stream;
     int N = 0, Pp = 0, Q = 0;
     choose_fir(M, n, 0, N, Pp, Q);
-    const int64_t B = N - Pp + 1;
+    // Many partitions: a frequency-domain delay line (fir_fft.h) computes each
+    // input segment's spectrum once and reuses it for Q blocks -- two transforms
+    // per block of N/2 outputs instead of Q + 1 per block of N - P + 1, for
+    // 8 B/output of spectrum writes and 8 Q B/output of reads.  Measured on
+    // MI355X: slower at 64 k taps (classic Q = 5: 7.1 ms vs 7.7 ms per 1024
+    // signals), so it takes over only from Q = 8 (>= ~115 k taps).
+    const bool fdl = Q >= 8;
+    if (fdl) {
+        N = FIR_NMAX;
+        Pp = N / 2;
+        Q = (int)((M + Pp - 1) / Pp);
+    }
+    const int64_t B = fdl ? Pp : N - Pp + 1;
     const int64_t blocks = (n + B - 1) / B;
     if (blocks * n_signals > INT32_MAX) return fail(ctx, MSG_E_UNSUPPORTED, "too many output blocks");
     if (fir_shape) { fir_shape[0] = N; fir_shape[1] = Pp; fir_shape[2] = Q; }
@@ -745,6 +757,7 @@ int msg_fir(msg_ctx* ctx, const float* x_dev, float* y_dev, int64_t n, int32_t n
         r.y_off = (int64_t)i * n;
         r.fir_on = 1; r.fir_N = N; r.fir_P = Pp; r.fir_Q = Q; r.fir_B = (int32_t)B;
         r.h_off = 0;
+        r.fir_block_begin = (int32_t)(i * blocks);     // FDL: first segment spectrum of this signal
         for (int64_t b = 0; b < blocks; ++b) fj.push_back(make_int2(i, (int)b));
     }
     HIPCHK(ctx, ctx->sf_prt.ensure(prt.size()));
@@ -752,6 +765,7 @@ int msg_fir(msg_ctx* ctx, const float* x_dev, float* y_dev, int64_t n, int32_t n
     HIPCHK(ctx, ctx->sf_irjobs.ensure(jobs.size()));
     HIPCHK(ctx, ctx->sf_h.ensure((size_t)M));
     HIPCHK(ctx, ctx->sf_hspec.ensure((size_t)Q * K));
+    if (fdl) HIPCHK(ctx, ctx->sf_xspec.ensure((size_t)fj.size() * K));
     HIPCHK(ctx, hipMemcpyAsync(ctx->sf_prt.p, prt.data(), sizeof(PresetRt) * prt.size(), hipMemcpyHostToDevice, s));
     HIPCHK(ctx, hipMemcpyAsync(ctx->sf_jobs.p, fj.data(), sizeof(int2) * fj.size(), hipMemcpyHostToDevice, s));
     HIPCHK(ctx, hipMemcpyAsync(ctx->sf_irjobs.p, jobs.data(), sizeof(int64_t) * jobs.size(), hipMemcpyHostToDevice,
@@ -761,8 +775,12 @@ int msg_fir(msg_ctx* ctx, const float* x_dev, float* y_dev, int64_t n, int32_t n
                                ctx->fir_plans.dev.p, ctx->sf_h.p, ctx->sf_hspec.p));
     int ti = 0;
     while ((1024 << ti) != N / 2) ++ti;
-    HIPCHK(ctx, launch_fir2(N / 2, (unsigned)fj.size(), s, ctx->sf_prt.p, ctx->sf_jobs.p, ctx->d_fir2tab[ti],
-                            ctx->sf_hspec.p, x_dev, y_dev));
+    if (fdl)
+        HIPCHK(ctx, launch_fdl(N / 2, (unsigned)fj.size(), s, ctx->sf_prt.p, ctx->sf_jobs.p, ctx->d_fir2tab[ti],
+                               ctx->sf_hspec.p, ctx->sf_xspec.p, x_dev, y_dev));
+    else
+        HIPCHK(ctx, launch_fir2(N / 2, (unsigned)fj.size(), s, ctx->sf_prt.p, ctx->sf_jobs.p, ctx->d_fir2tab[ti],
+                                ctx->sf_hspec.p, x_dev, y_dev));
     // pageable-host H2D copies are staged before hipMemcpyAsync returns (as in
     // msg_render_batch), so the host vectors may go; the FIR runs asynchronously.
     return MSG_OK;

@@ -30,7 +30,8 @@ def test_fftconvolve_matches_oracle():
     np.testing.assert_allclose(_ref(x, h), O.fir_causal(x, h), rtol=0, atol=1e-9)
 
 
-@pytest.mark.parametrize("M,n,S", [(16384, 60000, 3), (65536, 200000, 2), (8192, 384000, 1)])
+@pytest.mark.parametrize("M,n,S", [(16384, 60000, 3), (65536, 200000, 2), (8192, 384000, 1),
+                                   (262144, 300000, 2)])   # the last: frequency-domain delay line
 def test_fir_long_taps(M, n, S):
     import torch
     from msgpu.engine import default_engine
@@ -41,6 +42,8 @@ def test_fir_long_taps(M, n, S):
     y, (N, P, Q) = eng.fir(torch.from_numpy(x).cuda(), h)
     torch.cuda.synchronize()
     assert P * Q >= M and N <= 32768
+    if M >= 200000:
+        assert P == N // 2            # the frequency-domain delay line path
     y = y.cpu().numpy()
     for b in range(S):
         assert _rel_rms(y[b], _ref(x[b], h)) <= REL, (b, N, P, Q)

@@ -29,7 +29,7 @@ def main():
     ap.add_argument("--n", type=int, default=384000)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--taps", default="16384,65536")
+    ap.add_argument("--taps", default="16384,65536,262144")
     ap.add_argument("--cpu", action="store_true")
     a = ap.parse_args()
     import torch
