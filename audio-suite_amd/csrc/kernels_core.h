@@ -326,21 +326,35 @@ k_ola_env(const msg_event* __restrict__ events, const PresetRt* __restrict__ rt,
         }
         const uint64_t live = __ballot(s < t1);           // sorted: a prefix of the lanes
         const int cnt = __popcll(live);
-        for (int i = 0; i < cnt; ++i) {
-            const int si = __builtin_amdgcn_readlane(s, i);
-            const int Li = __builtin_amdgcn_readlane(L, i);
-            if (Li <= 0 || (int64_t)si + Li <= t0) continue;
-            const float ai = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(amp), i));
-            const int64_t gi = ((int64_t)__builtin_amdgcn_readlane((int)(goff >> 32), i) << 32) |
-                               (uint32_t)__builtin_amdgcn_readlane((int)goff, i);
-            const float* g = grain_pool + gi;
-            const int q0 = (int)t0 - si + (int)threadIdx.x;
+        // two events per iteration: both grains' loads are in flight before the
+        // first multiply-add (accumulation stays in event order)
+        for (int i = 0; i < cnt; i += 2) {
+            float gv[2][PER];
+            bool take[2][PER];
+            float av[2];
 #pragma unroll
-            for (int u = 0; u < PER; ++u) {
-                const int q = q0 + u * OLA_T;
-                if (u * OLA_T + (int)threadIdx.x < (int)(t1 - t0) && q >= 0 && q < Li)
-                    acc[u] = fmaf(ai, g[q], acc[u]);
+            for (int h = 0; h < 2; ++h) {
+                const int ii = i + h < cnt ? i + h : i;
+                const int si = __builtin_amdgcn_readlane(s, ii);
+                const int Li = (i + h < cnt) ? __builtin_amdgcn_readlane(L, ii) : 0;
+                av[h] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(amp), ii));
+                const int64_t gi = ((int64_t)__builtin_amdgcn_readlane((int)(goff >> 32), ii) << 32) |
+                                   (uint32_t)__builtin_amdgcn_readlane((int)goff, ii);
+                const float* g = grain_pool + gi;
+                const bool ev_on = Li > 0 && (int64_t)si + Li > t0;
+                const int q0 = (int)t0 - si + (int)threadIdx.x;
+#pragma unroll
+                for (int u = 0; u < PER; ++u) {
+                    const int q = q0 + u * OLA_T;
+                    take[h][u] = ev_on && u * OLA_T + (int)threadIdx.x < (int)(t1 - t0) && q >= 0 && q < Li;
+                    gv[h][u] = take[h][u] ? g[q] : 0.f;
+                }
             }
+#pragma unroll
+            for (int h = 0; h < 2; ++h)
+#pragma unroll
+                for (int u = 0; u < PER; ++u)
+                    if (take[h][u]) acc[u] = fmaf(av[h], gv[h][u], acc[u]);
         }
         if (cnt < 64) break;
     }
