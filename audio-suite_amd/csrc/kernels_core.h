@@ -391,10 +391,12 @@ MSG_DEV int mod_n(int64_t i, int64_t n) {
     return (int)(i < 0 ? i + n : i);
 }
 
-// Stage len floats y[(b0 + u) mod n] into w[0 .. len) (coalesced, all loads in flight).
+// Stage len floats y[(b0 + u) mod n] into w[0 .. len): coalesced loads into
+// registers (stereo_load), then LDS stores (stereo_store), split so that a
+// kernel can have every global load of its tile in flight before the first
+// store waits on them.
 template <int PER>
-MSG_DEV void stereo_window(const float* __restrict__ y, int n, int b0, int len, float* w) {
-    float v[PER];
+MSG_DEV void stereo_load(const float* __restrict__ y, int n, int b0, int len, float (&v)[PER]) {
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
         const int u = threadIdx.x + i * ST_T;
@@ -403,6 +405,9 @@ MSG_DEV void stereo_window(const float* __restrict__ y, int n, int b0, int len, 
         else j %= n;
         v[i] = u < len ? y[j] : 0.f;
     }
+}
+template <int PER>
+MSG_DEV void stereo_store(int len, const float (&v)[PER], float* w) {
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
         const int u = threadIdx.x + i * ST_T;
@@ -449,7 +454,6 @@ k_stereo_max(const PresetRt* __restrict__ rt, const int32_t* __restrict__ st_beg
     const float* y = ybuf + r.y_off;
     const int n = (int)r.out_n;
     const StereoTile st = stereo_tile(r, (int64_t)(b - st_begin[p]) * ST_TILE);
-    if (r.stereo_fir == 1) stereo_window<ST_WPER>(y, n, mod_n((int64_t)st.t0 + r.dr - 24, n), ST_WIN, w);
     // max|L| over all frames equals max|y| (L is a rotation of y): read y directly
     // (y regions are 16-byte aligned and t0 is a multiple of ST_TILE)
     float4 yv[ST_RUNS];
@@ -464,6 +468,11 @@ k_stereo_max(const PresetRt* __restrict__ rt, const int32_t* __restrict__ st_beg
             yv[i].z = u + 2 < st.cnt ? y[st.t0 + u + 2] : 0.f;
             yv[i].w = 0.f;
         }
+    }
+    if (r.stereo_fir == 1) {
+        float wv[ST_WPER];
+        stereo_load<ST_WPER>(y, n, mod_n((int64_t)st.t0 + r.dr - 24, n), ST_WIN, wv);
+        stereo_store<ST_WPER>(ST_WIN, wv, w);
     }
     __syncthreads();
     float m = 0.f;
@@ -520,8 +529,13 @@ k_stereo_out(const PresetRt* __restrict__ rt, const int32_t* __restrict__ st_beg
     const float* y = ybuf + r.y_off;
     const int n = (int)r.out_n;
     const StereoTile st = stereo_tile(r, (int64_t)(b - st_begin[p]) * ST_TILE);
-    if (r.stereo_fir == 1) stereo_window<ST_WPER>(y, n, mod_n((int64_t)st.t0 + r.dr - 24, n), ST_WIN, w);
-    stereo_window<ST_LPER>(y, n, r.stereo_fir ? st.lbase : st.t0, st.cnt, lw);
+    {
+        float lv[ST_LPER], wv[ST_WPER];
+        stereo_load<ST_LPER>(y, n, r.stereo_fir ? st.lbase : st.t0, st.cnt, lv);
+        if (r.stereo_fir == 1) stereo_load<ST_WPER>(y, n, mod_n((int64_t)st.t0 + r.dr - 24, n), ST_WIN, wv);
+        stereo_store<ST_LPER>(st.cnt, lv, lw);
+        if (r.stereo_fir == 1) stereo_store<ST_WPER>(ST_WIN, wv, w);
+    }
     const float d = r.drive;
     const float inv_td = d > 0.f ? 1.0f / tanh_fast(d) : 1.f;
     const float M = __uint_as_float(maxbits[p]);
