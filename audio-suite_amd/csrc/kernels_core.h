@@ -425,9 +425,8 @@ MSG_DEV StereoTile stereo_tile(const PresetRt& r, int64_t t0) {
 }
 
 // R[u + k] = sum_m J_m w[u + k + 2m], k < 4, u a multiple of 4 (same fma order as the
-// reference-checked scalar form: m = 0 .. 24).
-MSG_DEV void stereo_r4(const PresetRt& r, const float* w, int u, float (&R)[4]) {
-    float x[52];
+// reference-checked scalar form: m = 0 .. 24); x receives w[u .. u + 52).
+MSG_DEV void stereo_r4(const PresetRt& r, const float* w, int u, float (&R)[4], float (&x)[52]) {
     const float4* w4 = reinterpret_cast<const float4*>(w + u);
 #pragma unroll
     for (int i = 0; i < 13; ++i) {
@@ -454,39 +453,47 @@ k_stereo_max(const PresetRt* __restrict__ rt, const int32_t* __restrict__ st_beg
     const float* y = ybuf + r.y_off;
     const int n = (int)r.out_n;
     const StereoTile st = stereo_tile(r, (int64_t)(b - st_begin[p]) * ST_TILE);
-    // max|L| over all frames equals max|y| (L is a rotation of y): read y directly
-    // (y regions are 16-byte aligned and t0 is a multiple of ST_TILE)
+    // max|L| over all frames equals max|y| (L is a rotation of y).  With the
+    // Bessel FIR, the centre tap of output u + k is y[(t0 + u + k + dr) mod n]:
+    // over all tiles those cover every sample once, so max|y| comes from the
+    // staged window; otherwise read y directly (16-byte aligned regions, t0 a
+    // multiple of ST_TILE).
+    const bool fir = r.stereo_fir == 1;
     float4 yv[ST_RUNS];
-#pragma unroll
-    for (int i = 0; i < ST_RUNS; ++i) {
-        const int u = 4 * (threadIdx.x + i * ST_T);
-        if (u + 4 <= st.cnt) {
-            yv[i] = *reinterpret_cast<const float4*>(y + st.t0 + u);
-        } else {
-            yv[i].x = u < st.cnt ? y[st.t0 + u] : 0.f;
-            yv[i].y = u + 1 < st.cnt ? y[st.t0 + u + 1] : 0.f;
-            yv[i].z = u + 2 < st.cnt ? y[st.t0 + u + 2] : 0.f;
-            yv[i].w = 0.f;
-        }
-    }
-    if (r.stereo_fir == 1) {
+    if (fir) {
         float wv[ST_WPER];
         stereo_load<ST_WPER>(y, n, mod_n((int64_t)st.t0 + r.dr - 24, n), ST_WIN, wv);
         stereo_store<ST_WPER>(ST_WIN, wv, w);
+    } else {
+#pragma unroll
+        for (int i = 0; i < ST_RUNS; ++i) {
+            const int u = 4 * (threadIdx.x + i * ST_T);
+            if (u + 4 <= st.cnt) {
+                yv[i] = *reinterpret_cast<const float4*>(y + st.t0 + u);
+            } else {
+                yv[i].x = u < st.cnt ? y[st.t0 + u] : 0.f;
+                yv[i].y = u + 1 < st.cnt ? y[st.t0 + u + 1] : 0.f;
+                yv[i].z = u + 2 < st.cnt ? y[st.t0 + u + 2] : 0.f;
+                yv[i].w = 0.f;
+            }
+        }
     }
     __syncthreads();
     float m = 0.f;
 #pragma unroll
     for (int i = 0; i < ST_RUNS; ++i) {
         const int u = 4 * (threadIdx.x + i * ST_T);
-        m = fmaxf(m, fmaxf(fmaxf(fabsf(yv[i].x), fabsf(yv[i].y)), fmaxf(fabsf(yv[i].z), fabsf(yv[i].w))));
-        if (r.stereo_fir == 1 && u < st.cnt) {
-            float R[4];
-            stereo_r4(r, w, u, R);
+        if (fir) {
+            if (u < st.cnt) {
+                float R[4], x[52];
+                stereo_r4(r, w, u, R, x);
 #pragma unroll
-            for (int k = 0; k < 4; ++k)
-                if (u + k < st.cnt) m = fmaxf(m, fabsf(R[k]));
+                for (int k = 0; k < 4; ++k)
+                    if (u + k < st.cnt) m = fmaxf(m, fmaxf(fabsf(R[k]), fabsf(x[k + 24])));
+            }
+            continue;
         }
+        m = fmaxf(m, fmaxf(fmaxf(fabsf(yv[i].x), fabsf(yv[i].y)), fmaxf(fabsf(yv[i].z), fabsf(yv[i].w))));
         if (r.stereo_fir == 2) {
 #pragma unroll
             for (int k = 0; k < 4; ++k)
@@ -552,7 +559,8 @@ k_stereo_out(const PresetRt* __restrict__ rt, const int32_t* __restrict__ st_beg
         const float L[4] = {l4.x, l4.y, l4.z, l4.w};
         float R[4];
         if (r.stereo_fir == 1) {
-            stereo_r4(r, w, u, R);
+            float x[52];
+            stereo_r4(r, w, u, R, x);
         } else {
 #pragma unroll
             for (int k = 0; k < 4; ++k)
