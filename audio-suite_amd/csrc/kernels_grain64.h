@@ -1,4 +1,5 @@
-// kernels_grain64.h — the float64 grain chain (TU: k_grain64.hip).
+// kernels_grain64.h — the float64 grain chain (TUs: k_grain64_lds.hip and
+// k_grain64_glb.hip for k_grain64<false/true>, k_grain64.hip for the rest).
 //
 // Presets that use a stage whose reference result hinges on float64 decisions
 // or float64 noise floors run every event through this chain instead of the
@@ -799,29 +800,6 @@ k_chain64(const msg_preset* __restrict__ presets, const Ev64* __restrict__ ev64,
     }   // chains
 }
 #endif  // __HIPCC__
-
-#if defined(__HIPCC__)
-// Single float64 real transform (tests / precision probes): inverse = 0 ->
-// io[0..n) real in, io[0..2K) = X[0..K) out; inverse = 1 -> X in, real out.
-__global__ void __launch_bounds__(G64_T)
-k_fft64_one(const Real64Plan* __restrict__ plans, int plan, int inverse, double* __restrict__ io,
-            double2* gA, double2* gB) {
-    extern __shared__ __attribute__((aligned(16))) double2 lds_buf[];
-    double2* buf = gA ? gA : lds_buf;      // global buffers: the engine's ping-pong mode
-    double2* scr = gA ? gB : nullptr;
-    const Real64Plan& rp = plans[plan];
-    const int n = rp.n, K = n / 2 + 1;
-    double* d = reinterpret_cast<double*>(buf);
-    const int cnt = inverse ? 2 * K : n;
-    for (int j = threadIdx.x; j < cnt; j += G64_T) d[j] = io[j];
-    __syncthreads();
-    if (inverse) f64_irfft<G64_T, G64_MAXE>(buf, rp, scr);
-    else f64_rfft<G64_T, G64_MAXE>(buf, rp, scr);
-    __syncthreads();
-    const int cnt2 = inverse ? n : 2 * K;
-    for (int j = threadIdx.x; j < cnt2; j += G64_T) io[j] = d[j];
-}
-#endif
 
 #if defined(__HIPCC__)
 // ---------------------------------------------------------------------------

@@ -61,6 +61,17 @@ struct G64Global {
     int64_t slot_cap, mask_words;
 };
 void grain64_init_attrs();
+// the two k_grain64 instantiations live in their own TUs (k_grain64_lds.hip,
+// k_grain64_glb.hip) so they compile in parallel; launch_grain64 picks one
+void grain64_lds_init_attr();
+hipError_t launch_grain64_lds(unsigned grid, int lds_bytes, hipStream_t s, const msg_preset* presets,
+                              const Ev64* ev64, const PresetRt* rt, const Real64Plan* plans, const int32_t* list,
+                              int n_list, const double* irbank, const uint8_t* imgbank, nprng::Zig z,
+                              double* micro64, double* grain64, double2* save, float* grain_pool);
+hipError_t launch_grain64_glb(const G64Global& g, unsigned grid, hipStream_t s, const msg_preset* presets,
+                              const Ev64* ev64, const PresetRt* rt, const Real64Plan* plans, const int32_t* list,
+                              int n_list, const double* irbank, const uint8_t* imgbank, nprng::Zig z,
+                              double* micro64, double* grain64, double2* save, float* grain_pool);
 hipError_t launch_grain64(const G64Global* g, unsigned grid, int lds_bytes, hipStream_t s, const msg_preset* presets,
                           const Ev64* ev64, const PresetRt* rt, const Real64Plan* plans, const int32_t* list,
                           int n_list, const double* irbank, const uint8_t* imgbank, nprng::Zig z, double* micro64,
