@@ -101,7 +101,10 @@ constexpr int GEN_T = 64;          // one wave per event
 constexpr int OLA_T = 256;
 constexpr int OLA_TILE = 4096;
 constexpr int ST_T = 256;
-constexpr int ST_TILE = 4096;
+#ifndef MSG_ST_TILE
+#define MSG_ST_TILE 4096           // tuning builds override (build.py --exp)
+#endif
+constexpr int ST_TILE = MSG_ST_TILE;
 
 // shared helpers
 //
