@@ -6,6 +6,14 @@
 --stamps builds msgpu/libmsgpu_stamps.so with per-phase clock stamps in the
 spectral kernel (-DMSG_STAMPS, read by tools/spec_stamps.py); load it with
 MSGPU_LIB=.../libmsgpu_stamps.so.  Never the product library.
+
+--exp builds msgpu/libmsgpu_exp.so for tuning experiments with the extra defines
+in MSGPU_EXP_DEFS (e.g. MSGPU_EXP_DEFS="-DMSG_ST_TILE=2048"); load it with
+MSGPU_LIB=.../libmsgpu_exp.so.  Never the product library.
+
+Objects are cached per variant and rebuilt when a source or local header is
+newer, or when the variant's defines differ from those recorded in the object
+directory's defs stamp (so changing MSGPU_EXP_DEFS always recompiles).
 """
 import concurrent.futures as cf
 import os
@@ -51,6 +59,27 @@ VARIANTS = {"": ([], "build", "libmsgpu.so"), "stamps": (["-DMSG_STAMPS"], "buil
             "exp": (os.environ.get("MSGPU_EXP_DEFS", "").split(), "build_exp", "libmsgpu_exp.so")}
 
 
+def _defs_stamp(variant):
+    """Drop the variant's cached objects when its defines changed since they were
+    built (the stamp file records the defines and flags of the objects)."""
+    defs, objdir, _ = VARIANTS[variant]
+    d = os.path.join(HERE, objdir)
+    stamp = os.path.join(d, "defs.stamp")
+    want = " ".join(FLAGS + defs)
+    try:
+        with open(stamp) as f:
+            have = f.read()
+    except OSError:
+        have = None
+    if have != want:
+        for tu in TUS:
+            o = os.path.join(d, tu.replace(".hip", ".o"))
+            if os.path.exists(o):
+                os.remove(o)
+        with open(stamp, "w") as f:
+            f.write(want)
+
+
 def _compile(tu, variant=""):
     defs, objdir, _ = VARIANTS[variant]
     src = os.path.join(CSRC, tu)
@@ -73,6 +102,7 @@ def build(force: bool = False, variant: str = "") -> str:
             o = os.path.join(HERE, objdir, tu.replace(".hip", ".o"))
             if os.path.exists(o):
                 os.remove(o)
+    _defs_stamp(variant)
     with cf.ThreadPoolExecutor(max_workers=len(TUS)) as ex:
         objs = list(ex.map(lambda tu: _compile(tu, variant), TUS))
     OUT = out

@@ -4,6 +4,11 @@
 #include "kernels_grain64.h"
 #include "launch.h"
 
+// launch.h keeps host copies of the float64 engine's shape for the planner
+static_assert(G64_THREADS == G64_T, "launch.h G64_THREADS must match kernels_grain64.h G64_T");
+static_assert(G64_SLOTS == G64_CAP, "launch.h G64_SLOTS must match kernels_grain64.h G64_CAP");
+static_assert(G64_MAXPAR_HOST == G64_MAXPAR, "launch.h G64_MAXPAR_HOST must match kernels_grain64.h G64_MAXPAR");
+
 // Single float64 real transform (tests / precision probes): inverse = 0 ->
 // io[0..n) real in, io[0..2K) = X[0..K) out; inverse = 1 -> X in, real out.
 __global__ void __launch_bounds__(G64_T)

@@ -377,6 +377,9 @@ k_ola_env(const msg_event* __restrict__ events, const PresetRt* __restrict__ rt,
 // window instead of 100 scalar reads (the kernels were LDS-issue bound).
 // L[t] = y[(t - dl) mod n] is staged the same way in k_stereo_out.
 constexpr int ST_RUNS = ST_TILE / (4 * ST_T);     // runs of 4 frames per thread
+static_assert(ST_TILE >= 4 * ST_T && ST_TILE % (4 * ST_T) == 0,
+              "MSG_ST_TILE must be a multiple of 4 * ST_T (every frame of a tile has a run)");
+static_assert((2 * ST_TILE + 48) * 4 <= 160 * 1024, "MSG_ST_TILE: stereo tile window exceeds the 160 KiB LDS of a CU");
 constexpr int ST_WIN = ST_TILE + 48;
 constexpr int ST_WPER = (ST_WIN + ST_T - 1) / ST_T;
 constexpr int ST_LPER = ST_TILE / ST_T;

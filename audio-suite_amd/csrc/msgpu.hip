@@ -11,9 +11,13 @@
 #include <cstdio>
 #include <cstring>
 #include <map>
+#include <atomic>
+#include <condition_variable>
+#include <functional>
 #include <memory>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "msg_common.h"
@@ -50,6 +54,135 @@ struct DevBuf {
     void release() { if (p) hipFree(p); p = nullptr; cap = 0; }
 };
 
+// Host worker pool for the per-preset planning of a batch (plan.h on the CPU).
+// One process-wide pool; the caller takes part in the work.  A call that finds
+// the pool busy (another thread rendering) runs its loop inline.
+class HostPool {
+  public:
+    static HostPool& get() {
+        static HostPool pool;
+        return pool;
+    }
+    template <class F>
+    void run(int count, F&& f) {
+        if (count <= 0) return;
+        std::unique_lock<std::mutex> busy(busy_, std::try_to_lock);
+        if (!busy.owns_lock() || workers_.empty() || count < 2) {
+            for (int i = 0; i < count; ++i) f(i);
+            return;
+        }
+        std::function<void(int)> fn(std::ref(f));
+        {
+            std::lock_guard<std::mutex> lk(m_);
+            job_ = &fn;
+            count_ = count;
+            next_.store(0);
+            running_ = (int)workers_.size();
+            ++gen_;
+        }
+        cv_.notify_all();
+        drain(fn);
+        std::unique_lock<std::mutex> lk(m_);
+        done_cv_.wait(lk, [&] { return running_ == 0; });
+        job_ = nullptr;
+    }
+    ~HostPool() {
+        {
+            std::lock_guard<std::mutex> lk(m_);
+            stop_ = true;
+            ++gen_;
+        }
+        cv_.notify_all();
+        for (auto& t : workers_) t.join();
+    }
+
+  private:
+    HostPool() {
+        int n = 8;
+        if (const char* e = getenv("MSGPU_HOST_THREADS")) n = atoi(e);
+        const int hw = (int)std::thread::hardware_concurrency();
+        if (hw > 0) n = std::min(n, hw);
+        for (int i = 0; i + 1 < n; ++i) workers_.emplace_back([this] { loop(); });
+    }
+    void drain(const std::function<void(int)>& fn) {
+        for (int i = next_.fetch_add(1); i < count_; i = next_.fetch_add(1)) fn(i);
+    }
+    void loop() {
+        uint64_t seen = 0;
+        for (;;) {
+            const std::function<void(int)>* fn;
+            {
+                std::unique_lock<std::mutex> lk(m_);
+                cv_.wait(lk, [&] { return stop_ || gen_ != seen; });
+                if (stop_) return;
+                seen = gen_;
+                fn = job_;
+            }
+            drain(*fn);
+            std::lock_guard<std::mutex> lk(m_);
+            if (--running_ == 0) done_cv_.notify_all();
+        }
+    }
+    std::vector<std::thread> workers_;
+    std::mutex busy_, m_;
+    std::condition_variable cv_, done_cv_;
+    const std::function<void(int)>* job_ = nullptr;
+    std::atomic<int> next_{0};
+    int count_ = 0, running_ = 0;
+    uint64_t gen_ = 0;
+    bool stop_ = false;
+};
+
+// Pinned staging for a batch's host -> device uploads.  Two slots alternate
+// between batches; a slot is refilled only after the copies that read it (two
+// batches back) have run, so msg_render_batch never waits on the render
+// stream and every copy is a true asynchronous DMA from pinned memory.
+struct Staging {
+    struct Item { void* dst; const void* src; size_t bytes; };
+    struct Slot { char* host = nullptr; size_t cap = 0; hipEvent_t done = nullptr; bool armed = false; };
+    Slot slot[2];
+    int cur = 0;
+    std::vector<Item> items;
+    void add(void* dst, const void* src, size_t bytes) {
+        if (bytes) items.push_back(Item{dst, src, bytes});
+    }
+    hipError_t flush(hipStream_t s) {
+        Slot& sl = slot[cur];
+        hipError_t e = hipSuccess;
+        if (!sl.done) e = hipEventCreateWithFlags(&sl.done, hipEventDisableTiming);
+        if (e == hipSuccess && sl.armed) e = hipEventSynchronize(sl.done);
+        size_t total = 0;
+        for (const Item& it : items) total += (it.bytes + 255) & ~size_t(255);
+        if (e == hipSuccess && total > sl.cap) {
+            if (sl.host) hipHostFree(sl.host);
+            sl.host = nullptr;
+            sl.cap = 0;
+            const size_t want = total + total / 4 + 4096;
+            e = hipHostMalloc((void**)&sl.host, want, hipHostMallocDefault);
+            if (e == hipSuccess) sl.cap = want;
+        }
+        size_t off = 0;
+        for (const Item& it : items) {
+            if (e != hipSuccess) break;
+            std::memcpy(sl.host + off, it.src, it.bytes);
+            e = hipMemcpyAsync(it.dst, sl.host + off, it.bytes, hipMemcpyHostToDevice, s);
+            off += (it.bytes + 255) & ~size_t(255);
+        }
+        if (e == hipSuccess) e = hipEventRecord(sl.done, s);
+        sl.armed = e == hipSuccess;
+        items.clear();
+        cur ^= 1;
+        return e;
+    }
+    void release() {
+        for (Slot& sl : slot) {
+            if (sl.done) { hipEventSynchronize(sl.done); hipEventDestroy(sl.done); }
+            if (sl.host) hipHostFree(sl.host);
+            sl = Slot();
+        }
+    }
+};
+
 template <class P>
 struct PlanStoreT {
     std::vector<P> host;                 // descriptors (device pointers inside)
@@ -67,11 +200,17 @@ struct msg_ctx {
     int device = 0;
     std::string err;
     bool profiling = false;
-    bool pending = false;         // events of the last profiled batch not yet read
-    bool pending_fir = false;
+    // stage events: two sets alternate between batches; a set is read (folded
+    // into the sums) when it comes round again, two batches later, or at
+    // msg_stage_times -- profiling never makes the host wait for the last batch
+    bool pending[2] = {false, false};
+    bool pending_fir[2] = {false, false};
+    int ev_cur = 0;
     double stage_sum[10] = {0};   // accumulated stage times since msg_set_profiling(ctx, 1)
     int64_t stage_cnt = 0;
-    hipEvent_t ev[10] = {};
+    hipEvent_t ev[2][10] = {};
+    bool device_plan = false;     // MSGPU_DEVICE_PLAN=1: plan on the device (k_plan_*), read back
+    Staging staging;              // pinned uploads of a batch
     // constant tables
     uint64_t* d_ki = nullptr; double* d_wi = nullptr; double* d_fi = nullptr;
     uint64_t* d_ke = nullptr; double* d_we = nullptr; double* d_fe = nullptr;
@@ -124,6 +263,8 @@ struct msg_ctx {
     // host mirrors of the last batch
     std::vector<msg_plan_info> h_info;
     std::vector<msg_event> h_events;
+    std::vector<int32_t> h_er_off;
+    std::vector<double> h_er_gain;
     std::vector<PresetRt> h_prt;
     std::vector<int32_t> h_slot_base;
     std::vector<Ev64> h_ev64;
@@ -377,7 +518,7 @@ static int g64_ops(const msg_preset& p, const msg_event& e) {
 }
 
 static void stage_mark(msg_ctx* ctx, int i, hipStream_t s) {
-    if (ctx->profiling) hipEventRecord(ctx->ev[i], s);
+    if (ctx->profiling) hipEventRecord(ctx->ev[ctx->ev_cur][i], s);
 }
 
 // ---------------------------------------------------------------------------
@@ -444,7 +585,9 @@ msg_ctx* msg_create(int device_ordinal) {
             return nullptr;
         }
     }
-    for (auto& ev : ctx->ev) hipEventCreate(&ev);
+    for (auto& set : ctx->ev)
+        for (auto& ev : set) hipEventCreate(&ev);
+    if (const char* e = getenv("MSGPU_DEVICE_PLAN")) ctx->device_plan = e[0] == '1';
     spectral_ct_init_attrs();
     spectral_init_attrs();
     fir_init_attrs();
@@ -470,7 +613,9 @@ void msg_destroy(msg_ctx* ctx) {
     ctx->fir_jobs.release();
     ctx->sf_prt.release(); ctx->sf_jobs.release(); ctx->sf_irjobs.release(); ctx->sf_h.release();
     ctx->sf_hspec.release(); ctx->sf_xspec.release();
-    for (auto& ev : ctx->ev) hipEventDestroy(ev);
+    for (auto& set : ctx->ev)
+        for (auto& ev : set) hipEventDestroy(ev);
+    ctx->staging.release();
     ctx->presets.release(); ctx->frag_len.release(); ctx->info.release(); ctx->slot_base.release();
     ctx->tap_base.release(); ctx->events.release(); ctx->er_off.release(); ctx->er_gain.release();
     ctx->ert.release(); ctx->prt.release(); ctx->gen_list.release(); ctx->spec_small.release();
@@ -494,19 +639,25 @@ void msg_destroy(msg_ctx* ctx) {
 // Fold the event times of the last profiled batch into the running sums.
 // The events are read lazily (here, at the next batch of the same context or
 // at msg_stage_times) so profiling never blocks the host between batches.
-static void collect_stage_times(msg_ctx* ctx) {
-    if (!ctx->pending) return;
-    hipEventSynchronize(ctx->ev[7]);
+static void collect_stage_set(msg_ctx* ctx, int k) {
+    if (!ctx->pending[k]) return;
+    hipEvent_t* ev = ctx->ev[k];
+    hipEventSynchronize(ev[7]);
     float ms[10] = {0};
-    for (int i = 0; i < 7; ++i) hipEventElapsedTime(&ms[i], ctx->ev[i], ctx->ev[i + 1]);
-    hipEventElapsedTime(&ms[7], ctx->ev[0], ctx->ev[7]);
-    if (ctx->pending_fir) {   // the FIR kernel alone, and the h build before it
-        hipEventElapsedTime(&ms[8], ctx->ev[8], ctx->ev[9]);
-        hipEventElapsedTime(&ms[9], ctx->ev[5], ctx->ev[8]);
+    for (int i = 0; i < 7; ++i) hipEventElapsedTime(&ms[i], ev[i], ev[i + 1]);
+    hipEventElapsedTime(&ms[7], ev[0], ev[7]);
+    if (ctx->pending_fir[k]) {   // the FIR kernel alone, and the h build before it
+        hipEventElapsedTime(&ms[8], ev[8], ev[9]);
+        hipEventElapsedTime(&ms[9], ev[5], ev[8]);
     }
     for (int i = 0; i < 10; ++i) ctx->stage_sum[i] += ms[i];
     ++ctx->stage_cnt;
-    ctx->pending = false;
+    ctx->pending[k] = false;
+}
+// all sets (msg_stage_times / msg_set_profiling): waits for the profiled batches
+static void collect_stage_times(msg_ctx* ctx) {
+    collect_stage_set(ctx, ctx->ev_cur ^ 1);
+    collect_stage_set(ctx, ctx->ev_cur);
 }
 
 int msg_set_profiling(msg_ctx* ctx, int32_t on) {
@@ -843,7 +994,7 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
     if (!ctx || !presets || P <= 0 || !out_dev || !out_offsets) return fail(ctx, MSG_E_ARG, "bad arguments");
     hipStream_t s = (hipStream_t)stream;
     HIPCHK(ctx, hipSetDevice(ctx->device));
-    collect_stage_times(ctx);
+    collect_stage_set(ctx, ctx->ev_cur);   // this batch's event set: from two batches back
     for (int p = 0; p < P; ++p) {
         std::string why;
         if (!supported(presets[p], why)) return fail(ctx, MSG_E_UNSUPPORTED, "preset " + std::to_string(p) + ": " + why);
@@ -854,51 +1005,80 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
         if (ic >= n_irs || (ic >= 0 && !irs)) return fail(ctx, MSG_E_ARG, "bad IR index");
     }
     stage_mark(ctx, 0, s);
-    // ---- phase 1: sizes ----
     std::vector<int64_t> flen(P, 0);
     for (int p = 0; p < P; ++p) {
         const int f = presets[p].ir_frag;
         flen[p] = (f >= 0 && f < n_irs) ? ir_lens[f] : 0;
     }
     HIPCHK(ctx, ctx->presets.ensure(P));
-    HIPCHK(ctx, ctx->frag_len.ensure(P));
-    HIPCHK(ctx, ctx->info.ensure(P));
-    HIPCHK(ctx, hipMemcpyAsync(ctx->presets.p, presets, sizeof(msg_preset) * P, hipMemcpyHostToDevice, s));
-    HIPCHK(ctx, hipMemcpyAsync(ctx->frag_len.p, flen.data(), sizeof(int64_t) * P, hipMemcpyHostToDevice, s));
-    const int pb = 64;
-    hipLaunchKernelGGL(k_plan_sizes, dim3((P + pb - 1) / pb), dim3(pb), 0, s,
-                       ctx->presets.p, P, ctx->frag_len.p, ctx->dzig, ctx->info.p);
-    HIPCHK(ctx, hipGetLastError());
     std::vector<msg_plan_info> info(P);
-    HIPCHK(ctx, hipMemcpyAsync(info.data(), ctx->info.p, sizeof(msg_plan_info) * P, hipMemcpyDeviceToHost, s));
-    HIPCHK(ctx, hipStreamSynchronize(s));
-    // ---- phase 2: events + ER taps ----
     std::vector<int32_t> slot_base(P), tap_base(P);
     int64_t nslots = 0, ntaps = 0;
-    for (int p = 0; p < P; ++p) {
-        slot_base[p] = (int32_t)nslots;
-        tap_base[p] = (int32_t)ntaps;
-        nslots += info[p].n_slots;
-        if (presets[p].flags & MSG_F_ER_CLOUD) ntaps += std::max(1, presets[p].er_taps);
+    auto bases = [&]() -> int {
+        nslots = ntaps = 0;
+        for (int p = 0; p < P; ++p) {
+            slot_base[p] = (int32_t)nslots;
+            tap_base[p] = (int32_t)ntaps;
+            nslots += info[p].n_slots;
+            if (presets[p].flags & MSG_F_ER_CLOUD) ntaps += std::max(1, presets[p].er_taps);
+        }
+        if (nslots > INT32_MAX / 2) return fail(ctx, MSG_E_UNSUPPORTED, "too many events in one batch");
+        return MSG_OK;
+    };
+    if (!ctx->device_plan) {
+        // ---- host plan (plan.h, the device planner's code) on the host pool:
+        // no device round trip, so the call returns once the batch is enqueued
+        HostPool& pool = HostPool::get();
+        pool.run(P, [&](int p) { msgplan::plan_sizes(presets[p], kHostZig, flen[p], info[p]); });
+        if (int st = bases()) return st;
+        ctx->h_events.resize(nslots);
+        ctx->h_er_off.resize(ntaps);
+        ctx->h_er_gain.resize(ntaps);
+        pool.run(P, [&](int p) {
+            const bool er = (presets[p].flags & MSG_F_ER_CLOUD) != 0;
+            msgplan::plan_events(presets[p], kHostZig, flen[p], p, info[p], ctx->h_events.data() + slot_base[p],
+                                 er ? ctx->h_er_off.data() + tap_base[p] : nullptr,
+                                 er ? ctx->h_er_gain.data() + tap_base[p] : nullptr);
+        });
+        HIPCHK(ctx, ctx->events.ensure(nslots));
+        HIPCHK(ctx, ctx->er_off.ensure(ntaps));
+        HIPCHK(ctx, ctx->er_gain.ensure(ntaps));
+        ctx->staging.add(ctx->presets.p, presets, sizeof(msg_preset) * P);
+        ctx->staging.add(ctx->events.p, ctx->h_events.data(), sizeof(msg_event) * nslots);
+        ctx->staging.add(ctx->er_off.p, ctx->h_er_off.data(), sizeof(int32_t) * ntaps);
+        ctx->staging.add(ctx->er_gain.p, ctx->h_er_gain.data(), sizeof(double) * ntaps);
+    } else {
+        // ---- device plan, phase 1: sizes ----
+        HIPCHK(ctx, ctx->frag_len.ensure(P));
+        HIPCHK(ctx, ctx->info.ensure(P));
+        HIPCHK(ctx, hipMemcpyAsync(ctx->presets.p, presets, sizeof(msg_preset) * P, hipMemcpyHostToDevice, s));
+        HIPCHK(ctx, hipMemcpyAsync(ctx->frag_len.p, flen.data(), sizeof(int64_t) * P, hipMemcpyHostToDevice, s));
+        const int pb = 64;
+        hipLaunchKernelGGL(k_plan_sizes, dim3((P + pb - 1) / pb), dim3(pb), 0, s,
+                           ctx->presets.p, P, ctx->frag_len.p, ctx->dzig, ctx->info.p);
+        HIPCHK(ctx, hipGetLastError());
+        HIPCHK(ctx, hipMemcpyAsync(info.data(), ctx->info.p, sizeof(msg_plan_info) * P, hipMemcpyDeviceToHost, s));
+        HIPCHK(ctx, hipStreamSynchronize(s));
+        // ---- phase 2: events + ER taps ----
+        if (int st = bases()) return st;
+        HIPCHK(ctx, ctx->slot_base.ensure(P));
+        HIPCHK(ctx, ctx->tap_base.ensure(P));
+        HIPCHK(ctx, ctx->events.ensure(nslots));
+        HIPCHK(ctx, ctx->er_off.ensure(ntaps));
+        HIPCHK(ctx, ctx->er_gain.ensure(ntaps));
+        HIPCHK(ctx, hipMemcpyAsync(ctx->slot_base.p, slot_base.data(), sizeof(int32_t) * P, hipMemcpyHostToDevice, s));
+        HIPCHK(ctx, hipMemcpyAsync(ctx->tap_base.p, tap_base.data(), sizeof(int32_t) * P, hipMemcpyHostToDevice, s));
+        hipLaunchKernelGGL(k_plan_events, dim3((P + pb - 1) / pb), dim3(pb), 0, s,
+                           ctx->presets.p, P, ctx->frag_len.p, ctx->dzig, ctx->slot_base.p, ctx->tap_base.p,
+                           ctx->events.p, ctx->er_off.p, ctx->er_gain.p, ctx->info.p);
+        HIPCHK(ctx, hipGetLastError());
+        ctx->h_events.resize(nslots);
+        HIPCHK(ctx, hipMemcpyAsync(info.data(), ctx->info.p, sizeof(msg_plan_info) * P, hipMemcpyDeviceToHost, s));
+        if (nslots)
+            HIPCHK(ctx, hipMemcpyAsync(ctx->h_events.data(), ctx->events.p, sizeof(msg_event) * nslots,
+                                       hipMemcpyDeviceToHost, s));
+        HIPCHK(ctx, hipStreamSynchronize(s));
     }
-    if (nslots > INT32_MAX / 2) return fail(ctx, MSG_E_UNSUPPORTED, "too many events in one batch");
-    HIPCHK(ctx, ctx->slot_base.ensure(P));
-    HIPCHK(ctx, ctx->tap_base.ensure(P));
-    HIPCHK(ctx, ctx->events.ensure(nslots));
-    HIPCHK(ctx, ctx->er_off.ensure(ntaps));
-    HIPCHK(ctx, ctx->er_gain.ensure(ntaps));
-    HIPCHK(ctx, hipMemcpyAsync(ctx->slot_base.p, slot_base.data(), sizeof(int32_t) * P, hipMemcpyHostToDevice, s));
-    HIPCHK(ctx, hipMemcpyAsync(ctx->tap_base.p, tap_base.data(), sizeof(int32_t) * P, hipMemcpyHostToDevice, s));
-    hipLaunchKernelGGL(k_plan_events, dim3((P + pb - 1) / pb), dim3(pb), 0, s,
-                       ctx->presets.p, P, ctx->frag_len.p, ctx->dzig, ctx->slot_base.p, ctx->tap_base.p,
-                       ctx->events.p, ctx->er_off.p, ctx->er_gain.p, ctx->info.p);
-    HIPCHK(ctx, hipGetLastError());
-    ctx->h_events.resize(nslots);
-    HIPCHK(ctx, hipMemcpyAsync(info.data(), ctx->info.p, sizeof(msg_plan_info) * P, hipMemcpyDeviceToHost, s));
-    if (nslots)
-        HIPCHK(ctx, hipMemcpyAsync(ctx->h_events.data(), ctx->events.p, sizeof(msg_event) * nslots,
-                                   hipMemcpyDeviceToHost, s));
-    HIPCHK(ctx, hipStreamSynchronize(s));
     stage_mark(ctx, 1, s);
 
     // ---- host: runtime records ----
@@ -1266,7 +1446,8 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
     HIPCHK(ctx, ctx->irbank.ensure(irbank.size()));
     HIPCHK(ctx, ctx->maxbits.ensure(P));
     auto h2d = [&](void* dst, const void* src, size_t bytes) -> hipError_t {
-        return bytes ? hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, s) : hipSuccess;
+        ctx->staging.add(dst, src, bytes);    // copied at the flush below, from pinned memory
+        return hipSuccess;
     };
     for (int p = 0; p < P; ++p) tile_begin[p] = prt[p].tile_begin;
     HIPCHK(ctx, h2d(ctx->ert.p, ert.data(), sizeof(EventRt) * nslots));
@@ -1299,6 +1480,7 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
     HIPCHK(ctx, h2d(ctx->gen64_off.p, gen64_off.data(), sizeof(int64_t) * gen64_off.size()));
     HIPCHK(ctx, h2d(ctx->chains.p, chains.data(), sizeof(Chain64) * chains.size()));
     HIPCHK(ctx, h2d(ctx->imgbank.p, imgbank.data(), imgbank.size()));
+    HIPCHK(ctx, ctx->staging.flush(s));
 
     // ---- generate ----
     stage_mark(ctx, 2, s);
@@ -1407,8 +1589,9 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
     ctx->h_last64 = last64;
     ctx->last_n = P;
     if (ctx->profiling) {
-        ctx->pending = true;
-        ctx->pending_fir = hblocks > 0;
+        ctx->pending[ctx->ev_cur] = true;
+        ctx->pending_fir[ctx->ev_cur] = hblocks > 0;
+        ctx->ev_cur ^= 1;
     }
     return MSG_OK;
 }

@@ -10,7 +10,15 @@ Returns ``(audio, meta)`` like the reference: ``audio`` is a C-contiguous
 with ``astype(np.float32)`` before ``sf.write``, MS:1473-1519, 1589), ``meta``
 has ``out_sr``, ``design_sr_base``, ``micro_last``, ``grain_last`` (MS:786-791).
 The ``progress`` callback gets the reference's messages: 0 with the SR line,
-every 50th placed event, and 100 "Done." (MS:599-600, 757-758, 783-784).
+every 50th event, and 100 "Done." (MS:599-600, 757-758, 783-784).  The event
+messages are sent from the render's plan while the device is still rendering
+(msg_render_batch returns once the batch is enqueued), "Done." after the
+device has finished.
+
+Errors follow the reference: ``KeyError`` for a key ``render`` indexes and the
+dict lacks (pass ``msgpu.merged(partial)`` for a partial preset, as the UI's
+loader merges it over the factory defaults), ``ValueError`` where MS raises it,
+``NotImplementedError`` for the device limits in DESIGN.md.
 """
 from __future__ import annotations
 
@@ -18,29 +26,33 @@ import numpy as np
 
 from .engine import default_engine
 from .pack import PackedBatch, design_sr
-from .params import merged
+from .params import first_missing_key, merged
 
 _NOTE = {"IR fragment": "IR fragment", "Image scanline": ""}
 
 
 def render(params, progress=None, device: int = 0):
+    missing = first_missing_key(params)
+    if missing is not None:
+        raise KeyError(missing)
     p = merged(params)
     base_sr = int(p["base_sr"])
     if progress:
         progress(0, f"Output SR {base_sr} Hz | Design SR {design_sr(p)} Hz")
     eng = default_engine(device)
     packed = PackedBatch([p])
-    out = eng.render_packed(packed)
-    eng.torch.cuda.synchronize(eng.device)
-    audio = out.cpu().numpy().reshape(packed.total_frames, 2)
+    out = eng.render_packed(packed)           # returns once enqueued
     info = eng.last_plan()[0]
-    if progress:
+    if progress:                              # MS:757-758, while the device renders
         events = eng.last_events(0)
         n = len(events)
         note = _fragment_note(p)
         for e in events:
             if e.len > 0 and e.index % 50 == 0:
                 progress(int(5 + 70 * (e.index / max(1, n))), f"Events {e.index}/{n}  {note}".strip())
+    eng.torch.cuda.synchronize(eng.device)
+    audio = out.cpu().numpy().reshape(packed.total_frames, 2)
+    if progress:
         progress(100, "Done.")
     micro = grain = None
     if info.n_events > 0:

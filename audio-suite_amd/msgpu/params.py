@@ -3,8 +3,10 @@
 The reference's ``render(params)`` (microsound_0.2.1/main_v2.py:588, "MS" below)
 indexes an 83-key dict built by ``MicrosoundV2.get_params`` (MS:1166-1266).  The
 factory defaults are the widget initial values (MS:893-1137); partial presets are
-merged over them (MS:1288-1290).  ``DEFAULTS`` reproduces that snapshot so a
-partial dict can be passed straight to :func:`msgpu.render`.
+merged over them (MS:1288-1290).  ``DEFAULTS`` reproduces that snapshot; the
+drop-in :func:`msgpu.render` raises ``KeyError`` for a key the reference would
+index and not find (:func:`first_missing_key`), and :func:`merged` builds a full
+dict from a partial one the way the UI's preset loader does.
 """
 from __future__ import annotations
 
@@ -168,3 +170,89 @@ def config_params(name: str, seed: int = 1000, irs: dict | None = None, **overri
             raise KeyError(f"config {name} needs IR {ir_name!r}")
         p["_ir_audio"] = irs[ir_name]
     return p
+
+
+_BASIC_MODES = ("Gaussian click", "Dust impulses", "Noise burst", "Skewed transient", "Resonant strike")
+_MODE_KEYS = {
+    "Crackle / corona": ("crackle_alpha", "crackle_density", "crackle_kernel"),
+    "Stick–slip friction": ("ss_threshold", "ss_build", "ss_decay", "ss_noise"),
+    "Micro-chaos": ("chaos_r", "chaos_gate"),
+    "Wavelet atoms": ("wav_base_hz", "wav_count", "wav_spread"),
+}
+
+
+def accessed_keys(params: dict, has_events: bool = True):
+    """The keys ``render`` indexes (MS:589-784), in the order it indexes them, for
+    the branches ``params`` selects.  The event loop's keys are included when the
+    render has events (the reference reads them at its first event, MS:633-758)."""
+    get = params.get
+    yield from ("base_sr", "out_dur_s", "time_unfold", "bp_density", "bp_unfold", "bp_cutoff",
+                "bp_stretch", "event_process", "grains_per_sec", "seed", "cluster_size",
+                "cluster_spread_ms", "hawkes_gain", "hawkes_decay_s", "max_grains",
+                "spectral_imprint_on")                                           # MS:589-625
+    if has_events:
+        yield from ("bandlimit_out_hz", "partial_stretch", "grain_amp_rand", "micro_ms", "gen_mode")  # MS:634-648
+        mode = get("gen_mode")
+        if mode in _BASIC_MODES:
+            yield from ("seed", "dust_density", "noise_tilt", "ring_hz", "ring_decay_ms")   # MS:650-660
+        else:
+            yield "seed"
+            yield from _MODE_KEYS.get(mode, ())
+        yield "bandlimit_on"                                                     # MS:690
+        if get("bandlimit_on"):
+            yield "bandlimit_roll_hz"
+        for flag, keys in (("nl_warp_on", ("nl_warp_power",)), ("cep_warp_on", ("cep_factor",)),
+                           ("partial_lock_on", ("pl_top_n", "pl_neigh"))):       # MS:694-702
+            yield flag
+            if get(flag):
+                yield from keys
+        for flag, keys in (("res_bank_on", ("res_modes", "res_fmin", "res_fmax", "res_decay_ms", "seed")),
+                           ("wg_on", ("wg_lines", "wg_max_ms", "wg_fb", "seed"))):   # MS:704-717
+            yield flag
+            if get(flag):
+                yield from keys
+        yield "unfold_mode"                                                      # MS:719
+        if get("unfold_mode", "Classic reinterpret") != "Classic reinterpret":
+            yield from ("mb_b1", "mb_b2", "mb_b3", "mb_u1", "mb_u2", "mb_u3", "mb_roll")
+        yield "event_feedback_on"                                                # MS:731 (1st event: no prev)
+        if get("spectral_imprint_on"):
+            yield from ("spectral_imprint_amt", "spectral_imprint_smooth")       # MS:736-738
+        yield "grain_offset_on"                                                  # MS:746
+        if get("grain_offset_on"):
+            yield "grain_offset_max_ms"
+    yield from ("env_a", "env_d", "env_s", "env_r", "env_curve", "er_cloud_on")  # MS:760-766
+    if get("er_cloud_on"):
+        yield from ("er_taps", "er_max_ms", "seed")
+    yield "space_ir_on"                                                          # MS:772
+    if get("space_ir_on") and get("_ir_audio") is not None:
+        yield "space_ir_max_samps"
+    yield "stereo_on"                                                            # MS:775
+    if get("stereo_on"):
+        yield "stereo_width"
+    yield from ("sat_drive", "peak")                                             # MS:780-781
+
+
+def first_missing_key(params: dict):
+    """The key whose absence makes the reference's ``render`` raise KeyError, or None.
+    Whether the event loop runs is decided by the host planner (msg_plan_host, the
+    event process of MS:507-558 and the max_grains cut of MS:617-618)."""
+    keys = list(accessed_keys(params, has_events=False))
+    for k in keys:
+        if k not in params:
+            return k
+    if _n_events(params) > 0:
+        for k in accessed_keys(params, has_events=True):
+            if k not in params:
+                return k
+    return None
+
+
+def _n_events(params: dict) -> int:
+    import ctypes as C
+    from . import _lib as L
+    from .pack import Banks, pack_preset
+    s = pack_preset(merged(params), Banks())
+    info = L.MsgPlanInfo()
+    L.check(L.lib().msg_plan_host(C.byref(s), None, 0, C.byref(info), None, 0, None, None), None)
+    return int(info.n_events)
+

@@ -1,24 +1,35 @@
 #!/usr/bin/env python3
 """Benchmark: Msamples/s rendered by the MI355X Microsound render path.
 
-Workload (BASELINE.json configs[2], SURVEY.md section 8 "C3"): 384 kHz output,
-unfold x100 (design SR clamps to 30 MHz), spectral stretch x2, resonant
-transient, Poisson events, 16 k-tap IR request (8192-tap cap, MS:443),
-early reflections, stereo diffusion — a batch of 1024 presets per GPU, seeds
-1000 + rank*batch + b.  One step = one full render of the batch (device plan ->
-generate -> spectral -> overlap-add -> FIR -> stereo/normalise) with inputs
-(packed presets + IR) resident.  Weak scaling: every rank renders its own batch.
+Headline workload (BASELINE.json configs[2], SURVEY.md section 8 "C3"): 384 kHz
+output, unfold x100 (design SR clamps to 30 MHz), spectral stretch x2, resonant
+transient, Poisson events, 16 k-tap IR request (8192-tap cap, MS:443), early
+reflections, stereo diffusion -- 1024 presets per GPU, seeds 1000 + rank*batch + b.
+One step = one full render of the batch (device plan -> generate -> spectral ->
+overlap-add -> FIR -> stereo/normalise) with the packed presets and IRs resident
+and the output left in HBM.  Weak scaling: every rank renders its own batch.
 
-    python bench.py [--gpus N --steps K --warmup W --config C3 --batch 1024]
+    python bench.py [--gpus N --steps K --warmup W --config C3 --batch 1024 --points C4,C5]
 
-Multi-GPU: launched by torch.distributed.run, one process per GPU, no
-data-path collective (presets are independent); barrier + max-over-ranks timing.
+Multi-GPU (presets are independent, no data-path
+collective), two launch modes with the same per-rank code:
+  * under torch.distributed.run (RANK / WORLD_SIZE / LOCAL_RANK in the env): this
+    process is one rank on device LOCAL_RANK;
+  * ``--gpus N`` without a launcher: this process starts N rank processes itself
+    (before it touches the GPU), one per device, and relays rank 0's line.
+Ranks meet on a gloo group (127.0.0.1) for the timing barrier, the MAX of the
+elapsed times and the per-rank record -- host-side only, no RCCL.
+
+``--dry-run`` replaces the device render by a host sleep (for the CPU launcher
+tests); it never prints a bench line the driver could take for a measurement.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -30,13 +41,37 @@ import numpy as np  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: 8.0 TB/s spec
 # Per-launch HBM bytes of each kernel from rocprofv3 PMC passes (FETCH_SIZE x2
-# per the gfx950 correction + WRITE_SIZE), written by tools/pmc_traffic.py.
-TRAFFIC_JSON = os.path.join(REPO, "profiles", "traffic.json")
+# per the gfx950 correction + WRITE_SIZE), written by tools/pmc_traffic.py:
+# profiles/traffic_<config>.json, or profiles/traffic.json (C3, round 1).
+PROFILES = os.path.join(REPO, "profiles")
 # bench stage -> the kernel it times (rocprofv3 kernel-name prefix)
 STAGE_KERNEL = {"generate": "k_gen_normal", "spectral": "k_spectral", "overlap_add": "k_ola_env",
                 "fir_kernel": "k_fir2<", "stereo": "k_stereo_out"}
+STAGE_NAMES = ["plan", "host_prep", "generate", "spectral", "overlap_add", "fir", "stereo", "total",
+               "fir_kernel", "fir_h"]
+KERNEL_STAGES = ["generate", "spectral", "overlap_add", "fir_kernel", "stereo"]
 # host cores of the GPU box available to one job (its CPU share; nproc shows the machine)
 BOX_CORES = 16
+
+# Per-GPU batch of each config (BASELINE.json configs: C2 batch 1; C3 1024 on one
+# GPU; C4 4096 and C5 8192 across 8 GPUs = 512 and 1024 per GPU) and the presets
+# per in-flight sub-batch.  A C5 preset (8.4 M frames, 4000 events) needs ~0.2 GB
+# of working buffers besides its 67 MB output, so C5 renders in sub-batches of 128.
+CONFIG_BATCH = {"C1": 1, "C2": 1, "C3": 1024, "C4": 512, "C5": 1024, "H48": 1024}
+CONFIG_SUB = {"C5": 128}
+WORKLOAD = {
+    "C1": "C1: 48 kHz out, no band limit, unfold x1, stretch x1, Single event, 1 s, ER 320 taps, stereo",
+    "C2": "C2: 192 kHz out, unfold x10 (1.92 MHz design SR), stretch x1, Poisson 18/s, 1 s, 4096-tap IR, "
+          "ER 320 taps, stereo",
+    "C3": "C3: 384 kHz out, unfold x100 (30 MHz design SR), stretch x2, Poisson 18/s, 1 s, "
+          "16k-tap IR request (8192 cap), ER 320 taps, stereo",
+    "C4": "C4: 384 kHz out, unfold x200 (30 MHz design SR), stretch x4, Poisson 18/s, 1 s, "
+          "64k-tap IR request (8192 cap), ER 320 taps, stereo",
+    "C5": "C5: 3072 Hz out x unfold 500 (1.536 MHz design SR), stretch x4, 8388608 frames, Poisson capped "
+          "at 4000 events, 64k-tap IR request (8192 cap), ER 320 taps, stereo",
+    "H48": "H48: 48 kHz out, unfold x8 (384 kHz design SR), Poisson 18/s, 1 s, 4096-tap IR, ER 320 taps, "
+           "stereo",
+}
 
 
 def load_irs():
@@ -44,8 +79,9 @@ def load_irs():
     return {k: z[k] for k in z.files}
 
 
-def stage_bytes(infos, _packed, params):
-    """Algorithmic (compulsory) HBM bytes per stage for one step."""
+def stage_bytes(infos):
+    """Algorithmic (compulsory) HBM bytes per stage for the presets in ``infos``
+    (DESIGN.md section 4)."""
     sum_n = sum(int(i.pool_len) for i in infos)
     out_n = sum(int(i.out_n) for i in infos)
     return {
@@ -59,21 +95,24 @@ def stage_bytes(infos, _packed, params):
 
 
 def measured_traffic(kernel, cfg, batch):
-    """HBM bytes per launch of `kernel` from the committed PMC summary, or None
-    when no summary for this workload exists (bench cannot read PMC itself)."""
-    try:
-        with open(TRAFFIC_JSON) as f:
-            t = json.load(f)
-    except (OSError, ValueError):
-        return None
-    if t.get("config") != cfg or int(t.get("batch", -1)) != batch:
-        return None
-    for name, rec in t.get("kernels", {}).items():
-        if name.startswith(kernel):
-            return rec.get("hbm_bytes_per_launch")
+    """HBM bytes per launch of `kernel` from the committed PMC summary of this
+    workload, or None when there is none (bench cannot read PMC itself)."""
+    for path in (os.path.join(PROFILES, f"traffic_{cfg}.json"), os.path.join(PROFILES, "traffic.json")):
+        try:
+            with open(path) as f:
+                t = json.load(f)
+        except (OSError, ValueError):
+            continue
+        if t.get("config") != cfg or int(t.get("batch", -1)) != batch:
+            continue
+        for name, rec in t.get("kernels", {}).items():
+            if name.startswith(kernel):
+                return rec.get("hbm_bytes_per_launch")
     return None
 
 
+# ---------------------------------------------------------------------------
+# CPU baseline (rank 0 at N = 1 only, before the GPU is touched)
 def _cpu_worker(job):
     """Render presets seed0, seed0 + stride, ... with the oracle for budget_s seconds."""
     cfg, seed0, stride, budget_s = job
@@ -115,196 +154,456 @@ def cpu_baseline(cfg, budget_s):
                       f"{wall:.1f} s"}
 
 
+# ---------------------------------------------------------------------------
+# sharding
 def rank_seeds(rank, batch):
     """Preset seeds of one rank: contiguous, disjoint across ranks (weak scaling)."""
     return [1000 + rank * batch + b for b in range(batch)]
 
 
-def max_over_ranks(elapsed, world, device):
-    """The job's time is the slowest rank's (all-reduce MAX; no data-path collective)."""
+def preset_cost(info, taps=8192):
+    """Predicted device cost of one preset from its plan:
+    sum n log2 n over its grains + out_n (log2 L + taps / L), L the FIR block."""
+    n_ev = max(int(info.n_events), 0)
+    if n_ev == 0:
+        grain = 0.0
+    else:
+        n = max(float(info.pool_len) / n_ev, 2.0)
+        grain = float(info.pool_len) * np.log2(n)
+    L = 16384.0
+    return grain + float(info.out_n) * (np.log2(L) + taps / L)
+
+
+def balance(costs, world):
+    """Contiguous partition of presets into ``world`` chunks of near-equal total
+    cost (greedy on the prefix sum: chunk r ends where the running cost crosses
+    (r + 1) / world of the total).  Returns world + 1 cut indices."""
+    c = np.asarray(costs, dtype=np.float64)
+    n = c.size
+    pref = np.concatenate([[0.0], np.cumsum(c)])
+    total = pref[-1]
+    cuts = [0]
+    for r in range(1, world):
+        target = total * r / world
+        k = int(np.searchsorted(pref, target, side="left"))
+        # pick the closer of the two prefix points around the target
+        if k > 0 and abs(pref[k - 1] - target) <= abs(pref[min(k, n)] - target):
+            k -= 1
+        cuts.append(min(max(k, cuts[-1]), n))
+    cuts.append(n)
+    return cuts
+
+
+def plan_costs(params_list):
+    """Host plans (msg_plan_host, the device planner's code on the CPU) -> costs."""
+    import ctypes as C
+    from msgpu import _lib as L
+    from msgpu.pack import Banks, pack_preset, fragment_source
+    lib = L.lib()
+    out = []
+    for p in params_list:
+        s = pack_preset(p, Banks())
+        info = L.MsgPlanInfo()
+        frag = fragment_source(p) if p.get("gen_mode") == "IR fragment" else None
+        fp = frag.ctypes.data_as(C.POINTER(C.c_double)) if frag is not None else None
+        L.check(lib.msg_plan_host(C.byref(s), fp, 0 if frag is None else frag.size, C.byref(info),
+                                  None, 0, None, None), None)
+        taps = len(p["_ir_audio"][:int(p["space_ir_max_samps"])][:8192]) if p.get("space_ir_on") and \
+            p.get("_ir_audio") is not None else 0
+        out.append(preset_cost(info, taps))
+    return out
+
+
+class Comm:
+    """Host-side rank group (gloo over 127.0.0.1): barrier, MAX, gather.  No RCCL:
+    nothing on the data path crosses GPUs."""
+
+    def __init__(self, rank, world):
+        self.rank, self.world = rank, world
+        self.dist = None
+        if world > 1:
+            import torch.distributed as dist
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            dist.init_process_group("gloo", rank=rank, world_size=world)
+            self.dist = dist
+
+    def barrier(self):
+        if self.dist:
+            self.dist.barrier()
+
+    def max(self, x):
+        if not self.dist:
+            return x
+        import torch
+        t = torch.tensor([x], dtype=torch.float64)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def gather(self, obj):
+        if not self.dist:
+            return [obj]
+        out = [None] * self.world
+        self.dist.all_gather_object(out, obj)
+        return out
+
+    def close(self):
+        if self.dist:
+            self.dist.destroy_process_group()
+
+
+def max_over_ranks(elapsed, world, _device=None):
+    """The job's time is the slowest rank's (all-reduce MAX on the host group)."""
     if world <= 1:
         return elapsed
     import torch
     import torch.distributed as dist
-    t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+    t = torch.tensor([elapsed], dtype=torch.float64)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
 
 
-def main():
+# ---------------------------------------------------------------------------
+# one GPU's work
+class Workload:
+    """One config's presets on this rank, packed into in-flight sub-batches."""
+
+    def __init__(self, cfg, seeds, sub, irs, n_engines):
+        import msgpu
+        from msgpu.pack import PackedBatch
+        self.cfg = cfg
+        self.seeds = seeds
+        self.params = [msgpu.config_params(cfg, seed=s, irs=irs) for s in seeds]
+        sub = max(1, min(sub, len(seeds)))
+        nsub = max(n_engines, -(-len(seeds) // sub)) if len(seeds) >= n_engines else len(seeds)
+        self.cut = [len(seeds) * i // nsub for i in range(nsub + 1)]
+        self.subs = [PackedBatch(self.params[self.cut[i]:self.cut[i + 1]]) for i in range(nsub)]
+        self.frames = sum(p.total_frames for p in self.subs)
+        self.outs = None
+
+
+class GpuRunner:
+    """S contexts + HIP streams on one device (one in-flight render per stream,
+    SURVEY section 8(e)); sub-batch i renders on context i mod S, so the host
+    plans one sub-batch while the device runs another and their kernels share
+    the CUs."""
+
+    def __init__(self, dev, streams):
+        import torch
+        from msgpu.engine import Engine
+        self.torch = torch
+        self.dev = dev
+        torch.cuda.set_device(dev)
+        self.engs = [Engine(dev) for _ in range(streams)]
+        self.streams = [torch.cuda.Stream(device=dev) for _ in range(streams)]
+
+    def prepare(self, w: Workload):
+        S = len(self.engs)
+        w.outs = [self.engs[i % S].alloc_output(p) for i, p in enumerate(w.subs)]
+
+    def step(self, w: Workload):
+        S = len(self.engs)
+        for i, (p, o) in enumerate(zip(w.subs, w.outs)):
+            self.engs[i % S].render_packed(p, o, self.streams[i % S])
+
+    def sync(self):
+        self.torch.cuda.synchronize(self.dev)
+
+    def profiling(self, on):
+        for e in self.engs:
+            e.set_profiling(on)
+
+    def stage_ms(self):
+        return np.mean([np.array(e.stage_times()) for e in self.engs], axis=0)
+
+    def infos(self, w: Workload):
+        """Plan summaries of every preset of ``w``.  Each context keeps the plan of
+        the last sub-batch it rendered; earlier sub-batches are planned again."""
+        S = len(self.engs)
+        nsub = len(w.subs)
+        self.sync()
+        per = {i: self.engs[i % S].last_plan() for i in range(max(0, nsub - S), nsub)}
+        for i in range(max(0, nsub - S)):
+            e = self.engs[i % S]
+            e.render_packed(w.subs[i], w.outs[i], self.streams[i % S])
+            self.sync()
+            per[i] = e.last_plan()
+        return [x for i in range(nsub) for x in per[i]]
+
+    def check(self, w: Workload, golden, k=4):
+        """Summaries of the first k presets of sub-batch 0 against the reference's
+        (tests/golden/golden_info.json): |rms - ref| <= 1e-5, |sum - ref| <= 1e-5 n."""
+        res = {}
+        host = None
+        for j, seed in enumerate(w.seeds[:min(k, w.subs[0].n)]):
+            ref = golden.get(f"{w.cfg}_{seed}")
+            if ref is None:
+                continue
+            if host is None:
+                self.sync()
+                host = w.outs[0].cpu().numpy()
+            o, n = int(w.subs[0].offsets[j]), int(w.subs[0].out_n[j])
+            a = host[o:o + n].astype(np.float64)
+            d = {"rms": abs(float(np.sqrt(np.mean(a ** 2))) - ref["rms"]),
+                 "sum_l": abs(float(a[:, 0].sum()) - ref["sum_l"]) / n,
+                 "sum_r": abs(float(a[:, 1].sum()) - ref["sum_r"]) / n}
+            res[str(seed)] = {k2: float(f"{v:.3g}") for k2, v in d.items()}
+            res[str(seed)]["ok"] = bool(max(d.values()) <= 1e-5 and list(a.shape) == ref["shape"])
+        return {"presets": res, "all_ok": bool(res) and all(v["ok"] for v in res.values()),
+                "tolerance": "|rms - ref| <= 1e-5 and |sum_ch - ref| <= 1e-5 * out_n against the "
+                             "reference render's summaries (golden_info.json)"} if res else None
+
+    def free(self, w: Workload):
+        w.outs = None
+        self.torch.cuda.empty_cache()
+
+
+class DryRunner:
+    """Stand-in for GpuRunner in the CPU launcher tests: a step sleeps
+    dry_ms * (rank + 1) ms, so the slowest rank is known."""
+
+    def __init__(self, rank, dry_ms):
+        self.delay = dry_ms * (rank + 1) / 1e3
+        self.dev = rank
+
+    def prepare(self, w):
+        pass
+
+    def step(self, w):
+        time.sleep(self.delay)
+
+    def sync(self):
+        pass
+
+
+def timed(runner, w, steps, warmup, comm):
+    """W untimed steps, then K steps bracketed by barrier + device sync; returns
+    (this rank's seconds, max over ranks)."""
+    for _ in range(warmup):
+        runner.step(w)
+    runner.sync()
+    comm.barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        runner.step(w)
+    runner.sync()
+    comm.barrier()
+    mine = time.perf_counter() - t0
+    return mine, comm.max(mine)
+
+
+def measure(runner, cfg, seeds, sub, steps, warmup, comm, irs, golden, iso_steps=0):
+    """Time one config on this rank; returns the point record (rank 0 fills it)."""
+    world = comm.world
+    w = Workload(cfg, seeds, sub, irs, len(runner.engs))
+    runner.prepare(w)
+    for _ in range(max(1, warmup)):
+        runner.step(w)
+    runner.sync()
+    runner.profiling(True)
+    mine, elapsed = timed(runner, w, steps, 0, comm)
+    runner.profiling(False)
+    stages = {n: round(float(v), 4) for n, v in zip(STAGE_NAMES, runner.stage_ms())}
+    check = runner.check(w, golden) if comm.rank == 0 else None
+    infos = runner.infos(w)
+    nsub = len(w.subs)
+    sb = stage_bytes(infos)
+    sb_launch = {k: v / nsub for k, v in sb.items()}
+    dom = max(KERNEL_STAGES, key=lambda k: stages[k])
+    achieved = sb_launch[dom] / (stages[dom] * 1e-3) / 1e9
+    launch_batch = len(seeds) // nsub
+    sum_n = sum(int(i.pool_len) for i in infos)
+    n_ev = sum(int(i.n_events) for i in infos)
+    rec = {
+        "value": round(w.frames * world * steps / elapsed / 1e6, 3), "unit": "Msamples/s",
+        "ms_per_step": round(elapsed / steps * 1e3, 3), "steps": steps,
+        "workload": WORKLOAD.get(cfg, cfg), "presets_per_gpu": len(seeds), "sub_batches": nsub,
+        "frames_per_gpu_step": w.frames, "events_per_gpu_step": n_ev, "design_samples_per_gpu_step": sum_n,
+        "design_msamples_per_s": round(sum_n * world * steps / elapsed / 1e6, 1),
+        "roofline": {"bound": "hbm", "kernel": STAGE_KERNEL[dom].rstrip("<"),
+                     "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 4),
+                     "traffic": measured_traffic(STAGE_KERNEL[dom], cfg, launch_batch),
+                     "algorithmic_bytes": sb_launch[dom], "kernel_ms": stages[dom],
+                     "note": f"per launch in the timed region ({nsub} sub-batches of ~{launch_batch} presets "
+                             f"on {len(runner.engs)} streams sharing the GPU)"},
+        "stage_ms": stages,
+        "stage_algorithmic_GBs": {k: round(sb_launch[k] / (stages[k] * 1e-3) / 1e9, 1)
+                                  for k in sb if stages.get(k, 0) > 0},
+        "check": check, "_rank_s": mine,
+    }
+    if iso_steps > 0:
+        rec["roofline_isolated"] = isolated(runner, w, iso_steps, sb, cfg)
+    runner.free(w)
+    return rec
+
+
+def isolated(runner, w, iso_steps, sb, cfg):
+    """The whole batch on one stream, kernels not sharing the GPU."""
+    from msgpu.pack import PackedBatch
+    if len(w.subs) != len(runner.engs):
+        return None                      # sub-batched configs: one launch is not the whole batch
+    packed = PackedBatch(w.params)
+    e = runner.engs[0]
+    o = e.alloc_output(packed)
+    e.render_packed(packed, o, runner.streams[0])
+    runner.sync()
+    e.set_profiling(True)
+    for _ in range(iso_steps):
+        e.render_packed(packed, o, runner.streams[0])
+    runner.sync()
+    e.set_profiling(False)
+    iso = {n: round(float(v), 4) for n, v in zip(STAGE_NAMES, e.stage_times())}
+    dom = max(KERNEL_STAGES, key=lambda k: iso[k])
+    ach = sb[dom] / (iso[dom] * 1e-3) / 1e9
+    del o
+    return {"kernel": STAGE_KERNEL[dom].rstrip("<"), "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
+            "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "algorithmic_bytes": sb[dom],
+            "kernel_ms": iso[dom], "traffic": measured_traffic(STAGE_KERNEL[dom], cfg, len(w.params)),
+            "stage_ms": iso, "note": f"whole batch on one stream, {iso_steps} renders after the timed region"}
+
+
+# ---------------------------------------------------------------------------
+def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="C3")
-    ap.add_argument("--batch", type=int, default=1024)
+    ap.add_argument("--batch", type=int, default=0, help="presets per GPU (0: the config's default)")
+    ap.add_argument("--sub", type=int, default=0, help="presets per in-flight sub-batch (0: config default)")
     ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of CPU-baseline work")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--streams", type=int, default=2, help="in-flight sub-batches (contexts/streams) per GPU")
     ap.add_argument("--iso-steps", type=int, default=3, help="single-stream renders for roofline_isolated")
-    ap.add_argument("--h48-steps", type=int, default=5,
-                    help="steps of the 384 kHz -> 48 kHz point (config H48, same batch), 0 = skip")
-    args = ap.parse_args()
+    ap.add_argument("--points", default="H48,C4,C5",
+                    help="secondary configs timed after the headline (comma list, '' = none)")
+    ap.add_argument("--point-steps", type=int, default=3)
+    ap.add_argument("--dry-run", type=float, default=0.0, metavar="MS",
+                    help="CPU launcher test: a step sleeps MS*(rank+1) ms instead of rendering")
+    return ap.parse_args()
 
+
+def default_batch(cfg, args):
+    return args.batch if (args.batch > 0 and cfg == args.config) else CONFIG_BATCH.get(cfg, 1024)
+
+
+def default_sub(cfg, args, batch):
+    if args.sub > 0 and cfg == args.config:
+        return args.sub
+    return CONFIG_SUB.get(cfg, -(-batch // max(1, args.streams)))
+
+
+def free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch(args):
+    """--gpus N without torch.distributed.run: one rank process per GPU, started
+    before this process touches the GPU; rank 0 prints the line.  Returns the
+    exit code (the first failing rank's, after stopping the others)."""
+    n = args.gpus
+    port = str(free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(n), LOCAL_RANK=str(r), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=port, MSGPU_BENCH_CHILD="1")
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *sys.argv[1:]], env=env))
+    code = 0
+    live = set(range(n))
+    while live:
+        for r in sorted(live):
+            rc = procs[r].poll()
+            if rc is None:
+                continue
+            live.discard(r)
+            if rc != 0 and code == 0:
+                code = rc
+                for q in live:
+                    procs[q].terminate()
+        time.sleep(0.05)
+    return code
+
+
+def main():
+    args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world == 1 and args.gpus > 1:
+        sys.exit(launch(args))
     rank = int(os.environ.get("RANK", "0"))
-    cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu:
-        cpu = cpu_baseline(args.config, args.cpu_budget)
-
-    import torch
-    import torch.distributed as dist
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
-    dev = local if world > 1 else 0
+    cfg = args.config
+    batch = default_batch(cfg, args)
+    seeds = rank_seeds(rank, batch)
 
-    import msgpu
-    from msgpu.engine import Engine
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu and not args.dry_run:
+        cpu = cpu_baseline(cfg, args.cpu_budget)
+    comm = Comm(rank, world)
+    try:
+        if args.dry_run:
+            return dry_main(args, comm, cfg, seeds, local)
+        irs = load_irs()
+        with open(os.path.join(REPO, "tests", "golden", "golden_info.json")) as f:
+            golden = json.load(f)["summaries"]
+        runner = GpuRunner(local, max(1, args.streams))
+        head = measure(runner, cfg, seeds, default_sub(cfg, args, batch), args.steps, args.warmup, comm, irs,
+                       golden, iso_steps=args.iso_steps)
+        points = {}
+        for pc in [c for c in args.points.split(",") if c and c != cfg]:
+            pb = default_batch(pc, args)
+            points[pc] = measure(runner, pc, rank_seeds(rank, pb), default_sub(pc, args, pb), args.point_steps,
+                                 1, comm, irs, golden)
+        ranks = comm.gather({"rank": rank, "pid": os.getpid(), "device": local,
+                             "seeds": [seeds[0], seeds[-1]], "elapsed_s": round(head["_rank_s"], 6),
+                             "frames": head["frames_per_gpu_step"] * args.steps})
+        if rank == 0:
+            for r in [head, *points.values()]:
+                r.pop("_rank_s", None)
+            line = {
+                "metric": "Msamples/sec rendered (microsound full pipe, 384 kHz->48 kHz) at 1/2/4/8 GPUs",
+                "value": head["value"], "unit": "Msamples/s", "n_gpus": world, "steps": args.steps,
+                "warmup": args.warmup, "ms_per_step": head["ms_per_step"], "higher_is_better": True,
+                "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
+                "data": "synthetic presets (reference param dicts, seeds per rank), IRs from irs/",
+                "config": {"workload": head["workload"], "presets_per_gpu": batch,
+                           "frames_per_gpu_step": head["frames_per_gpu_step"],
+                           "events_per_gpu_step": head["events_per_gpu_step"],
+                           "design_samples_per_gpu_step": head["design_samples_per_gpu_step"],
+                           "sub_batches_per_gpu": head["sub_batches"],
+                           "parallelism": f"preset-sharded x{world}", "streams_per_gpu": len(runner.engs)},
+                "roofline": head["roofline"], "roofline_isolated": head.get("roofline_isolated"),
+                "stage_ms": head["stage_ms"], "stage_algorithmic_GBs": head["stage_algorithmic_GBs"],
+                "design_msamples_per_s": head["design_msamples_per_s"],
+                "checked": head["check"],
+                "cpu_baseline": cpu,
+                "points": points,
+                "ranks": ranks,
+            }
+            print(json.dumps(line), flush=True)
+    finally:
+        comm.close()
+
+
+def dry_main(args, comm, cfg, seeds, local):
+    """The launcher path with the device work stubbed (CPU tests): same seeds,
+    same timing protocol, per-rank record; prints a 'dry_run' line, no metric."""
     from msgpu.pack import PackedBatch
-
+    import msgpu
     irs = load_irs()
-    seeds = rank_seeds(rank, args.batch)
-    params = [msgpu.config_params(args.config, seed=s, irs=irs) for s in seeds]
-    S = max(1, min(args.streams, args.batch))
-    # S in-flight renders per GPU, one context + one HIP stream each (SURVEY
-    # section 8e: "one HIP stream per render"): the host plans one sub-batch
-    # while the device runs the other, and their kernels share the CUs.
-    cut = [len(params) * i // S for i in range(S + 1)]
-    subs = [PackedBatch(params[cut[i]:cut[i + 1]]) for i in range(S)]
-    engs = [Engine(dev) for _ in range(S)]
-    outs = [e.alloc_output(p) for e, p in zip(engs, subs)]
-    streams = [torch.cuda.Stream(device=dev) for _ in range(S)]
-
-    def barrier():
-        if world > 1:
-            dist.barrier()
-
-    def step():
-        for e, p, o, st in zip(engs, subs, outs, streams):
-            e.render_packed(p, o, st)
-
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize(dev)
-    infos = [i for e in engs for i in e.last_plan()]
-
-    for e in engs:
-        e.set_profiling(True)
-    barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize(dev)
-    barrier()
-    elapsed = time.perf_counter() - t0
-    for e in engs:
-        e.set_profiling(False)
-    elapsed = max_over_ranks(elapsed, world, f"cuda:{dev}")
-    names = ["plan", "host_prep", "generate", "spectral", "overlap_add", "fir", "stereo", "total",
-             "fir_kernel", "fir_h"]
-    # per-launch stage times in the timed region (each sub-batch on its own stream)
-    stage_ms = np.mean([np.array(e.stage_times()) for e in engs], axis=0)
-    stages = {n: round(float(v), 4) for n, v in zip(names, stage_ms)}
-
-    # isolated pass: the whole batch on one stream, kernels not sharing the GPU
-    iso = {}
-    if args.iso_steps > 0:
-        packed = PackedBatch(params)
-        e1 = engs[0]
-        o1 = e1.alloc_output(packed)
-        e1.render_packed(packed, o1, streams[0])
-        torch.cuda.synchronize(dev)
-        e1.set_profiling(True)
-        for _ in range(args.iso_steps):
-            e1.render_packed(packed, o1, streams[0])
-        torch.cuda.synchronize(dev)
-        e1.set_profiling(False)
-        iso = {n: round(float(v), 4) for n, v in zip(names, e1.stage_times())}
-        del o1
-
-    frames_rank = sum(p.total_frames for p in subs)
-    total_frames = frames_rank * world * args.steps
-    value = total_frames / elapsed / 1e6
-    ms_step = elapsed / args.steps * 1e3
-    sb = stage_bytes(infos, None, params)
-    sb_launch = {k: v / S for k, v in sb.items()}
-    stage_gbs = {k: round(sb_launch[k] / (stages[k] * 1e-3) / 1e9, 1) for k in sb if stages.get(k, 0) > 0}
-    # dominant single kernel (the FIR stage is timed without its h build)
-    kernel_stages = ["generate", "spectral", "overlap_add", "fir_kernel", "stereo"]
-    dom = max(kernel_stages, key=lambda k: stages[k])
-    achieved = sb_launch[dom] / (stages[dom] * 1e-3) / 1e9
-    traffic = measured_traffic(STAGE_KERNEL[dom], args.config, args.batch // S)
-    sum_n = sum(int(i.pool_len) for i in infos)
-    n_ev = sum(int(i.n_events) for i in infos)
-    roof_iso = None
-    if iso:
-        dom_i = max(kernel_stages, key=lambda k: iso[k])
-        ach_i = sb[dom_i] / (iso[dom_i] * 1e-3) / 1e9
-        roof_iso = {"kernel": STAGE_KERNEL[dom_i].rstrip("<"), "achieved": round(ach_i, 1),
-                    "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach_i / HBM_PEAK_GBS, 4),
-                    "algorithmic_bytes": sb[dom_i], "kernel_ms": iso[dom_i],
-                    "traffic": measured_traffic(STAGE_KERNEL[dom_i], args.config, args.batch),
-                    "stage_ms": iso, "note": f"whole batch on one stream, {args.iso_steps} renders after the "
-                                             f"timed region"}
-
-    # the metric label's "384 kHz -> 48 kHz" read literally: H48 presets, same batch
-    h48 = None
-    if args.h48_steps > 0 and args.config != "H48":
-        hp = [msgpu.config_params("H48", seed=s, irs=irs) for s in seeds]
-        hsubs = [PackedBatch(hp[cut[i]:cut[i + 1]]) for i in range(S)]
-        houts = [e.alloc_output(p) for e, p in zip(engs, hsubs)]
-
-        def hstep():
-            for e, p, o, st in zip(engs, hsubs, houts, streams):
-                e.render_packed(p, o, st)
-
-        hstep()
-        torch.cuda.synchronize(dev)
-        barrier()
-        t1 = time.perf_counter()
-        for _ in range(args.h48_steps):
-            hstep()
-        torch.cuda.synchronize(dev)
-        barrier()
-        he = max_over_ranks(time.perf_counter() - t1, world, f"cuda:{dev}")
-        hframes = sum(p.total_frames for p in hsubs)
-        h48 = {"config": "H48: 48 kHz out, unfold x8 (384 kHz design SR), Poisson 18/s, 1 s, 4096-tap IR, "
-                         "ER 320 taps, stereo",
-               "value": round(hframes * world * args.h48_steps / he / 1e6, 3), "unit": "Msamples/s",
-               "ms_per_step": round(he / args.h48_steps * 1e3, 3), "steps": args.h48_steps,
-               "presets_per_gpu": args.batch, "streams_per_gpu": S}
-        del houts
-
-    if rank == 0:
-        line = {
-            "metric": "Msamples/sec rendered (microsound full pipe, 384 kHz->48 kHz) at 1/2/4/8 GPUs",
-            "value": round(value, 3), "unit": "Msamples/s", "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": round(ms_step, 3), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
-            "data": "synthetic presets (reference param dicts, seeds per rank), IR ir_tiny_room_250ms",
-            "config": {"workload": f"{args.config}: 384 kHz out, unfold x100 (30 MHz design SR), stretch x2, "
-                                   f"Poisson 18/s, 1 s, 16k-tap IR request (8192 cap), ER 320 taps, stereo",
-                       "presets_per_gpu": args.batch, "frames_per_gpu_step": frames_rank,
-                       "events_per_gpu_step": n_ev, "design_samples_per_gpu_step": sum_n,
-                       "parallelism": f"preset-sharded x{world}", "streams_per_gpu": S},
-            "roofline": {"bound": "hbm", "kernel": STAGE_KERNEL[dom].rstrip("<"),
-                         "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                         "algorithmic_bytes": sb_launch[dom], "kernel_ms": stages[dom],
-                         "note": f"per launch in the timed region ({S} sub-batches of {args.batch // S} presets "
-                                 f"on {S} streams sharing the GPU)"},
-            "roofline_isolated": roof_iso,
-            "stage_ms": stages, "stage_algorithmic_GBs": stage_gbs,
-            "design_msamples_per_s": round(sum_n * world * args.steps / elapsed / 1e6, 1),
-            "cpu_baseline": cpu,
-            "point_384k_to_48k": h48,
-        }
-        print(json.dumps(line), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
+    runner = DryRunner(comm.rank, args.dry_run)
+    w = type("W", (), {})()
+    frames = PackedBatch([msgpu.config_params(cfg, seed=s, irs=irs) for s in seeds]).total_frames
+    mine, elapsed = timed(runner, w, args.steps, args.warmup, comm)
+    ranks = comm.gather({"rank": comm.rank, "pid": os.getpid(), "device": local, "seeds": seeds,
+                         "elapsed_s": mine, "frames": frames * args.steps})
+    if comm.rank == 0:
+        total = sum(r["frames"] for r in ranks)
+        print(json.dumps({"dry_run": True, "n_gpus": comm.world, "elapsed_max_s": elapsed,
+                          "value": total / elapsed / 1e6, "ranks": ranks}), flush=True)
 
 
 if __name__ == "__main__":

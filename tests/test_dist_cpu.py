@@ -1,18 +1,25 @@
 """Multi-rank path of bench.py on CPU (gloo, world size 2).
 
 The render shards by preset with no data-path collective:
-each rank packs its own seeds, and only the timing barrier and the MAX
-all-reduce of the elapsed time cross ranks.  These tests run that logic in two
-gloo processes; the device render itself is covered by the -m gpu tests.
+each rank packs its own seeds, and only the timing barrier, the MAX of the
+elapsed times and the per-rank record cross ranks, on a host gloo group.
+These tests run that logic in two processes -- through bench.py's own
+``--gpus 2`` launcher with the device work stubbed (``--dry-run``), and through
+the rank helpers directly; the device render itself is covered by -m gpu.
 """
+import json
 import os
 import socket
+import subprocess
+import sys
 
 import numpy as np
 import pytest
 import torch.multiprocessing as mp
 
 import bench
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def _free_port():
@@ -57,6 +64,80 @@ def test_two_rank_sharding_gloo():
     assert seeds == list(range(1000, 1000 + world * batch))      # disjoint, contiguous
     assert all(t == pytest.approx(0.5) for *_, t in res)          # max over ranks
     assert res[0][2] == res[1][2] == batch * 192000               # C2: 1 s at 192 kHz
+
+
+def _run_bench(*args, env_extra=None, timeout=300):
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
+    env.update(env_extra or {})
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), *args], capture_output=True, text=True,
+                       timeout=timeout, env=env, cwd=REPO)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    return json.loads(lines[0])
+
+
+def test_launcher_two_ranks_dry_run():
+    """bench.py --gpus 2 starts two rank processes itself (no torchrun): disjoint
+    contiguous seeds, two child PIDs (neither the parent's), devices 0 and 1, and
+    the job time is the slow rank's."""
+    d = _run_bench("--gpus", "2", "--steps", "4", "--warmup", "1", "--batch", "3", "--config", "C2",
+                   "--dry-run", "50")
+    assert d["dry_run"] is True and d["n_gpus"] == 2
+    ranks = sorted(d["ranks"], key=lambda r: r["rank"])
+    assert [r["rank"] for r in ranks] == [0, 1]
+    assert [r["device"] for r in ranks] == [0, 1]
+    pids = {r["pid"] for r in ranks}
+    assert len(pids) == 2 and os.getpid() not in pids
+    seeds = [s for r in ranks for s in r["seeds"]]
+    assert seeds == list(range(1000, 1006))
+    # rank 1 sleeps 100 ms per step, rank 0 50 ms: the max-reduced time is rank 1's
+    assert d["elapsed_max_s"] >= 0.4
+    assert d["elapsed_max_s"] == pytest.approx(max(r["elapsed_s"] for r in ranks), rel=0.05)
+    assert ranks[0]["elapsed_s"] < d["elapsed_max_s"] + 1e-9
+    assert d["value"] == pytest.approx(2 * 4 * 3 * 192000 / d["elapsed_max_s"] / 1e6)
+
+
+def test_launcher_one_rank_dry_run():
+    """--gpus 1 stays in-process (no child)."""
+    d = _run_bench("--gpus", "1", "--steps", "2", "--warmup", "0", "--batch", "2", "--config", "C2",
+                   "--dry-run", "10")
+    assert d["n_gpus"] == 1 and len(d["ranks"]) == 1
+    assert d["ranks"][0]["seeds"] == [1000, 1001]
+
+
+def test_launcher_propagates_rank_failure():
+    """A failing rank stops the job with its exit code (the other rank is not left
+    waiting in the barrier)."""
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--dry-run", "10",
+                        "--config", "NOPE", "--batch", "1"], capture_output=True, text=True, timeout=300, env=env,
+                       cwd=REPO)
+    assert r.returncode != 0
+
+
+def test_balance_contiguous_and_even():
+    rng = np.random.default_rng(0)
+    costs = rng.uniform(1, 10, size=1000)
+    for world in (1, 2, 3, 8):
+        cuts = bench.balance(costs, world)
+        assert cuts[0] == 0 and cuts[-1] == costs.size and len(cuts) == world + 1
+        assert all(a <= b for a, b in zip(cuts, cuts[1:]))
+        loads = [costs[a:b].sum() for a, b in zip(cuts, cuts[1:])]
+        assert max(loads) - min(loads) <= 2 * costs.max()
+    # one expensive preset among cheap ones goes to a rank of its own
+    cuts = bench.balance([1, 1, 1, 100, 1, 1, 1], 2)
+    assert cuts == [0, 3, 7] or cuts == [0, 4, 7]
+
+
+def test_plan_costs_track_config_size():
+    """The host planner's cost estimate orders configs by their device work."""
+    import msgpu
+    irs = bench.load_irs()
+    c2 = bench.plan_costs([msgpu.config_params("C2", seed=1000, irs=irs)])[0]
+    c3 = bench.plan_costs([msgpu.config_params("C3", seed=1000, irs=irs)])[0]
+    c5 = bench.plan_costs([msgpu.config_params("C5", seed=1000, irs=irs)])[0]
+    assert 0 < c2 < c3 < c5
 
 
 def test_single_rank_reduce_is_identity():

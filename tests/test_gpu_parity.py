@@ -221,3 +221,72 @@ def test_odd_length_stereo(msgpu, irs, frames):
         print(f"odd stereo n={a.shape[0]} w={p['stereo_width']}: rms {err:.3e}")
         assert err <= RMS_TOL
         assert np.max(np.abs(a)) > 0.5                 # a real signal, normalised to the peak
+
+
+def test_two_engines_two_streams_concurrent(msgpu, irs, golden_info):
+    """The bench's in-flight mode: two contexts rendering on two HIP streams at
+    once (sub-batches enqueued back to back, one sync at the end) give exactly
+    the single-engine renders; the C3 seeds 1000-1003 also match the reference
+    summaries."""
+    import torch
+    from msgpu.engine import Engine
+    from msgpu.pack import PackedBatch
+    seeds = list(range(1000, 1008))
+    params = [msgpu.config_params("C3", seed=s, irs=irs) for s in seeds]
+    halves = [PackedBatch(params[:4]), PackedBatch(params[4:])]
+    engs = [Engine(0), Engine(0)]
+    streams = [torch.cuda.Stream(device=0) for _ in range(2)]
+    outs = [e.alloc_output(p) for e, p in zip(engs, halves)]
+    for _ in range(2):                      # twice: the second pass reuses every buffer
+        for e, p, o, st in zip(engs, halves, outs, streams):
+            e.render_packed(p, o, st)
+    torch.cuda.synchronize(0)
+    conc = [o.cpu().numpy() for o in outs]
+    single = Engine(0)
+    for h, p in enumerate(halves):
+        ref = single.render_packed(p)
+        torch.cuda.synchronize(0)
+        assert np.array_equal(conc[h], ref.cpu().numpy()), h
+    for j, s in enumerate(seeds[:4]):
+        g = golden_info["summaries"][f"C3_{s}"]
+        o, n = int(halves[0].offsets[j]), int(halves[0].out_n[j])
+        a = conc[0][o:o + n].astype(np.float64)
+        assert abs(float(np.sqrt(np.mean(a ** 2))) - g["rms"]) <= RMS_TOL
+        assert abs(float(a[:, 0].sum()) - g["sum_l"]) <= RMS_TOL * n
+        assert abs(float(a[:, 1].sum()) - g["sum_r"]) <= RMS_TOL * n
+
+
+def test_host_plan_equals_device_plan(msgpu, irs, golden_info, monkeypatch):
+    """msg_render_batch plans on the host pool (no device round trip); the device
+    planner (k_plan_sizes / k_plan_events, MSGPU_DEVICE_PLAN=1) runs the same
+    plan.h code.  Both give the same events and the same audio, on a batch that
+    mixes every event process and several generators."""
+    import torch
+    from msgpu.engine import Engine
+    from msgpu.pack import PackedBatch
+    params = [msgpu.config_params("C3", seed=1000, irs=irs, out_dur_s=0.3),
+              msgpu.config_params("C2", seed=1001, irs=irs)]
+    for name in ("wavelet_mist", "02_friction_lattice", "chaotic_dustfield", "micro_carillon"):
+        p = msgpu.merged(golden_info["preset_params"][name])
+        p["out_dur_s"] = 0.5
+        p["_ir_audio"] = irs["tiny_room_ir"]
+        params.append(p)
+    for proc in ("Clustered", "Hawkes", "Single"):
+        params.append(msgpu.config_params("C2", seed=1002, irs=irs, event_process=proc, out_dur_s=0.5))
+    packed = PackedBatch(params)
+    host_eng = Engine(0)
+    monkeypatch.setenv("MSGPU_DEVICE_PLAN", "1")
+    dev_eng = Engine(0)
+    a = host_eng.render_packed(packed)
+    b = dev_eng.render_packed(packed)
+    torch.cuda.synchronize(0)
+    for i in range(packed.n):
+        eh, ed = host_eng.last_events(i), dev_eng.last_events(i)
+        assert len(eh) == len(ed) > 0
+        for x, y in zip(eh, ed):
+            assert (x.n, x.start, x.offset, x.len, x.gen_sr) == (y.n, y.start, y.offset, y.len, y.gen_sr), i
+            # float64 event times / amplitudes: the host's libm and the device's
+            # log1p/exp (ziggurat slow paths) may differ in the last ulp
+            assert abs(x.t0 - y.t0) <= 4e-16 * max(1.0, abs(y.t0)), (i, x.t0, y.t0)
+            assert abs(x.amp - y.amp) <= 4e-16 * abs(y.amp), (i, x.amp, y.amp)
+    assert float(np.max(np.abs(a.cpu().numpy() - b.cpu().numpy()))) <= 1e-6
