@@ -44,10 +44,13 @@ template <int M> struct FirGeo {
     static constexpr int NB1 = M / R1, NB2 = M / R2, NB3 = M / R3;
     static constexpr int BP1 = NB1 / T, BP2 = NB2 / T;        // butterflies per thread
     static_assert(NB1 % T == 0 && NB2 % T == 0 && NB3 == 2 * T, "FIR FFT plan");
-    // twiddle tables (float2 entries) at LDS offset 0
-    static constexpr int S2 = R2 * (R1 > R3 ? R1 : R3);        // w_S2^x: passes 2 and 2'
-    static constexpr int OFF_S2 = 0;
-    static constexpr int OFF_MLO = S2;                          // w_M^x, x < 128
+    // twiddle tables (float2 entries) at LDS offset 0.  The radix-R2 passes
+    // read w_{NS R2}^{k r} at [r][k] (k = butterfly index mod NS): the lanes of a
+    // wave read consecutive entries, so the table reads are conflict-free
+    // (a k*r-strided single table conflicted up to 16-way at r = 16).
+    static constexpr int OFF_T2A = 0;                           // pass 2:  NS = R1, [R2][R1]
+    static constexpr int OFF_T2B = R2 * R1;                     // pass 2': NS = R3, [R2][R3]
+    static constexpr int OFF_MLO = OFF_T2B + R2 * R3;           // w_M^x, x < 128
     static constexpr int OFF_MHI = OFF_MLO + 128;               // w_M^(128 x), x < M/128
     static constexpr int OFF_PLO = OFF_MHI + M / 128;           // w_2M^x, x < 128
     static constexpr int OFF_PHI = OFF_PLO + 128;               // w_2M^(128 x), 128 x <= NB3
@@ -65,11 +68,13 @@ template <int M> struct FirGeo {
 template <int S> MSG_HD constexpr int padx(int x) { return x + (x >> fir_ilog2(S)); }
 
 // One radix-R Stockham pass LDS -> LDS: read layout SI with NB = M/R
-// butterflies, twiddles w_{NS R}^{k r} from the exact S2 table, write layout SO.
+// butterflies, twiddles w_{NS R}^{k r} from the exact [r][k] table, write layout SO.
 template <int M, int R, int NS, int BP, int SI, int SO>
 MSG_DEV void fir_pass_lds(float2* buf, const float2* tab, int t) {
     using G = FirGeo<M>;
-    constexpr int NB = M / R, T = G::T, F = G::S2 / (NS * R);
+    constexpr int NB = M / R, T = G::T;
+    constexpr int OFF_T = NS == G::R1 ? G::OFF_T2A : G::OFF_T2B;
+    static_assert(NS == G::R1 || NS == G::R3, "radix-R2 pass after R1 or R3");
     float2 v[BP][R];
 #pragma unroll
     for (int b = 0; b < BP; ++b) {
@@ -82,9 +87,8 @@ MSG_DEV void fir_pass_lds(float2* buf, const float2* tab, int t) {
     for (int b = 0; b < BP; ++b) {
         const int j = t + b * T;
         const int k = j & (NS - 1), q = j / NS;
-        const int kf = k * F;
 #pragma unroll
-        for (int r = 1; r < R; ++r) v[b][r] = cmul(v[b][r], tab[G::OFF_S2 + ((kf * r) & (G::S2 - 1))]);
+        for (int r = 1; r < R; ++r) v[b][r] = cmul(v[b][r], tab[OFF_T + r * NS + k]);
         Dft<R, false>::run(v[b]);
         const int obase = padx<SO>(q * NS * R + k);
 #pragma unroll
@@ -526,7 +530,10 @@ inline void fir2_tables(std::vector<float>& out) {
         out[2 * at] = (float)cosl(a);
         out[2 * at + 1] = (float)sinl(a);
     };
-    for (int x = 0; x < G::S2; ++x) put(G::OFF_S2 + x, x, G::S2);
+    for (int r = 0; r < G::R2; ++r)
+        for (int k = 0; k < G::R1; ++k) put(G::OFF_T2A + r * G::R1 + k, (long double)k * r, (long double)G::R1 * G::R2);
+    for (int r = 0; r < G::R2; ++r)
+        for (int k = 0; k < G::R3; ++k) put(G::OFF_T2B + r * G::R3 + k, (long double)k * r, (long double)G::R3 * G::R2);
     for (int x = 0; x < 128; ++x) put(G::OFF_MLO + x, x, M);
     for (int x = 0; x < M / 128; ++x) put(G::OFF_MHI + x, 128.0L * x, M);
     for (int x = 0; x < 128; ++x) put(G::OFF_PLO + x, x, 2.0L * M);

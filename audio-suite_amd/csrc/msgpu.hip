@@ -679,112 +679,7 @@ int msg_stage_times(msg_ctx* ctx, float* ms, int32_t n) {
     return MSG_OK;
 }
 
-int msg_plan_host(const msg_preset* preset, const double* ir_frag, int64_t ir_frag_len,
-                  msg_plan_info* info, msg_event* events, int32_t max_events,
-                  int32_t* er_off, double* er_gain) {
-    (void)ir_frag;
-    if (!preset || !info) return fail(nullptr, MSG_E_ARG, "null argument");
-    msg_plan_info sz;
-    msgplan::plan_sizes(*preset, kHostZig, ir_frag_len, sz);
-    *info = sz;
-    if (!events) return MSG_OK;
-    if (sz.n_slots > max_events) return fail(nullptr, MSG_E_ARG, "event buffer too small");
-    const bool er = (preset->flags & MSG_F_ER_CLOUD) != 0;
-    msgplan::plan_events(*preset, kHostZig, ir_frag_len, 0, *info, events,
-                         er ? er_off : nullptr, er ? er_gain : nullptr);
-    return MSG_OK;
-}
-
-int msg_rng_raw(uint64_t seed, uint64_t* out, int64_t n) {
-    nprng::Pcg64 g = nprng::default_rng(seed);
-    for (int64_t i = 0; i < n; ++i) out[i] = nprng::next_u64(g);
-    return MSG_OK;
-}
-int msg_rng_normal(uint64_t seed, double* out, int64_t n) {
-    nprng::Pcg64 g = nprng::default_rng(seed);
-    for (int64_t i = 0; i < n; ++i) out[i] = nprng::standard_normal(g, kHostZig);
-    return MSG_OK;
-}
-int msg_rng_exponential(uint64_t seed, double* out, int64_t n) {
-    nprng::Pcg64 g = nprng::default_rng(seed);
-    for (int64_t i = 0; i < n; ++i) out[i] = nprng::standard_exponential(g, kHostZig);
-    return MSG_OK;
-}
-int msg_rng_integers(uint64_t seed, int64_t low, int64_t high, int64_t* out, int64_t n) {
-    if (high <= low) return fail(nullptr, MSG_E_VALUE, "low >= high");
-    nprng::Pcg64 g = nprng::default_rng(seed);
-    for (int64_t i = 0; i < n; ++i) out[i] = nprng::integers(g, low, high);
-    return MSG_OK;
-}
-
-// Host emulation of k_gen_normal's chunked walk (same decisions, sequential lanes).
-int msg_rng_normal_chunked(uint64_t seed, double* out, int64_t n) {
-    const nprng::Pcg64 g0 = nprng::default_rng(seed);
-    nprng::Jump ja[64];
-    for (int l = 0; l < 64; ++l) ja[l] = nprng::jump_of((uint64_t)l + 1);
-    const nprng::Jump j64 = nprng::jump_of(64);
-    nprng::u128 st[64];
-    for (int l = 0; l < 64; ++l) st[l] = ja[l].a * g0.state + g0.inc * ja[l].s;
-    int64_t produced = 0;
-    int local = 0;
-    while (produced < n) {
-        uint64_t rabs[64]; int idx[64]; double x[64]; uint64_t F = 0;
-        for (int l = 0; l < 64; ++l) {
-            const uint64_t raw = nprng::xsl_rr(st[l]);
-            idx[l] = (int)(raw & 0xff);
-            const uint64_t rr = raw >> 8;
-            rabs[l] = (rr >> 1) & 0x000fffffffffffffULL;
-            x[l] = (double)rabs[l] * zig_wi_double[idx[l]];
-            if (rr & 1) x[l] = -x[l];
-            if (rabs[l] < zig_ki_double[idx[l]]) F |= 1ULL << l;
-        }
-        while (local < 64 && produced < n) {
-            const uint64_t S = ~F & (~0ULL << local);
-            const int q = S ? __builtin_ctzll(S) : 64;
-            for (int l = local; l < q; ++l) {
-                const int64_t j = produced + l - local;
-                if (j < n) out[j] = x[l];
-            }
-            produced += q - local;
-            if (q == 64) { local = 64; break; }
-            nprng::Pcg64 g;
-            g.state = st[q]; g.inc = g0.inc; g.has_u32 = 0; g.u32 = 0;
-            // replicate slow_normal (host copy of the same control flow)
-            int c = 1;
-            uint64_t ra = rabs[q]; int id = idx[q]; double xv = x[q]; double v = 0.0;
-            for (;;) {
-                if (id == 0) {
-                    for (;;) {
-                        const double xx = -nprng::ZIG_NOR_INV_R * log1p(-nprng::next_double(g));
-                        const double yy = -log1p(-nprng::next_double(g));
-                        c += 2;
-                        if (yy + yy > xx * xx) { v = ((ra >> 8) & 1) ? -(nprng::ZIG_NOR_R + xx) : nprng::ZIG_NOR_R + xx; break; }
-                    }
-                    break;
-                }
-                const double u = nprng::next_double(g);
-                c += 1;
-                if (((zig_fi_double[id - 1] - zig_fi_double[id]) * u + zig_fi_double[id]) < exp(-0.5 * xv * xv)) { v = xv; break; }
-                uint64_t r = nprng::next_u64(g);
-                c += 1;
-                id = (int)(r & 0xff); r >>= 8;
-                const int sign = (int)(r & 1);
-                ra = (r >> 1) & 0x000fffffffffffffULL;
-                xv = (double)ra * zig_wi_double[id];
-                if (sign) xv = -xv;
-                if (ra < zig_ki_double[id]) { v = xv; break; }
-            }
-            if (produced < n) out[produced] = v;
-            ++produced;
-            local = q + c;
-        }
-        do {
-            for (int l = 0; l < 64; ++l) st[l] = j64.a * st[l] + g0.inc * j64.s;
-            local -= 64;
-        } while (local >= 64);
-    }
-    return MSG_OK;
-}
+#include "host_abi.inc"
 
 int msg_bench_fft(msg_ctx* ctx, int32_t n, int32_t reps, int32_t blocks, float* ms_out) {
     if (!ctx || !ms_out || n < 2 || reps < 1 || blocks < 1) return MSG_E_ARG;

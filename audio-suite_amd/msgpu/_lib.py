@@ -130,10 +130,12 @@ def lib() -> C.CDLL:
             # torch bundles its own HIP runtime and resolves it by file name; load it
             # first so libmsgpu binds to that same libamdhip64.so.7 (by SONAME)
             # instead of a second copy from /opt/rocm.
-            try:
-                import torch  # noqa: F401
-            except ImportError:
-                pass
+            # (MSGPU_HOST_ONLY=1: the host-sanitizer build has no HIP code; skip it)
+            if os.environ.get("MSGPU_HOST_ONLY") != "1":
+                try:
+                    import torch  # noqa: F401
+                except ImportError:
+                    pass
             L = C.CDLL(LIB_PATH)
             for name, (res, args) in _PROTOS.items():
                 f = getattr(L, name)

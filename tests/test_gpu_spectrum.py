@@ -89,7 +89,7 @@ def test_batch_variations_match_single_renders(tmp_path):
     assert [r[0] for r in res] == ["ms_seed1001_unf15_st0p9_48000Hz.wav", "ms_seed1001_unf15_st1p2_48000Hz.wav",
                                    "ms_seed1002_unf15_st0p9_48000Hz.wav", "ms_seed1002_unf15_st1p2_48000Hz.wav"]
     for (name, audio, sr), (sd, st) in zip(res, [(1001, 0.9), (1001, 1.2), (1002, 0.9), (1002, 1.2)]):
-        p = dict(base, seed=sd, time_unfold=15.0, partial_stretch=st)
+        p = msgpu.merged(base, seed=sd, time_unfold=15.0, partial_stretch=st)   # full dict, as get_params
         ref, meta = msgpu.render(p)
         assert sr == meta["out_sr"] == 48000
         # same engine; the FIR transform size is chosen per batch, so float32 rounding

@@ -1,0 +1,46 @@
+"""Host code under AddressSanitizer + UndefinedBehaviorSanitizer.
+
+The render plan (csrc/plan.h) and the NumPy stream primitives (csrc/nprng.h)
+run on the host in every batch (msg_render_batch plans on a host thread pool)
+and on the device.  csrc/host_san.cpp compiles their host entry points
+(csrc/host_abi.inc, the same source the product library includes) with
+``g++ -fsanitize=address,undefined -fno-sanitize-recover=undefined`` into a
+host-only library, and this test runs tests/test_plan_host.py and
+tests/test_rng_host.py against it in a child interpreter with the sanitizer
+runtimes preloaded.  Any ASan report or UBSan runtime error fails the run.
+"""
+import os
+import shutil
+import subprocess
+import sys
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CSRC = os.path.join(REPO, "audio-suite_amd", "csrc")
+
+
+def _runtime(name):
+    p = subprocess.run(["g++", f"-print-file-name={name}"], capture_output=True, text=True).stdout.strip()
+    return p if os.path.isabs(p) and os.path.exists(p) else None
+
+
+@pytest.mark.skipif(shutil.which("g++") is None, reason="needs g++")
+def test_plan_and_rng_under_asan_ubsan(tmp_path):
+    asan, ubsan = _runtime("libasan.so"), _runtime("libubsan.so")
+    if not asan or not ubsan:
+        pytest.skip("sanitizer runtimes not installed")
+    lib = str(tmp_path / "libmsgpu_hostsan.so")
+    subprocess.run(["g++", "-std=c++17", "-O1", "-g", "-fPIC", "-shared", "-fno-omit-frame-pointer",
+                    "-fsanitize=address,undefined", "-fno-sanitize-recover=undefined", "-Wall", "-Werror",
+                    "-Wno-unused-function", "-o", lib, os.path.join(CSRC, "host_san.cpp")], check=True)
+    env = dict(os.environ, MSGPU_LIB=lib, MSGPU_HOST_ONLY="1", LD_PRELOAD=f"{asan}:{ubsan}",
+               ASAN_OPTIONS="detect_leaks=0:abort_on_error=1", UBSAN_OPTIONS="print_stacktrace=1:halt_on_error=1",
+               PYTHONDONTWRITEBYTECODE="1")
+    r = subprocess.run([sys.executable, "-m", "pytest", "-q", "-x", "-p", "no:cacheprovider",
+                        os.path.join(REPO, "tests", "test_plan_host.py"), os.path.join(REPO, "tests", "test_rng_host.py")],
+                       capture_output=True, text=True, env=env, cwd=REPO, timeout=900)
+    out = r.stdout + r.stderr
+    assert r.returncode == 0, out[-4000:]
+    assert "ERROR: AddressSanitizer" not in out and "runtime error:" not in out, out[-4000:]
+    assert " passed" in out
