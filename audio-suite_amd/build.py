@@ -14,6 +14,12 @@ MSGPU_LIB=.../libmsgpu_exp.so.  Never the product library.
 Objects are cached per variant and rebuilt when a source or local header is
 newer, or when the variant's defines differ from those recorded in the object
 directory's defs stamp (so changing MSGPU_EXP_DEFS always recompiles).
+
+--exp-tu NAME[,NAME..] [--out FILE] is the fast form of --exp for one-kernel
+experiments: only the named translation units are compiled (with
+MSGPU_EXP_DEFS, into build_exp_tu/, always from scratch) and linked with the
+product build's objects for the rest; the library goes to msgpu/FILE
+(default libmsgpu_exp.so).  Never the product library.
 """
 import concurrent.futures as cf
 import os
@@ -25,7 +31,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 OBJ = os.path.join(HERE, "build")
 OUT = os.path.join(HERE, "msgpu", "libmsgpu.so")
-TUS = ["msgpu.hip", "k_spectral.hip", "k_spectral_ct.hip", "k_fir.hip", "k_grain64.hip", "k_grain64_lds.hip",
+TUS = ["msgpu.hip", "k_spectral.hip", "k_spectral_ct.hip", "k_spec3.hip", "k_fir.hip", "k_grain64.hip", "k_grain64_lds.hip",
        "k_grain64_glb.hip", "k_stereo_odd.hip"]
 HEADERS = [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".h")] + \
           [os.path.join(os.path.dirname(HERE), "include", "msgpu.h")]
@@ -114,6 +120,32 @@ def build(force: bool = False, variant: str = "") -> str:
     return OUT
 
 
+def build_exp_tu(tus, out_name="libmsgpu_exp.so") -> str:
+    """Experiment library: `tus` compiled with MSGPU_EXP_DEFS, the rest from the product build."""
+    build()                                   # product objects up to date
+    defs = os.environ.get("MSGPU_EXP_DEFS", "").split()
+    objdir = os.path.join(HERE, "build_exp_tu")
+    os.makedirs(objdir, exist_ok=True)
+    objs = []
+    for tu in TUS:
+        if tu in tus:
+            o = os.path.join(objdir, tu.replace(".hip", ".o"))
+            cmd = [HIPCC, *FLAGS, *defs, "-c", "-o", o, os.path.join(CSRC, tu)]
+            print("[msgpu build]", " ".join(cmd), flush=True)
+            subprocess.check_call(cmd)
+        else:
+            o = os.path.join(HERE, "build", tu.replace(".hip", ".o"))
+        objs.append(o)
+    out = os.path.join(HERE, "msgpu", out_name)
+    subprocess.check_call([HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", out, *objs])
+    return out
+
+
 if __name__ == "__main__":
+    if "--exp-tu" in sys.argv:
+        tus = sys.argv[sys.argv.index("--exp-tu") + 1].split(",")
+        name = sys.argv[sys.argv.index("--out") + 1] if "--out" in sys.argv else "libmsgpu_exp.so"
+        print(build_exp_tu(tus, name))
+        sys.exit(0)
     var = "stamps" if "--stamps" in sys.argv else ("exp" if "--exp" in sys.argv else "")
     print(build(force="--force" in sys.argv, variant=var))

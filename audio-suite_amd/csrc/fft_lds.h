@@ -49,56 +49,70 @@ struct RealPlan {
     const float2* rt1;    // even: exp(-2 pi i 128 j / n), j < rt_hi_n
 };
 
-MSG_DEV float2 cmul(float2 a, float2 b) { return make_float2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x); }
-MSG_DEV float2 cmulc(float2 a, float2 b) { return make_float2(a.x * b.x + a.y * b.y, a.y * b.x - a.x * b.y); } // a*conj(b)
-MSG_DEV float2 cadd(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
-MSG_DEV float2 csub(float2 a, float2 b) { return make_float2(a.x - b.x, a.y - b.y); }
+// Complex arithmetic in the two-lane vector form the gfx950 packed FP32 ALU
+// executes directly (v_pk_mul/fma/add_f32 with op_sel/neg modifiers): a complex
+// multiply is one v_pk_mul + one v_pk_fma, where the scalar-component form
+// compiled to three packed ops and a v_mov per product (static VALU count of
+// a radix-5 DFT 25 -> 19, of the k_spec3 kernel 4561 -> 3033).
+typedef float f2v __attribute__((ext_vector_type(2)));
+MSG_DEV f2v vv(float2 a) { return f2v{a.x, a.y}; }
+MSG_DEV float2 ff(f2v a) { return make_float2(a.x, a.y); }
+MSG_DEV float2 cmul(float2 a, float2 b) {
+    return ff(f2v{a.x, a.x} * f2v{b.x, b.y} + f2v{-a.y, a.y} * f2v{b.y, b.x});
+}
+MSG_DEV float2 cmulc(float2 a, float2 b) {   // a * conj(b)
+    return ff(f2v{a.x, a.y} * f2v{b.x, b.x} + f2v{a.y, -a.x} * f2v{b.y, b.y});
+}
+MSG_DEV float2 cadd(float2 a, float2 b) { return ff(vv(a) + vv(b)); }
+MSG_DEV float2 csub(float2 a, float2 b) { return ff(vv(a) - vv(b)); }
 MSG_DEV float2 cconj(float2 a) { return make_float2(a.x, -a.y); }
-MSG_DEV float2 cscale(float2 a, float s) { return make_float2(a.x * s, a.y * s); }
+MSG_DEV float2 cscale(float2 a, float s) { return ff(vv(a) * s); }
 template <bool INV> MSG_DEV float2 mul_mi(float2 a) { return INV ? make_float2(-a.y, a.x) : make_float2(a.y, -a.x); }
 
 // ---- register-resident DFT kernels (forward sign -1, inverse +1), in place ----
 template <int R, bool INV> struct Dft;
 
 template <bool INV> struct Dft<2, INV> {
-    static MSG_DEV void run(float2* v) { float2 a = v[0], b = v[1]; v[0] = cadd(a, b); v[1] = csub(a, b); }
+    static MSG_DEV void run(float2* v) { const f2v a = vv(v[0]), b = vv(v[1]); v[0] = ff(a + b); v[1] = ff(a - b); }
 };
 template <bool INV> struct Dft<4, INV> {
     static MSG_DEV void run(float2* v) {
-        float2 a0 = cadd(v[0], v[2]), a1 = csub(v[0], v[2]);
-        float2 b0 = cadd(v[1], v[3]), b1 = mul_mi<INV>(csub(v[1], v[3]));
-        v[0] = cadd(a0, b0); v[2] = csub(a0, b0);
-        v[1] = cadd(a1, b1); v[3] = csub(a1, b1);
+        const f2v a0 = vv(v[0]) + vv(v[2]), a1 = vv(v[0]) - vv(v[2]);
+        const f2v b0 = vv(v[1]) + vv(v[3]), d = vv(v[1]) - vv(v[3]);
+        // b1 = -+i d: (d.y, -d.x) forward, (-d.y, d.x) inverse
+        const f2v b1 = f2v{d.y, d.x} * (INV ? f2v{-1.f, 1.f} : f2v{1.f, -1.f});
+        v[0] = ff(a0 + b0); v[2] = ff(a0 - b0);
+        v[1] = ff(a1 + b1); v[3] = ff(a1 - b1);
     }
 };
 template <int R, bool INV> struct DftOdd {   // odd prime radices, symmetric-pair form
     static MSG_DEV void run(float2* v) {
         constexpr int H = (R - 1) / 2;
-        float2 a[H], b[H];
-        const float2 x0 = v[0];
-        float2 s0 = x0;
+        f2v a[H], b[H];
+        const f2v x0 = vv(v[0]);
+        f2v s0 = x0;
 #pragma unroll
         for (int j = 1; j <= H; ++j) {
-            a[j - 1] = cadd(v[j], v[R - j]);
-            b[j - 1] = csub(v[j], v[R - j]);
-            s0 = cadd(s0, a[j - 1]);
+            a[j - 1] = vv(v[j]) + vv(v[R - j]);
+            b[j - 1] = vv(v[j]) - vv(v[R - j]);
+            s0 += a[j - 1];
         }
         float2 out[R];
-        out[0] = s0;
+        out[0] = ff(s0);
 #pragma unroll
         for (int k = 1; k <= H; ++k) {
-            float2 re = x0, im = make_float2(0.f, 0.f);
+            f2v re = x0, im = f2v{0.f, 0.f};
 #pragma unroll
             for (int j = 1; j <= H; ++j) {
                 const int jk = (j * k) % R;
                 const float c = (float)__builtin_cos(2.0 * 3.14159265358979323846 * jk / R);
-                const float s = (float)__builtin_sin(2.0 * 3.14159265358979323846 * jk / R);
-                re = make_float2(fmaf(a[j - 1].x, c, re.x), fmaf(a[j - 1].y, c, re.y));
-                im = make_float2(fmaf(b[j - 1].x, s, im.x), fmaf(b[j - 1].y, s, im.y));
+                const float sn = (float)__builtin_sin(2.0 * 3.14159265358979323846 * jk / R);
+                re += a[j - 1] * c;
+                // -+i sn b: (b.y sn, -b.x sn) forward, (-b.y sn, b.x sn) inverse
+                im += f2v{b[j - 1].y, b[j - 1].x} * (INV ? f2v{-sn, sn} : f2v{sn, -sn});
             }
-            const float2 t = INV ? make_float2(-im.y, im.x) : make_float2(im.y, -im.x);
-            out[k] = cadd(re, t);
-            out[R - k] = csub(re, t);
+            out[k] = ff(re + im);
+            out[R - k] = ff(re - im);
         }
 #pragma unroll
         for (int k = 0; k < R; ++k) v[k] = out[k];

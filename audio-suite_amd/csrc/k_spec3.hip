@@ -1,0 +1,47 @@
+// k_spec3.hip — translation unit of the band-pruned register-resident spectral
+// kernel (spec3.h) for the 30 MHz hot length.
+#include "spec3.h"
+#include "launch.h"
+
+void spec3_init_attrs() {
+    (void)hipFuncSetAttribute((const void*)k_spec3<Spec3P18750>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              Spec3P18750::LDS_BYTES);
+}
+
+bool spec3_tables(std::vector<float>& out) {
+    spec3_tables<Spec3P18750>(out);
+    return true;
+}
+
+// The event runs on k_spec3 (see spec3.h "Eligibility"): returns true and its band.
+bool spec3_eligible(int n, int ops, int gen_sr, double cutoff_gen, double roll, double stretch, int64_t float_off,
+                    int32_t* kb, int32_t* kz, int32_t* ky, double* inv_f) {
+    using P = Spec3P18750;
+    if (n != 2 * P::M || (float_off & 1)) return false;
+    if (ops & (SPEC_TILT_NOISE | SPEC_TILT_SKEW | SPEC_WARP)) return false;
+    if (!(ops & SPEC_LOWPASS)) return false;
+    const Spec3Band b = s3_band(n, gen_sr, cutoff_gen, roll, (ops & SPEC_STRETCH) != 0, stretch);
+    if (!(b.ky <= P::M / 2 && b.kz <= b.ky && s3_band_fits<P>(b.kz, b.ky))) return false;
+    *kb = b.kb; *kz = b.kz; *ky = b.ky; *inv_f = b.inv_f;
+    return true;
+}
+
+hipError_t launch_spec3(unsigned grid, hipStream_t s, const msg_event* events, const EventRt* ert, const PresetRt* rt,
+                        const float2* tables, const int32_t* ev_list, int n_list, const float* micro_pool,
+                        float* grain_pool) {
+    using P = Spec3P18750;
+    hipLaunchKernelGGL((k_spec3<P>), dim3(grid), dim3(P::T), P::LDS_BYTES, s, events, ert, rt, tables, ev_list,
+                       n_list, micro_pool, grain_pool);
+    return hipGetLastError();
+}
+
+#ifdef MSG_STAMPS
+// per-TU phase stamps of k_spec3 (debug builds): read and reset
+extern "C" int msg_debug_stamps_s3(unsigned long long* out, int n) {
+    unsigned long long h[16];
+    if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_spec_stamps), sizeof(h)) != hipSuccess) return 3;
+    for (int i = 0; i < n && i < 16; ++i) out[i] = h[i];
+    const unsigned long long z[16] = {};
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_spec_stamps), z, sizeof(z)) == hipSuccess ? 0 : 3;
+}
+#endif

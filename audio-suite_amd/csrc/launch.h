@@ -29,6 +29,15 @@ hipError_t launch_spectral_ct(int plan, unsigned grid, hipStream_t s, const msg_
                               const PresetRt* rt, const float2* tables, const int32_t* ev_list, int n_list,
                               float* micro_pool, float* grain_pool);
 
+// band-pruned register-resident spectral kernel for the 30 MHz hot length (spec3.h)
+void spec3_init_attrs();
+bool spec3_tables(std::vector<float>& out);
+bool spec3_eligible(int n, int ops, int gen_sr, double cutoff_gen, double roll, double stretch, int64_t float_off,
+                    int32_t* kb, int32_t* kz, int32_t* ky, double* inv_f);
+hipError_t launch_spec3(unsigned grid, hipStream_t s, const msg_event* events, const EventRt* ert, const PresetRt* rt,
+                        const float2* tables, const int32_t* ev_list, int n_list, const float* micro_pool,
+                        float* grain_pool);
+
 void fir_init_attrs();
 hipError_t launch_ir_spec(unsigned grid, int lds_bytes, hipStream_t s, const int64_t* jobs, int n_jobs,
                           const RealPlan* fir_plans, const double* ir_bank, float2* ir_spec);

@@ -217,6 +217,8 @@ struct msg_ctx {
     JumpTab* d_jump = nullptr;
     float2* d_fir2tab[5] = {};   // k_fir2 twiddle tables, M = 1024 << i
     float2* d_spec_ct_tab[SPEC_CT_PLANS] = {};   // compile-time spectral plans (spec_ct.h)
+    float2* d_spec3_tab = nullptr;               // band-pruned spectral kernel (spec3.h)
+    DevBuf<int32_t> spec3_list;
     nprng::Zig dzig{};
     PlanStore grain_plans, fir_plans;
     // per-batch buffers
@@ -585,10 +587,18 @@ msg_ctx* msg_create(int device_ordinal) {
             return nullptr;
         }
     }
+    {
+        std::vector<float> tab;
+        if (!spec3_tables(tab) || !up(ctx->d_spec3_tab, reinterpret_cast<float2*>(tab.data()), tab.size() / 2)) {
+            g_err = "uploading spectral twiddle tables failed";
+            return nullptr;
+        }
+    }
     for (auto& set : ctx->ev)
         for (auto& ev : set) hipEventCreate(&ev);
     if (const char* e = getenv("MSGPU_DEVICE_PLAN")) ctx->device_plan = e[0] == '1';
     spectral_ct_init_attrs();
+    spec3_init_attrs();
     spectral_init_attrs();
     fir_init_attrs();
     fft_bench_init_attrs();
@@ -609,6 +619,8 @@ void msg_destroy(msg_ctx* ctx) {
     hipFree(ctx->d_ke); hipFree(ctx->d_we); hipFree(ctx->d_fe); hipFree(ctx->d_jump);
     for (float2* t : ctx->d_fir2tab) hipFree(t);
     for (float2* t : ctx->d_spec_ct_tab) hipFree(t);
+    hipFree(ctx->d_spec3_tab);
+    ctx->spec3_list.release();
     ctx->spec_ct_list.release();
     ctx->fir_jobs.release();
     ctx->sf_prt.release(); ctx->sf_jobs.release(); ctx->sf_irjobs.release(); ctx->sf_h.release();
@@ -995,6 +1007,13 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
     std::vector<int32_t> spec_ct[SPEC_CT_PLANS];           // events of the compile-time spectral plans
     const char* ct_env = getenv("MSGPU_SPEC_CT");         // "0": runtime-plan kernels only (tests)
     const bool use_ct = !(ct_env && ct_env[0] == '0');
+    const char* s3_env = getenv("MSGPU_SPEC3");          // "0": no band-pruned kernel (A/B, tests)
+    const bool use_s3 = use_ct && !(s3_env && s3_env[0] == '0');
+    // MSGPU_G64_STOP=cep (tests only): float64-chain grains stop before the cepstral
+    // warp (MS:696-697), so meta grain_last is that stage's input (stage-pin tests)
+    const char* stop_env = getenv("MSGPU_G64_STOP");
+    const bool stop_cep = stop_env && std::strcmp(stop_env, "cep") == 0;
+    std::vector<int32_t> spec3;                           // events of the band-pruned kernel
     std::map<std::pair<int, int>, int64_t> ir_spec_of;   // (IR index, N) -> offset
     std::vector<int2> fjobs_by[5];                        // FIR output blocks per transform size
     std::vector<int64_t> ir_jobs;                         // [ir_off, ir_len, plan, out_off] per job
@@ -1188,6 +1207,8 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
                     g64_lds.push_back((int32_t)ev64.size());
                 }
                 v.ops = g64_ops(pr, e);
+                if (stop_cep && (v.ops & G64_CEP))   // debug: the grain as cepstral_warp receives it
+                    v.ops &= G64_LOWPASS | G64_WARP | G64_CHAIN;
                 v.n = e.n;
                 v.n0 = msgplan::grain_len(e.gen_sr, pr.micro_ms, 16);
                 v.gen_sr = e.gen_sr;
@@ -1247,7 +1268,11 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
             x.warp_power = pr.nl_warp_power;
             gen_list.push_back(ei);
             const int ctp = (x.ops && use_ct) ? spectral_ct_plan(e.n) : -1;
-            if (ctp >= 0) {
+            if (use_s3 && x.ops &&
+                spec3_eligible(e.n, x.ops, x.gen_sr, x.cutoff_gen, x.roll, x.stretch, r.pool_base + e.pool_off,
+                               &x.s3_kb, &x.s3_kz, &x.s3_ky, &x.s3_inv_f)) {
+                spec3.push_back(ei);
+            } else if (ctp >= 0) {
                 spec_ct[ctp].push_back(ei);
             } else if (x.ops) {
                 std::string why;
@@ -1358,6 +1383,8 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
     }
     ct_off[SPEC_CT_PLANS] = (int32_t)ct_list.size();
     HIPCHK(ctx, ctx->spec_ct_list.ensure(ct_list.size()));
+    HIPCHK(ctx, ctx->spec3_list.ensure(spec3.size()));
+    HIPCHK(ctx, h2d(ctx->spec3_list.p, spec3.data(), sizeof(int32_t) * spec3.size()));
     HIPCHK(ctx, h2d(ctx->spec_ct_list.p, ct_list.data(), sizeof(int32_t) * ct_list.size()));
     HIPCHK(ctx, h2d(ctx->tile_begin.p, tile_begin.data(), sizeof(int32_t) * P));
     HIPCHK(ctx, h2d(ctx->fir_begin.p, fir_begin.data(), sizeof(int32_t) * P));
@@ -1391,6 +1418,9 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
     HIPCHK(ctx, hipGetLastError());
     // ---- spectral chain ----
     stage_mark(ctx, 3, s);
+    if (!spec3.empty())
+        HIPCHK(ctx, launch_spec3((unsigned)spec3.size(), s, ctx->events.p, ctx->ert.p, ctx->prt.p, ctx->d_spec3_tab,
+                                 ctx->spec3_list.p, (int)spec3.size(), ctx->micro.p, ctx->grain.p));
     for (int i = 0; i < SPEC_CT_PLANS; ++i)
         if (ct_off[i + 1] > ct_off[i])
             HIPCHK(ctx, launch_spectral_ct(i, (unsigned)(ct_off[i + 1] - ct_off[i]), s, ctx->events.p, ctx->ert.p,

@@ -62,6 +62,9 @@ struct EventRt {
     double tilt_alpha;     // log2 of the per-octave gain (MS:229-230)
     double env_tau;        // noise/skewed envelope time constant (s)
     double warp_power;     // fft_warp_power exponent (MS:103-115)
+    // band of the band-pruned spectral kernel (spec3.h, host-computed by s3_band)
+    int32_t s3_kb, s3_kz, s3_ky, s3_pad;
+    double s3_inv_f;
 };
 enum : int32_t {
     SPEC_TILT_NOISE = 1, SPEC_TILT_SKEW = 2, SPEC_LOWPASS = 4, SPEC_STRETCH = 8, SPEC_WARP = 16,

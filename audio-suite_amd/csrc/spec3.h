@@ -1,0 +1,333 @@
+// spec3.h — band-pruned, register-resident spectral chain for the hot grain
+// length of the 30 MHz configurations (n = 37500: C3, C4), TU k_spec3.hip.
+//
+// The chain of one event (MS:690-702, 719-721; lowpass_fft MS:39-59 and
+// fft_partial_stretch MS:117-128, with irfft's dropped imaginary parts between
+// the fused stages) is
+//     grain = irfft( S( W . rfft(micro) ) )
+// with W the band-limit weights (zero from bin kz up) and S the stretch
+// interpolation (Y[k] = interp(k / f, X) restricted to sources below kz).
+// At the design rate of C3/C4 the band keeps ~9 % of the bins and the
+// stretched spectrum ~19 % (f = 2) to ~38 % (f = 4), so:
+//
+//   forward  M = n/2 = 18750-point complex FFT of the packed grain in three
+//            Stockham passes (radices 25, 30, 25), registers between passes,
+//            two LDS exchanges.  Pass 1 reads the grain straight from HBM
+//            (coalesced float2), pass 3 leaves Z in registers.
+//   band     only the bins the chain keeps move through LDS: Z[k], Z[M-k] for
+//            k < kz (the real-FFT split), X[k] = split * W[k] in place.
+//   inverse  the stretch gather and the irfft packing are evaluated on the fly
+//            as inverse pass 1's inputs (zero outside the stretched band, no
+//            zero fill), then the same two exchanges, and pass 3 writes the
+//            grain straight to HBM with the 1/M scale.
+//
+// LDS traffic per event is four full exchanges plus the band (the LDS Stockham
+// kernel of spec_ct.h moves the grain through LDS ~15 times).  Exchange A
+// (pass 1 -> 2) uses the identity layout, exchange B (pass 2 -> 3) one pad slot
+// every 750 entries: both are bank-conflict-free for their strided writes and
+// unit-stride reads (ds_write_b64 16-lane groups / ds_read_b64 32-lane groups;
+// checked exhaustively by tools/lds_banks.py).
+//
+// Eligibility (host, spec3_eligible): grain length 37500, chain = band limit
+// [+ stretch] with no tilt or power warp, and the stretched band no wider than
+// M/2 (so Y[M - k] = 0 wherever Y[k] is used).  Other events keep k_spectral_ct.
+#pragma once
+#include <cmath>
+#include <vector>
+#include "kernels_spectral.h"
+
+template <int M_, int T_, int R1_, int R2_, int R3_, int PADB_>
+struct Spec3Plan {
+    static constexpr int M = M_, T = T_, R1 = R1_, R2 = R2_, R3 = R3_, PADB = PADB_;
+    static constexpr int NB1 = M / R1, NB2 = M / R2, NB3 = M / R3;
+    static constexpr int NS2 = R1, NS3 = R1 * R2;
+    static_assert(R1 * R2 * R3 == M && NS3 == NB3, "three passes");
+    static_assert(NB1 <= T && NB2 <= T && NB3 <= T, "one butterfly per thread and pass");
+    static constexpr int K = M + 1;                            // rfft bins
+    // LDS: twiddle tables at offset 0, then the exchange buffer
+    static constexpr int OFF_T2 = 0;                           // w_{NS2 R2}^{k r} at [r][k]
+    static constexpr int HI_M = (M + 127) / 128;
+    static constexpr int HI_P = (M / 2) / 128 + 2;
+    static constexpr int OFF_MLO = OFF_T2 + R2 * NS2;          // w_M^x two-level
+    static constexpr int OFF_MHI = OFF_MLO + 128;
+    static constexpr int OFF_PLO = OFF_MHI + HI_M;             // w_2M^x two-level
+    static constexpr int OFF_PHI = OFF_PLO + 128;
+    static constexpr int TAB_USED = OFF_PHI + HI_P;
+    static constexpr int TAB = (TAB_USED + 15) & ~15;
+    static constexpr int BUF = (M - 1) + ((M - 1) / NB3) * PADB + 1;
+    static constexpr int LDS_BYTES = (TAB + BUF) * 8;
+    static_assert(LDS_BYTES <= 163840, "LDS budget");
+    static MSG_HD constexpr int phB(int x) { return x + (x / NB3) * PADB; }
+};
+
+using Spec3P18750 = Spec3Plan<18750, 768, 25, 30, 25, 11>;
+
+template <class P> MSG_DEV float2 s3_wM(const float2* tab, int x) {    // exp(-2 pi i x / M)
+    return cmul(tab[P::OFF_MHI + (x >> 7)], tab[P::OFF_MLO + (x & 127)]);
+}
+template <class P> MSG_DEV float2 s3_w2M(const float2* tab, int x) {   // exp(-2 pi i x / 2M)
+    return cmul(tab[P::OFF_PHI + (x >> 7)], tab[P::OFF_PLO + (x & 127)]);
+}
+
+// Pass 1 of a transform: v = DFT_R1 of the inputs in(j + r NB1) (registers;
+// the caller writes exchange A after its barrier).
+template <class P, class In>
+MSG_DEV void s3_pass1(float2 (&v)[P::R1], int j, In&& in) {
+#pragma unroll
+    for (int r = 0; r < P::R1; ++r) v[r] = in(j + r * P::NB1);
+    Dft<P::R1, false>::run(v);
+}
+template <class P> MSG_DEV void s3_store_a(float2* buf, const float2 (&v)[P::R1], int j) {
+#pragma unroll
+    for (int r = 0; r < P::R1; ++r) buf[j * P::R1 + r] = v[r];   // exchange A, identity layout
+}
+
+// Pass 2: exchange A -> twiddle [r][k] -> DFT_R2 -> exchange B (in place).
+template <class P> MSG_DEV void s3_pass2(float2* buf, const float2* tab) {
+    constexpr int R = P::R2, NS = P::NS2, NB = P::NB2;
+    const int j = otid();
+    float2 v[R];
+    if (j < NB) {
+#pragma unroll
+        for (int r = 0; r < R; ++r) v[r] = buf[j + r * NB];
+    }
+    __syncthreads();
+    if (j < NB) {
+        const int k = j % NS, q = j / NS;
+#pragma unroll
+        for (int r = 1; r < R; ++r) v[r] = cmul(v[r], tab[P::OFF_T2 + r * NS + k]);
+        Dft<R, false>::run(v);
+        // phB(q NS R + k + r NS) = q (NS R + PADB) + k + r NS, as k + r NS < NS R = NB3:
+        // one base address, immediate offsets
+        const int o = q * (NS * R + P::PADB) + k;
+        static_assert(NS * R == P::NB3, "pass 2 writes whole exchange-B rows");
+#pragma unroll
+        for (int r = 0; r < R; ++r) buf[o + r * NS] = v[r];
+    }
+    __syncthreads();
+}
+
+// Pass 3: exchange B -> twiddle w_M^{j r} (power tree) -> DFT_R3; v[r] = Z[j + r NB3].
+template <class P> MSG_DEV void s3_pass3(const float2* buf, const float2* tab, float2 (&v)[P::R3], int j) {
+#pragma unroll
+    for (int r = 0; r < P::R3; ++r) v[r] = buf[j + r * (P::NB3 + P::PADB)];
+    twiddle_pow<P::R3>(v, s3_wM<P>(tab, j));
+    Dft<P::R3, false>::run(v);
+}
+
+// Band of one event: bins [0, kz) survive the band limit; Y = S(X) is zero from ky up.
+struct Spec3Band {
+    int kb, kz, ky;
+    double inv_f;
+    bool stretch;
+};
+// Host and device: the same float64 threshold arithmetic as Lowpass (rfftfreq, MS:46-58).
+MSG_HD int s3_first_bin(double val, double x, int K, bool strict) {
+    double g = floor(x / val);
+    int k = g < 0.0 ? 0 : (g > (double)K ? K : (int)g);
+    if (strict) {
+        while (k > 0 && (double)(k - 1) * val > x) --k;
+        while (k < K && (double)k * val <= x) ++k;
+    } else {
+        while (k > 0 && (double)(k - 1) * val >= x) --k;
+        while (k < K && (double)k * val < x) ++k;
+    }
+    return k;
+}
+MSG_HD Spec3Band s3_band(int n, int sr, double cutoff, double roll, bool stretch, double factor) {
+    const int K = n / 2 + 1;
+    const double nyq = 0.5 * (double)sr;
+    const double c = fmin(fmax(cutoff, 1.0), nyq);
+    const double r = fmax(0.0, roll);
+    const double val = 1.0 / ((double)n * (1.0 / (double)sr));
+    const double f1 = fmin(nyq, c + r);
+    const double lim = r <= 0 ? c : f1;
+    Spec3Band b;
+    b.kb = s3_first_bin(val, c, K, false);
+    b.kz = s3_first_bin(val, lim, K, true);
+    b.stretch = stretch;
+    const double f = fmax(1e-12, factor);
+    b.inv_f = 1.0 / f;
+    if (stretch) {
+        const double e = ceil((double)b.kz * f) + 2.0;
+        b.ky = e < (double)K ? (int)e : K;
+    } else {
+        b.ky = b.kz;
+    }
+    return b;
+}
+
+// LDS of the band phase: Z[k] and Z[M-k] (k < kz), then Z'[i] and Z'[M-i] (i < ky) and a zero slot
+template <class P> MSG_HD constexpr bool s3_band_fits(int kz, int ky) {
+    return ((kz + 15) & ~15) + 2 * ((ky + 15) & ~15) + 16 <= P::BUF && 2 * ((kz + 15) & ~15) <= P::BUF;
+}
+
+template <class P>
+__global__ void __launch_bounds__(P::T)
+k_spec3(const msg_event* __restrict__ events, const EventRt* __restrict__ ert, const PresetRt* __restrict__ rt,
+        const float2* __restrict__ tables, const int32_t* __restrict__ ev_list, int n_list,
+        const float* __restrict__ micro_pool, float* __restrict__ grain_pool) {
+    constexpr int M = P::M, T = P::T, K = P::K;
+    extern __shared__ __attribute__((aligned(16))) float2 lds[];
+    float2* tab = lds;
+    float2* buf = lds + P::TAB;
+    const int li = blockIdx.x;
+    if (li >= n_list) return;
+    const int ei = ev_list[li];
+    const msg_event& e = events[ei];
+    const PresetRt& pr = rt[e.preset];
+    const int64_t off = pr.pool_base + e.pool_off;   // even (n even, 16-B aligned preset regions)
+    SPEC_STAMP_INIT;
+    int j = otid();
+
+    // ---- forward pass 1: the packed grain z[i] = x[2i] + i x[2i+1] from HBM
+    // (the grain's loads are issued before the twiddle tables' so both share
+    // one memory latency)
+    {
+        const float2* z = reinterpret_cast<const float2*>(micro_pool + off);
+        float2 v[P::R1];
+        if (j < P::NB1) {
+#pragma unroll
+            for (int r = 0; r < P::R1; ++r) v[r] = z[j + r * P::NB1];
+        }
+        for (int i = threadIdx.x; i < P::TAB_USED; i += T) tab[i] = tables[i];
+        if (j < P::NB1) {
+            Dft<P::R1, false>::run(v);
+            s3_store_a<P>(buf, v, j);
+        }
+    }
+    __syncthreads();
+    SPEC_STAMP(0);
+    s3_pass2<P>(buf, tab);
+    SPEC_STAMP(1);
+
+    // ---- band (host-computed, spec3_eligible)
+    const EventRt& ex = ert[ei];
+    const int kb = ex.s3_kb, kz = ex.s3_kz, ky = ex.s3_ky;
+    const int zh = (kz + 15) & ~15;                 // Z[M - m], m < kz, at buf[zh + m]
+    const int pl = zh;                              // Z'[i], i < ky (after the split frees Z[M - m])
+    const int ph = pl + ((ky + 15) & ~15);          // Z'[M - m], 1 <= m < ky
+    const int zs = ph + ((ky + 15) & ~15);          // one zero slot
+
+    // ---- forward pass 3 -> Z in registers -> band to LDS
+    j = otid();
+    {
+        float2 v[P::R3];
+        if (j < P::NB3) s3_pass3<P>(buf, tab, v, j);
+        __syncthreads();                            // exchange B fully read
+        if (j < P::NB3) {
+#pragma unroll
+            for (int r = 0; r < P::R3; ++r) {
+                const int i = j + r * P::NB3;
+                if (i < kz) buf[i] = v[r];
+                if (M - i < kz && i > 0) buf[zh + (M - i)] = v[r];
+            }
+        }
+    }
+    __syncthreads();
+    SPEC_STAMP(2);
+    // ---- real split X[k] (k < kz) and band-limit weights (MS:48-58), in place
+    {
+        const Lowpass lpw(2 * M, ex.gen_sr, ex.cutoff_gen, ex.roll);
+        for (int k = otid(); k < kz; k += T) {
+            float2 x;
+            if (k == 0) {
+                const float2 z0 = buf[0];
+                x = make_float2(z0.x + z0.y, 0.f);   // DC (imag dropped: drop_edge_imag)
+            } else {
+                const float2 zk = buf[k], zm = buf[zh + k];
+                const float2 w = s3_w2M<P>(tab, k);
+                const float2 ee = make_float2(0.5f * (zk.x + zm.x), 0.5f * (zk.y - zm.y));
+                const float2 d = make_float2(zk.x - zm.x, zk.y + zm.y);
+                const float2 wo = cmul(w, make_float2(0.5f * d.y, -0.5f * d.x));
+                x = cadd(ee, wo);
+            }
+            if (k >= kb) {
+                const float wk = lpw.w(k);
+                if (wk != 1.f) x = cscale(x, wk);
+            }
+            buf[k] = x;
+        }
+    }
+    __syncthreads();
+    SPEC_STAMP(3);
+    // ---- stretch gather Y = S(X) (MS:117-128) and the irfft packing of bins k
+    // and M - k (Y[M - k] = 0 in the band), conjugated for the forward engine
+    // (inverse = conj . F . conj): inverse pass 1's nonzero inputs
+    {
+        const bool stretch = (ex.ops & SPEC_STRETCH) != 0;
+        const double inv_f = ex.s3_inv_f;
+        for (int k = otid(); k < ky; k += T) {
+            float2 y;
+            if (!stretch) {
+                y = buf[k];
+            } else {
+                const double xs = (double)k * inv_f;
+                y = make_float2(0.f, 0.f);
+                if (xs >= 0.0 && xs <= (double)(K - 1) && xs < (double)kz) {
+                    const int j0 = (int)xs;
+                    const float fr = (float)(xs - (double)j0);
+                    const float2 a = buf[j0];
+                    const float2 b = j0 + 1 < kz ? buf[j0 + 1] : make_float2(0.f, 0.f);
+                    y = make_float2((b.x - a.x) * fr + a.x, (b.y - a.y) * fr + a.y);
+                }
+            }
+            if (k == 0) {
+                buf[pl] = make_float2(0.5f * y.x, -0.5f * y.x);   // imag of Y[0] ignored; Y[M] = 0
+                buf[zs] = make_float2(0.f, 0.f);
+            } else {
+                const float2 w = s3_w2M<P>(tab, k);
+                const float2 e1 = cscale(y, 0.5f);
+                const float2 o1 = cscale(cmulc(y, w), 0.5f);
+                buf[pl + k] = make_float2(e1.x - o1.y, -(e1.y + o1.x));
+                buf[ph + k] = make_float2(e1.x + o1.y, e1.y - o1.x);
+            }
+        }
+    }
+    __syncthreads();
+    // ---- inverse pass 1 (inputs zero outside the stretched band)
+    j = otid();
+    {
+        float2 v[P::R1];
+        if (j < P::NB1)
+            s3_pass1<P>(v, j, [&](int i) {
+                const int at = i < ky ? pl + i : (M - i < ky ? ph + (M - i) : zs);
+                return buf[at];
+            });
+        __syncthreads();                            // band fully read
+        if (j < P::NB1) s3_store_a<P>(buf, v, j);
+    }
+    __syncthreads();
+    SPEC_STAMP(4);
+    s3_pass2<P>(buf, tab);
+    SPEC_STAMP(5);
+    // ---- inverse pass 3 -> grain (x[2i] = Re z / M, x[2i+1] = -Im z / M) to HBM
+    j = otid();
+    if (j < P::NB3) {
+        float2 v[P::R3];
+        s3_pass3<P>(buf, tab, v, j);
+        float2* g = reinterpret_cast<float2*>(grain_pool + off);
+        const float s = 1.0f / (float)M;
+#pragma unroll
+        for (int r = 0; r < P::R3; ++r) g[j + r * P::NB3] = make_float2(v[r].x * s, -v[r].y * s);
+    }
+    SPEC_STAMP(6);
+}
+
+// Host: twiddle tables (float64-built, rounded once).
+template <class P>
+inline void spec3_tables(std::vector<float>& out) {
+    out.assign(2 * (size_t)P::TAB_USED, 0.f);
+    const long double PI = 3.14159265358979323846264338327950288L;
+    auto put = [&](int at, long double num, long double den) {
+        const long double a = -2.0L * PI * num / den;
+        out[2 * at] = (float)cosl(a);
+        out[2 * at + 1] = (float)sinl(a);
+    };
+    for (int r = 0; r < P::R2; ++r)
+        for (int k = 0; k < P::NS2; ++k) put(P::OFF_T2 + r * P::NS2 + k, (long double)k * r, (long double)P::NS2 * P::R2);
+    for (int x = 0; x < 128; ++x) put(P::OFF_MLO + x, x, P::M);
+    for (int x = 0; x < P::HI_M; ++x) put(P::OFF_MHI + x, 128.0L * x, P::M);
+    for (int x = 0; x < 128; ++x) put(P::OFF_PLO + x, x, 2.0L * P::M);
+    for (int x = 0; x < P::HI_P; ++x) put(P::OFF_PHI + x, 128.0L * x, 2.0L * P::M);
+}

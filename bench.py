@@ -146,8 +146,17 @@ def cpu_baseline(cfg, budget_s):
     wall = time.perf_counter() - t0
     pdone = sum(r[0] for r in res)
     pframes = sum(r[1] for r in res)
+    # one C2 preset on one core: the per-render time the drop-in is compared with
+    from oracle import msound_oracle as O
+    p2 = msgpu_config("C2")
+    c2 = []
+    for _ in range(3):
+        t1 = time.perf_counter()
+        O.render(p2)
+        c2.append(time.perf_counter() - t1)
     return {"value": pframes / wall / 1e6, "unit": "Msamples/s", "cores": procs, "kind": "port",
             "single_core": round(single, 4),
+            "per_render_ms_1core": {"C2": round(1e3 * float(np.median(c2)), 2), cfg: round(1e3 * dt / done, 2)},
             "sample": f"{cfg} presets rendered by oracle/msound_oracle.py (NumPy restatement of "
                       f"main_v2.render): {done} presets on 1 core in {dt:.1f} s "
                       f"({single:.3f} Msamples/s), then {pdone} presets on {procs} processes in "
@@ -156,6 +165,34 @@ def cpu_baseline(cfg, budget_s):
 
 # ---------------------------------------------------------------------------
 # sharding
+def msgpu_config(cfg, seed=1000):
+    import msgpu
+    return msgpu.config_params(cfg, seed=seed, irs=load_irs())
+
+
+def dropin_latency(cpu, reps=5):
+    """msgpu.render() of one preset, end to end as the unchanged UI calls it
+    (MS:811): dict checks and packing, host plan, enqueue, device render, D2H copy
+    of the (out_n, 2) float32 buffer and meta -- beside the CPU per-render time."""
+    import msgpu
+    out = {}
+    for cfg in ("C2", "C3"):
+        p = msgpu_config(cfg)
+        msgpu.render(p)                                    # warm (plans, buffers)
+        ts = []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            msgpu.render(p)
+            ts.append(time.perf_counter() - t0)
+        rec = {"gpu_ms": round(1e3 * float(np.median(ts)), 3), "reps": reps}
+        c = (cpu or {}).get("per_render_ms_1core", {}).get(cfg)
+        if c:
+            rec["cpu_ms_1core"] = c
+            rec["speedup"] = round(c / rec["gpu_ms"], 1)
+        out[cfg] = rec
+    return out
+
+
 def rank_seeds(rank, batch):
     """Preset seeds of one rank: contiguous, disjoint across ranks (weak scaling)."""
     return [1000 + rank * batch + b for b in range(batch)]
@@ -557,6 +594,7 @@ def main():
             pb = default_batch(pc, args)
             points[pc] = measure(runner, pc, rank_seeds(rank, pb), default_sub(pc, args, pb), args.point_steps,
                                  1, comm, irs, golden)
+        lat = dropin_latency(cpu) if (rank == 0 and world == 1 and not args.no_cpu) else None
         ranks = comm.gather({"rank": rank, "pid": os.getpid(), "device": local,
                              "seeds": [seeds[0], seeds[-1]], "elapsed_s": round(head["_rank_s"], 6),
                              "frames": head["frames_per_gpu_step"] * args.steps})
@@ -580,6 +618,7 @@ def main():
                 "design_msamples_per_s": head["design_msamples_per_s"],
                 "checked": head["check"],
                 "cpu_baseline": cpu,
+                "dropin_latency": lat,
                 "points": points,
                 "ranks": ranks,
             }
