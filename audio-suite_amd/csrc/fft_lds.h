@@ -225,8 +225,9 @@ MSG_DEV int otid() {
 }
 
 // One forward Stockham pass of radix R over buf[0..size), Ns = product of the
-// earlier radices.  Twiddles w^r for r < R come from w, w^2, w^3, w^4 and a
-// running power of w^4 (five live values, product depth <= R/4 + 2).
+// earlier radices.  Twiddles w^r for r < R come from w, w^2, w^3, w^4 (w and
+// w^4 from the table) and a running power of w^4 (five live values, product
+// depth <= R/4 + 2).
 template <int R, int T, int MAXM>
 MSG_DEV void stockham_pass(float2* buf, int size, int Ns, const TwLds& tw) {
     constexpr int BMAX = (MAXM + R * T - 1) / (R * T);
@@ -251,10 +252,12 @@ MSG_DEV void stockham_pass(float2* buf, int size, int Ns, const TwLds& tw) {
             const int q = fdiv(j, Ns, inv_ns);
             const int k = j - q * Ns;
             if (k != 0) {
+                // w^4 read from the table, not squared twice: a power carries its
+                // base's rounding error times the exponent (see twiddle_pow_ab)
                 const float2 w1 = tw_at(tw, k * stride);
                 const float2 w2 = cmul(w1, w1);
                 const float2 w3 = cmul(w2, w1);
-                const float2 w4 = cmul(w2, w2);
+                const float2 w4 = R > 4 ? tw_at(tw, 4 * k * stride) : cmul(w2, w2);
                 float2 pw = make_float2(1.f, 0.f);   // w^(4a)
 #pragma unroll
                 for (int r = 1; r < R; ++r) {
@@ -445,6 +448,33 @@ MSG_DEV void rtransform(float2* buf, const RealPlan& rp, const TwLds& tw, bool i
 }
 
 // v[r] *= w^r for r < R, powers by a balanced product tree (depth <= 2 log2 R)
+// v[r] *= w^r for r < R from two table values w1 = w and wB = w^B (B ~ sqrt R):
+// w^r = wB^(r / B) * w1^(r % B).  A power of a rounded twiddle carries r times
+// its rounding error (twiddle_pow below: up to 31x for R = 32); here no factor
+// is raised beyond ~sqrt R, which keeps the FIR and spectral transforms within
+// ~2x of a float32 FFT with exact twiddles (pocketfft) instead of ~3.5x.
+template <int R, int B>
+MSG_DEV void twiddle_pow_ab(float2 (&v)[R], float2 w1, float2 wB) {
+    constexpr int A = (R + B - 1) / B;
+    float2 p1[B], pb[A];
+    p1[0] = make_float2(1.f, 0.f);
+    p1[1 % B] = w1;
+#pragma unroll
+    for (int b = 2; b < B; ++b) p1[b] = (b % 2 == 0) ? cmul(p1[b / 2], p1[b / 2]) : cmul(p1[b - 1], w1);
+    pb[0] = make_float2(1.f, 0.f);
+    if (A > 1) pb[1] = wB;
+#pragma unroll
+    for (int a = 2; a < A; ++a) pb[a] = (a % 2 == 0) ? cmul(pb[a / 2], pb[a / 2]) : cmul(pb[a - 1], wB);
+#pragma unroll
+    for (int r = 1; r < R; ++r) {
+        const int a = r / B, b = r % B;
+        if (a == 0) v[r] = cmul(v[r], p1[b]);
+        else if (b == 0) v[r] = cmul(v[r], pb[a]);
+        else v[r] = cmul(v[r], cmul(pb[a], p1[b]));
+    }
+}
+template <int R> constexpr int tw_base() { return R <= 4 ? R : (R <= 9 ? 3 : (R <= 16 ? 4 : (R <= 25 ? 5 : 6))); }
+
 template <int R>
 MSG_DEV void twiddle_pow(float2 (&v)[R], float2 w) {
     float2 p[R];

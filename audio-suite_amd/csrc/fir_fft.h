@@ -240,7 +240,8 @@ k_fir2(const PresetRt* __restrict__ rt, const int2* __restrict__ jobs, const flo
         __syncthreads();   // LDS free for the next segment / the inverse
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
-            twiddle_pow<R3>(v[h], fir_wM(tab, G::OFF_MLO, G::OFF_MHI, js[h]));
+            twiddle_pow_ab<R3, tw_base<R3>()>(v[h], fir_wM(tab, G::OFF_MLO, G::OFF_MHI, js[h]),
+                                              fir_wM(tab, G::OFF_MLO, G::OFF_MHI, (js[h] * tw_base<R3>()) & (M - 1)));
             Dft<R3, false>::run(v[h]);
         }
         // ---- real split, X . H_q accumulated in registers (slot layout, fir_slots)
@@ -312,7 +313,8 @@ k_fir2(const PresetRt* __restrict__ rt, const int2* __restrict__ jobs, const flo
         const int base = padx<G::SD>(j);
 #pragma unroll
         for (int r = 0; r < R1; ++r) v[r] = buf[base + padx<G::SD>(r * NB1)];
-        twiddle_pow<R1>(v, fir_wM(tab, G::OFF_MLO, G::OFF_MHI, j));
+        twiddle_pow_ab<R1, tw_base<R1>()>(v, fir_wM(tab, G::OFF_MLO, G::OFF_MHI, j),
+                                          fir_wM(tab, G::OFF_MLO, G::OFF_MHI, (j * tw_base<R1>()) & (M - 1)));
         Dft<R1, false>::run(v);
 #pragma unroll
         for (int r = 0; r < R1; ++r) {
@@ -397,7 +399,8 @@ k_fdl_fwd(const PresetRt* __restrict__ rt, const int2* __restrict__ jobs, const 
     }
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-        twiddle_pow<R3>(v[h], fir_wM(tab, G::OFF_MLO, G::OFF_MHI, js[h]));
+        twiddle_pow_ab<R3, tw_base<R3>()>(v[h], fir_wM(tab, G::OFF_MLO, G::OFF_MHI, js[h]),
+                                          fir_wM(tab, G::OFF_MLO, G::OFF_MHI, (js[h] * tw_base<R3>()) & (M - 1)));
         Dft<R3, false>::run(v[h]);
     }
     float2 a[R3], bb[R3];

@@ -12,6 +12,7 @@
 #include <cstring>
 #include <map>
 #include <atomic>
+#include <chrono>
 #include <condition_variable>
 #include <functional>
 #include <memory>
@@ -98,7 +99,7 @@ class HostPool {
 
   private:
     HostPool() {
-        int n = 8;
+        int n = 16;                                   // the GPU box's CPU share per job
         if (const char* e = getenv("MSGPU_HOST_THREADS")) n = atoi(e);
         const int hw = (int)std::thread::hardware_concurrency();
         if (hw > 0) n = std::min(n, hw);
@@ -133,26 +134,37 @@ class HostPool {
     bool stop_ = false;
 };
 
-// Pinned staging for a batch's host -> device uploads.  Two slots alternate
-// between batches; a slot is refilled only after the copies that read it (two
-// batches back) have run, so msg_render_batch never waits on the render
-// stream and every copy is a true asynchronous DMA from pinned memory.
+// Pinned staging for a batch's host -> device uploads.  Every per-batch input
+// (presets, events, runtime records, job lists, IR bank ...) is packed into one
+// pinned slot and moved by ONE copy into a device arena; each input's device
+// pointer is then set to its place in the arena.  (One copy per input cost ~35
+// copy-engine blits per batch, ~2 ms of GPU time per C3 sub-batch.)  Two pinned
+// slots alternate between batches; a slot is refilled only after the copy that
+// read it (two batches back) has run, so msg_render_batch never waits on the
+// render stream.  The arena itself is reused in stream order.
 struct Staging {
-    struct Item { void* dst; const void* src; size_t bytes; };
+    struct Item { void** slot; const void* src; size_t bytes; };
     struct Slot { char* host = nullptr; size_t cap = 0; hipEvent_t done = nullptr; bool armed = false; };
     Slot slot[2];
     int cur = 0;
+    char* arena = nullptr;
+    size_t arena_cap = 0;
     std::vector<Item> items;
-    void add(void* dst, const void* src, size_t bytes) {
-        if (bytes) items.push_back(Item{dst, src, bytes});
+    template <class T> void add(T** dst, const T* src, size_t bytes) {
+        items.push_back(Item{reinterpret_cast<void**>(dst), src, bytes});
     }
     hipError_t flush(hipStream_t s) {
         Slot& sl = slot[cur];
         hipError_t e = hipSuccess;
         if (!sl.done) e = hipEventCreateWithFlags(&sl.done, hipEventDisableTiming);
         if (e == hipSuccess && sl.armed) e = hipEventSynchronize(sl.done);
+        std::vector<size_t> at(items.size());
         size_t total = 0;
-        for (const Item& it : items) total += (it.bytes + 255) & ~size_t(255);
+        for (size_t i = 0; i < items.size(); ++i) {
+            at[i] = total;
+            total += (items[i].bytes + 255) & ~size_t(255);
+        }
+        total = std::max<size_t>(total, 256);
         if (e == hipSuccess && total > sl.cap) {
             if (sl.host) hipHostFree(sl.host);
             sl.host = nullptr;
@@ -161,13 +173,29 @@ struct Staging {
             e = hipHostMalloc((void**)&sl.host, want, hipHostMallocDefault);
             if (e == hipSuccess) sl.cap = want;
         }
-        size_t off = 0;
-        for (const Item& it : items) {
-            if (e != hipSuccess) break;
-            std::memcpy(sl.host + off, it.src, it.bytes);
-            e = hipMemcpyAsync(it.dst, sl.host + off, it.bytes, hipMemcpyHostToDevice, s);
-            off += (it.bytes + 255) & ~size_t(255);
+        if (e == hipSuccess && total > arena_cap) {     // growth frees the old arena (hipFree waits)
+            if (arena) hipFree(arena);
+            arena = nullptr;
+            arena_cap = 0;
+            const size_t want = total + total / 4 + 4096;
+            e = hipMalloc((void**)&arena, want);
+            if (e == hipSuccess) arena_cap = want;
         }
+        if (e == hipSuccess) {   // pack in 1 MiB pieces on the host pool (C5: ~100 MB per sub-batch)
+            constexpr size_t PIECE = size_t(1) << 20;
+            std::vector<std::pair<size_t, size_t>> pieces;   // (item, byte offset in item)
+            for (size_t i = 0; i < items.size(); ++i)
+                for (size_t b = 0; b < items[i].bytes; b += PIECE) pieces.emplace_back(i, b);
+            HostPool::get().run((int)pieces.size(), [&](int k) {
+                const Item& it = items[pieces[k].first];
+                const size_t b = pieces[k].second;
+                std::memcpy(sl.host + at[pieces[k].first] + b, (const char*)it.src + b, std::min(PIECE, it.bytes - b));
+            });
+            size_t used = 0;
+            for (size_t i = 0; i < items.size(); ++i) used = at[i] + items[i].bytes;
+            if (used) e = hipMemcpyAsync(arena, sl.host, used, hipMemcpyHostToDevice, s);
+        }
+        for (size_t i = 0; i < items.size(); ++i) *items[i].slot = e == hipSuccess ? arena + at[i] : nullptr;
         if (e == hipSuccess) e = hipEventRecord(sl.done, s);
         sl.armed = e == hipSuccess;
         items.clear();
@@ -180,8 +208,14 @@ struct Staging {
             if (sl.host) hipHostFree(sl.host);
             sl = Slot();
         }
+        if (arena) hipFree(arena);
+        arena = nullptr;
+        arena_cap = 0;
     }
 };
+
+// A per-batch input living in the Staging arena (set at each flush).
+template <class T> struct Slice { T* p = nullptr; };
 
 template <class P>
 struct PlanStoreT {
@@ -208,6 +242,8 @@ struct msg_ctx {
     int ev_cur = 0;
     double stage_sum[10] = {0};   // accumulated stage times since msg_set_profiling(ctx, 1)
     int64_t stage_cnt = 0;
+    double host_sum[3] = {0};     // host wall clock per batch: plan, records, pinned upload
+    int64_t host_cnt = 0;
     hipEvent_t ev[2][10] = {};
     bool device_plan = false;     // MSGPU_DEVICE_PLAN=1: plan on the device (k_plan_*), read back
     Staging staging;              // pinned uploads of a batch
@@ -218,38 +254,44 @@ struct msg_ctx {
     float2* d_fir2tab[5] = {};   // k_fir2 twiddle tables, M = 1024 << i
     float2* d_spec_ct_tab[SPEC_CT_PLANS] = {};   // compile-time spectral plans (spec_ct.h)
     float2* d_spec3_tab = nullptr;               // band-pruned spectral kernel (spec3.h)
-    DevBuf<int32_t> spec3_list;
+    Slice<int32_t> spec3_list;
     nprng::Zig dzig{};
     PlanStore grain_plans, fir_plans;
     // per-batch buffers
-    DevBuf<msg_preset> presets;
+    // device planner (MSGPU_DEVICE_PLAN=1)
+    DevBuf<msg_preset> dp_presets;
     DevBuf<int64_t> frag_len;
     DevBuf<msg_plan_info> info;
     DevBuf<int32_t> slot_base, tap_base;
-    DevBuf<msg_event> events;
-    DevBuf<int32_t> er_off;
-    DevBuf<double> er_gain;
-    DevBuf<EventRt> ert;
-    DevBuf<PresetRt> prt;
-    DevBuf<int32_t> gen_list, spec_small, spec_big, tile_begin, fir_begin, h_begin, st_begin, fir_plan_of;
+    DevBuf<msg_event> dp_events;
+    DevBuf<int32_t> dp_er_off;
+    DevBuf<double> dp_er_gain;
+    // per-batch inputs, uploaded in one copy (Staging arena)
+    Slice<msg_preset> presets;
+    Slice<msg_event> events;
+    Slice<int32_t> er_off;
+    Slice<double> er_gain;
+    Slice<EventRt> ert;
+    Slice<PresetRt> prt;
+    Slice<int32_t> gen_list, spec_small, spec_big, tile_begin, fir_begin, h_begin, st_begin, fir_plan_of;
     DevBuf<float> micro, grain, mono_a, mono_y;
     DevBuf<float2> hspec, irspec;
     DevBuf<float> hscratch;                     // h of ER + IR presets (k_fir_hconv -> k_fir_h)
-    DevBuf<int32_t> conv_list;
-    DevBuf<int2> fir_jobs;
-    DevBuf<int32_t> spec_ct_list;
-    DevBuf<int64_t> irjobs;
-    DevBuf<double> irbank;
+    Slice<int32_t> conv_list;
+    Slice<int2> fir_jobs;
+    Slice<int32_t> spec_ct_list;
+    Slice<int64_t> irjobs;
+    Slice<double> irbank;
     DevBuf<unsigned> maxbits;
     // float64 grain chain (kernels_grain64.h)
     Plan64Store plans64;
-    DevBuf<Ev64> ev64;
-    DevBuf<int32_t> g64_list, gen64_list;
-    DevBuf<int64_t> gen64_off;
+    Slice<Ev64> ev64;
+    Slice<int32_t> g64_list, gen64_list;
+    Slice<int64_t> gen64_off;
     DevBuf<double> micro64, grain64, state64;
     DevBuf<double2> save64;
-    DevBuf<Chain64> chains;
-    DevBuf<uint8_t> imgbank;
+    Slice<Chain64> chains;
+    Slice<uint8_t> imgbank;
     DevBuf<double2> g64A, g64B;                 // global-class float64 grains (G64Global)
     DevBuf<uint32_t> g64mask;
     // standalone FIR (msg_fir): its own buffers, so it never touches a render batch's
@@ -265,6 +307,8 @@ struct msg_ctx {
     // host mirrors of the last batch
     std::vector<msg_plan_info> h_info;
     std::vector<msg_event> h_events;
+    std::unique_ptr<EventRt[]> h_ert;   // host EventRt records (grow-only, msg_render_batch)
+    size_t h_ert_cap = 0;
     std::vector<int32_t> h_er_off;
     std::vector<double> h_er_gain;
     std::vector<PresetRt> h_prt;
@@ -620,28 +664,19 @@ void msg_destroy(msg_ctx* ctx) {
     for (float2* t : ctx->d_fir2tab) hipFree(t);
     for (float2* t : ctx->d_spec_ct_tab) hipFree(t);
     hipFree(ctx->d_spec3_tab);
-    ctx->spec3_list.release();
-    ctx->spec_ct_list.release();
-    ctx->fir_jobs.release();
     ctx->sf_prt.release(); ctx->sf_jobs.release(); ctx->sf_irjobs.release(); ctx->sf_h.release();
     ctx->sf_hspec.release(); ctx->sf_xspec.release();
     for (auto& set : ctx->ev)
         for (auto& ev : set) hipEventDestroy(ev);
     ctx->staging.release();
-    ctx->presets.release(); ctx->frag_len.release(); ctx->info.release(); ctx->slot_base.release();
-    ctx->tap_base.release(); ctx->events.release(); ctx->er_off.release(); ctx->er_gain.release();
-    ctx->ert.release(); ctx->prt.release(); ctx->gen_list.release(); ctx->spec_small.release();
-    ctx->spec_big.release(); ctx->tile_begin.release(); ctx->fir_begin.release(); ctx->h_begin.release();
-    ctx->st_begin.release(); ctx->fir_plan_of.release(); ctx->micro.release(); ctx->grain.release();
+    ctx->dp_presets.release(); ctx->frag_len.release(); ctx->info.release(); ctx->slot_base.release();
+    ctx->tap_base.release(); ctx->dp_events.release(); ctx->dp_er_off.release(); ctx->dp_er_gain.release();
+    ctx->micro.release(); ctx->grain.release();
     ctx->mono_a.release(); ctx->mono_y.release(); ctx->hspec.release(); ctx->irspec.release();
-    ctx->hscratch.release(); ctx->conv_list.release();
-    ctx->irjobs.release(); ctx->irbank.release();
-    ctx->maxbits.release();
+    ctx->hscratch.release(); ctx->maxbits.release();
     for (void* p : ctx->plans64.allocs) hipFree(p);
     ctx->plans64.dev.release();
-    ctx->ev64.release(); ctx->g64_list.release(); ctx->gen64_list.release(); ctx->gen64_off.release();
     ctx->micro64.release(); ctx->grain64.release(); ctx->state64.release(); ctx->save64.release();
-    ctx->chains.release(); ctx->imgbank.release();
     ctx->g64A.release(); ctx->g64B.release(); ctx->g64mask.release();
     for (auto& kv : ctx->so_bp) kv.second.release();
     ctx->so_A.release(); ctx->so_r2.release();
@@ -678,7 +713,9 @@ int msg_set_profiling(msg_ctx* ctx, int32_t on) {
     ctx->profiling = on != 0;
     if (ctx->profiling) {
         for (double& v : ctx->stage_sum) v = 0.0;
+        for (double& v : ctx->host_sum) v = 0.0;
         ctx->stage_cnt = 0;
+        ctx->host_cnt = 0;
     }
     return MSG_OK;
 }
@@ -688,6 +725,8 @@ int msg_stage_times(msg_ctx* ctx, float* ms, int32_t n) {
     collect_stage_times(ctx);
     for (int i = 0; i < n && i < 10; ++i)
         ms[i] = ctx->stage_cnt ? (float)(ctx->stage_sum[i] / (double)ctx->stage_cnt) : 0.f;
+    for (int i = 10; i < n && i < 13; ++i)
+        ms[i] = ctx->host_cnt ? (float)(ctx->host_sum[i - 10] / (double)ctx->host_cnt) : 0.f;
     return MSG_OK;
 }
 
@@ -912,12 +951,13 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
         if (ic >= n_irs || (ic >= 0 && !irs)) return fail(ctx, MSG_E_ARG, "bad IR index");
     }
     stage_mark(ctx, 0, s);
+    using hclock = std::chrono::steady_clock;
+    const auto h0 = hclock::now();
     std::vector<int64_t> flen(P, 0);
     for (int p = 0; p < P; ++p) {
         const int f = presets[p].ir_frag;
         flen[p] = (f >= 0 && f < n_irs) ? ir_lens[f] : 0;
     }
-    HIPCHK(ctx, ctx->presets.ensure(P));
     std::vector<msg_plan_info> info(P);
     std::vector<int32_t> slot_base(P), tap_base(P);
     int64_t nslots = 0, ntaps = 0;
@@ -947,22 +987,17 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
                                  er ? ctx->h_er_off.data() + tap_base[p] : nullptr,
                                  er ? ctx->h_er_gain.data() + tap_base[p] : nullptr);
         });
-        HIPCHK(ctx, ctx->events.ensure(nslots));
-        HIPCHK(ctx, ctx->er_off.ensure(ntaps));
-        HIPCHK(ctx, ctx->er_gain.ensure(ntaps));
-        ctx->staging.add(ctx->presets.p, presets, sizeof(msg_preset) * P);
-        ctx->staging.add(ctx->events.p, ctx->h_events.data(), sizeof(msg_event) * nslots);
-        ctx->staging.add(ctx->er_off.p, ctx->h_er_off.data(), sizeof(int32_t) * ntaps);
-        ctx->staging.add(ctx->er_gain.p, ctx->h_er_gain.data(), sizeof(double) * ntaps);
+
     } else {
         // ---- device plan, phase 1: sizes ----
         HIPCHK(ctx, ctx->frag_len.ensure(P));
         HIPCHK(ctx, ctx->info.ensure(P));
-        HIPCHK(ctx, hipMemcpyAsync(ctx->presets.p, presets, sizeof(msg_preset) * P, hipMemcpyHostToDevice, s));
+        HIPCHK(ctx, ctx->dp_presets.ensure(P));
+        HIPCHK(ctx, hipMemcpyAsync(ctx->dp_presets.p, presets, sizeof(msg_preset) * P, hipMemcpyHostToDevice, s));
         HIPCHK(ctx, hipMemcpyAsync(ctx->frag_len.p, flen.data(), sizeof(int64_t) * P, hipMemcpyHostToDevice, s));
         const int pb = 64;
         hipLaunchKernelGGL(k_plan_sizes, dim3((P + pb - 1) / pb), dim3(pb), 0, s,
-                           ctx->presets.p, P, ctx->frag_len.p, ctx->dzig, ctx->info.p);
+                           ctx->dp_presets.p, P, ctx->frag_len.p, ctx->dzig, ctx->info.p);
         HIPCHK(ctx, hipGetLastError());
         HIPCHK(ctx, hipMemcpyAsync(info.data(), ctx->info.p, sizeof(msg_plan_info) * P, hipMemcpyDeviceToHost, s));
         HIPCHK(ctx, hipStreamSynchronize(s));
@@ -970,27 +1005,47 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
         if (int st = bases()) return st;
         HIPCHK(ctx, ctx->slot_base.ensure(P));
         HIPCHK(ctx, ctx->tap_base.ensure(P));
-        HIPCHK(ctx, ctx->events.ensure(nslots));
-        HIPCHK(ctx, ctx->er_off.ensure(ntaps));
-        HIPCHK(ctx, ctx->er_gain.ensure(ntaps));
+        HIPCHK(ctx, ctx->dp_events.ensure(nslots));
+        HIPCHK(ctx, ctx->dp_er_off.ensure(ntaps));
+        HIPCHK(ctx, ctx->dp_er_gain.ensure(ntaps));
         HIPCHK(ctx, hipMemcpyAsync(ctx->slot_base.p, slot_base.data(), sizeof(int32_t) * P, hipMemcpyHostToDevice, s));
         HIPCHK(ctx, hipMemcpyAsync(ctx->tap_base.p, tap_base.data(), sizeof(int32_t) * P, hipMemcpyHostToDevice, s));
         hipLaunchKernelGGL(k_plan_events, dim3((P + pb - 1) / pb), dim3(pb), 0, s,
-                           ctx->presets.p, P, ctx->frag_len.p, ctx->dzig, ctx->slot_base.p, ctx->tap_base.p,
-                           ctx->events.p, ctx->er_off.p, ctx->er_gain.p, ctx->info.p);
+                           ctx->dp_presets.p, P, ctx->frag_len.p, ctx->dzig, ctx->slot_base.p, ctx->tap_base.p,
+                           ctx->dp_events.p, ctx->dp_er_off.p, ctx->dp_er_gain.p, ctx->info.p);
         HIPCHK(ctx, hipGetLastError());
         ctx->h_events.resize(nslots);
         HIPCHK(ctx, hipMemcpyAsync(info.data(), ctx->info.p, sizeof(msg_plan_info) * P, hipMemcpyDeviceToHost, s));
         if (nslots)
-            HIPCHK(ctx, hipMemcpyAsync(ctx->h_events.data(), ctx->events.p, sizeof(msg_event) * nslots,
+            HIPCHK(ctx, hipMemcpyAsync(ctx->h_events.data(), ctx->dp_events.p, sizeof(msg_event) * nslots,
                                        hipMemcpyDeviceToHost, s));
+        ctx->h_er_off.resize(ntaps);
+        ctx->h_er_gain.resize(ntaps);
+        if (ntaps) {
+            HIPCHK(ctx, hipMemcpyAsync(ctx->h_er_off.data(), ctx->dp_er_off.p, sizeof(int32_t) * ntaps,
+                                       hipMemcpyDeviceToHost, s));
+            HIPCHK(ctx, hipMemcpyAsync(ctx->h_er_gain.data(), ctx->dp_er_gain.p, sizeof(double) * ntaps,
+                                       hipMemcpyDeviceToHost, s));
+        }
         HIPCHK(ctx, hipStreamSynchronize(s));
     }
     stage_mark(ctx, 1, s);
+    const auto h1 = hclock::now();
+    ctx->staging.add(&ctx->presets.p, presets, sizeof(msg_preset) * P);
+    ctx->staging.add(&ctx->events.p, ctx->h_events.data(), sizeof(msg_event) * nslots);
+    ctx->staging.add(&ctx->er_off.p, ctx->h_er_off.data(), sizeof(int32_t) * ntaps);
+    ctx->staging.add(&ctx->er_gain.p, ctx->h_er_gain.data(), sizeof(double) * ntaps);
 
     // ---- host: runtime records ----
     std::vector<PresetRt> prt(P);
-    std::vector<EventRt> ert(nslots);
+    // host EventRt records: a grow-only buffer reused across batches (a C5 sub-batch
+    // holds 512 k events; a fresh zero-filled vector cost ~8 ms of page faults and
+    // memset per batch).  Every slot an event list references is written below.
+    if ((size_t)nslots > ctx->h_ert_cap) {
+        ctx->h_ert.reset(new EventRt[(size_t)nslots + nslots / 4]);
+        ctx->h_ert_cap = (size_t)nslots + nslots / 4;
+    }
+    EventRt* const ert = ctx->h_ert.get();
     std::vector<int32_t> gen_list, spec_small, spec_big, tile_begin(P), fir_begin(P), h_begin(P), st_begin(P),
         fir_plan_of(P, 0);
     std::vector<double> irbank;
@@ -1014,6 +1069,7 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
     const char* stop_env = getenv("MSGPU_G64_STOP");
     const bool stop_cep = stop_env && std::strcmp(stop_env, "cep") == 0;
     std::vector<int32_t> spec3;                           // events of the band-pruned kernel
+    std::vector<int32_t> f32_presets;                     // presets on the float32 chain
     std::map<std::pair<int, int>, int64_t> ir_spec_of;   // (IR index, N) -> offset
     std::vector<int2> fjobs_by[5];                        // FIR output blocks per transform size
     std::vector<int64_t> ir_jobs;                         // [ir_off, ir_len, plan, out_off] per job
@@ -1163,9 +1219,12 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
         if (!precise) {
             // grains beyond the LDS-resident float32 spectral kernels run the float64
             // chain in global memory (micro_ms up to 80 ms at 30 MHz: 2.4 M samples)
+            int last_n = -1;
             for (int k = 0; k < inf.n_events && !precise; ++k) {
                 const msg_event& e = ctx->h_events[slot_base[p] + k];
-                if (!spec_ops(pr, e) || (use_ct && spectral_ct_plan(e.n) >= 0)) continue;
+                if (!spec_ops(pr, e) || e.n == last_n) continue;   // each spectral grain length once
+                last_n = e.n;
+                if (use_ct && spectral_ct_plan(e.n) >= 0) continue;
                 std::string why;
                 const int pi = real_plan(ctx->grain_plans, e.n, why);
                 if (pi < 0) return fail(ctx, MSG_E_DEVICE, "grain plan: " + why);
@@ -1251,7 +1310,25 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
             }
             continue;
         }
-        for (int k = 0; k < inf.n_events; ++k) {
+        f32_presets.push_back(p);
+    }
+    // ---- float32-chain event records (EventRt), presets in parallel on the host
+    // pool; the per-kernel event lists are concatenated in preset order.  Events
+    // that need a runtime FFT plan (no compile-time plan for their length) are
+    // planned afterwards on this thread (the plan cache is not shared).
+    struct F32Lists { std::vector<int32_t> gen, s3, ct[SPEC_CT_PLANS], small, pending; };
+    std::vector<F32Lists> f32l(f32_presets.size());
+    HostPool::get().run((int)f32_presets.size(), [&](int i) {
+        const int p = f32_presets[i];
+        const msg_preset& pr = presets[p];
+        const PresetRt& r = prt[p];
+        F32Lists& L = f32l[i];
+        const double tilt = pr.gen_mode == MSG_GEN_FALLBACK ? -3.0 : pr.noise_tilt;
+        const double tilt_alpha = std::log(std::pow(10.0, tilt / 20.0)) / std::log(2.0);
+        const double env_tau = std::max(1e-6, (pr.micro_ms / 1000.0) * (pr.gen_mode == MSG_GEN_SKEWED ? 0.2 : 0.25));
+        const int ne = info[p].n_events;
+        L.gen.reserve(ne);
+        for (int k = 0; k < ne; ++k) {
             const int ei = slot_base[p] + k;
             const msg_event& e = ctx->h_events[ei];
             EventRt& x = ert[ei];
@@ -1262,36 +1339,44 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
             x.cutoff_gen = e.cutoff_out * e.ufac;
             x.roll = pr.bandlimit_roll_hz;
             x.stretch = e.stretch;
-            const double tilt = pr.gen_mode == MSG_GEN_FALLBACK ? -3.0 : pr.noise_tilt;
-            x.tilt_alpha = std::log(std::pow(10.0, tilt / 20.0)) / std::log(2.0);
-            x.env_tau = std::max(1e-6, (pr.micro_ms / 1000.0) * (pr.gen_mode == MSG_GEN_SKEWED ? 0.2 : 0.25));
+            x.tilt_alpha = tilt_alpha;
+            x.env_tau = env_tau;
             x.warp_power = pr.nl_warp_power;
-            gen_list.push_back(ei);
+            L.gen.push_back(ei);
             const int ctp = (x.ops && use_ct) ? spectral_ct_plan(e.n) : -1;
             if (use_s3 && x.ops &&
                 spec3_eligible(e.n, x.ops, x.gen_sr, x.cutoff_gen, x.roll, x.stretch, r.pool_base + e.pool_off,
-                               &x.s3_kb, &x.s3_kz, &x.s3_ky, &x.s3_inv_f)) {
-                spec3.push_back(ei);
-            } else if (ctp >= 0) {
-                spec_ct[ctp].push_back(ei);
-            } else if (x.ops) {
-                std::string why;
-                const int pi = real_plan(ctx->grain_plans, e.n, why);
-                if (pi < 0) return fail(ctx, MSG_E_DEVICE, "grain plan: " + why);
-                x.plan = pi;
-                const RealPlan& gp = ctx->grain_plans.host[pi];
-                if (gp.lds_bytes <= SPEC_SMALL_BYTES && gp.c.size <= SPEC_M_SMALL) {
-                    spec_small.push_back(ei);
-                    spec_small_lds = std::max(spec_small_lds, gp.lds_bytes);
-                } else if (gp.lds_bytes <= LDS_MAX && gp.c.size <= SPEC_M_BIG) {
-                    spec_big.push_back(ei);
-                    spec_big_lds = std::max(spec_big_lds, gp.lds_bytes);
-                } else {
-                    return fail(ctx, MSG_E_UNSUPPORTED, "grain of " + std::to_string(e.n) +
-                                " samples exceeds the LDS-resident FFT (even n <= ~39900)");
-                }
-            } else {
+                               &x.s3_kb, &x.s3_kz, &x.s3_ky, &x.s3_inv_f))
+                L.s3.push_back(ei);
+            else if (ctp >= 0)
+                L.ct[ctp].push_back(ei);
+            else if (x.ops)
+                L.pending.push_back(ei);
+            else
+                L.small.push_back(ei);
+        }
+    });
+    for (F32Lists& L : f32l) {
+        gen_list.insert(gen_list.end(), L.gen.begin(), L.gen.end());
+        spec3.insert(spec3.end(), L.s3.begin(), L.s3.end());
+        for (int c = 0; c < SPEC_CT_PLANS; ++c) spec_ct[c].insert(spec_ct[c].end(), L.ct[c].begin(), L.ct[c].end());
+        spec_small.insert(spec_small.end(), L.small.begin(), L.small.end());
+        for (int ei : L.pending) {
+            EventRt& x = ert[ei];
+            std::string why;
+            const int pi = real_plan(ctx->grain_plans, x.n, why);
+            if (pi < 0) return fail(ctx, MSG_E_DEVICE, "grain plan: " + why);
+            x.plan = pi;
+            const RealPlan& gp = ctx->grain_plans.host[pi];
+            if (gp.lds_bytes <= SPEC_SMALL_BYTES && gp.c.size <= SPEC_M_SMALL) {
                 spec_small.push_back(ei);
+                spec_small_lds = std::max(spec_small_lds, gp.lds_bytes);
+            } else if (gp.lds_bytes <= LDS_MAX && gp.c.size <= SPEC_M_BIG) {
+                spec_big.push_back(ei);
+                spec_big_lds = std::max(spec_big_lds, gp.lds_bytes);
+            } else {
+                return fail(ctx, MSG_E_UNSUPPORTED, "grain of " + std::to_string(x.n) +
+                            " samples exceeds the LDS-resident FFT (even n <= ~39900)");
             }
         }
     }
@@ -1324,25 +1409,12 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
         gg.B = ctx->g64B.p;
         gg.mask = ctx->g64mask.p;
     }
-    HIPCHK(ctx, ctx->ev64.ensure(ev64.size()));
-    HIPCHK(ctx, ctx->g64_list.ensure(g64_list.size()));
-    HIPCHK(ctx, ctx->gen64_list.ensure(gen64_list.size()));
-    HIPCHK(ctx, ctx->gen64_off.ensure(gen64_off.size()));
     HIPCHK(ctx, ctx->micro64.ensure(sum64));
     HIPCHK(ctx, ctx->grain64.ensure(sum64));
     HIPCHK(ctx, ctx->save64.ensure(save_sum));
     HIPCHK(ctx, ctx->state64.ensure(state_sum));
-    HIPCHK(ctx, ctx->chains.ensure(chains.size()));
-    HIPCHK(ctx, ctx->imgbank.ensure(imgbank.size()));
     HIPCHK(ctx, ctx->so_r2.ensure(r2_sum));
     HIPCHK(ctx, ctx->so_A.ensure(so_M));
-    HIPCHK(ctx, ctx->ert.ensure(nslots));
-    HIPCHK(ctx, ctx->prt.ensure(P));
-    HIPCHK(ctx, ctx->gen_list.ensure(gen_list.size()));
-    HIPCHK(ctx, ctx->spec_small.ensure(spec_small.size()));
-    HIPCHK(ctx, ctx->spec_big.ensure(spec_big.size()));
-    HIPCHK(ctx, ctx->tile_begin.ensure(P));
-    HIPCHK(ctx, ctx->fir_begin.ensure(P));
     std::vector<int2> fir_jobs;
     int32_t fjob_off[6] = {0};
     for (int i = 0; i < 5; ++i) {
@@ -1350,10 +1422,6 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
         fir_jobs.insert(fir_jobs.end(), fjobs_by[i].begin(), fjobs_by[i].end());
     }
     fjob_off[5] = (int32_t)fir_jobs.size();
-    HIPCHK(ctx, ctx->fir_jobs.ensure(fir_jobs.size()));
-    HIPCHK(ctx, ctx->h_begin.ensure(P));
-    HIPCHK(ctx, ctx->st_begin.ensure(P));
-    HIPCHK(ctx, ctx->fir_plan_of.ensure(P));
     HIPCHK(ctx, ctx->micro.ensure(pool));
     HIPCHK(ctx, ctx->grain.ensure(pool));
     HIPCHK(ctx, ctx->mono_a.ensure(ysum));
@@ -1361,20 +1429,17 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
     HIPCHK(ctx, ctx->hspec.ensure(hsum));
     HIPCHK(ctx, ctx->irspec.ensure(irs_sum));
     HIPCHK(ctx, ctx->hscratch.ensure(hs_sum));
-    HIPCHK(ctx, ctx->conv_list.ensure(conv_list.size()));
-    HIPCHK(ctx, ctx->irjobs.ensure(ir_jobs.size()));
-    HIPCHK(ctx, ctx->irbank.ensure(irbank.size()));
     HIPCHK(ctx, ctx->maxbits.ensure(P));
-    auto h2d = [&](void* dst, const void* src, size_t bytes) -> hipError_t {
-        ctx->staging.add(dst, src, bytes);    // copied at the flush below, from pinned memory
+    auto h2d = [&](auto** dst, const auto* src, size_t bytes) -> hipError_t {
+        ctx->staging.add(dst, src, bytes);    // copied at the flush below, one copy for all
         return hipSuccess;
     };
     for (int p = 0; p < P; ++p) tile_begin[p] = prt[p].tile_begin;
-    HIPCHK(ctx, h2d(ctx->ert.p, ert.data(), sizeof(EventRt) * nslots));
-    HIPCHK(ctx, h2d(ctx->prt.p, prt.data(), sizeof(PresetRt) * P));
-    HIPCHK(ctx, h2d(ctx->gen_list.p, gen_list.data(), sizeof(int32_t) * gen_list.size()));
-    HIPCHK(ctx, h2d(ctx->spec_small.p, spec_small.data(), sizeof(int32_t) * spec_small.size()));
-    HIPCHK(ctx, h2d(ctx->spec_big.p, spec_big.data(), sizeof(int32_t) * spec_big.size()));
+    HIPCHK(ctx, h2d(&ctx->ert.p, ert, sizeof(EventRt) * nslots));
+    HIPCHK(ctx, h2d(&ctx->prt.p, prt.data(), sizeof(PresetRt) * P));
+    HIPCHK(ctx, h2d(&ctx->gen_list.p, gen_list.data(), sizeof(int32_t) * gen_list.size()));
+    HIPCHK(ctx, h2d(&ctx->spec_small.p, spec_small.data(), sizeof(int32_t) * spec_small.size()));
+    HIPCHK(ctx, h2d(&ctx->spec_big.p, spec_big.data(), sizeof(int32_t) * spec_big.size()));
     std::vector<int32_t> ct_list;
     int32_t ct_off[SPEC_CT_PLANS + 1] = {0};
     for (int i = 0; i < SPEC_CT_PLANS; ++i) {
@@ -1382,27 +1447,33 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
         ct_list.insert(ct_list.end(), spec_ct[i].begin(), spec_ct[i].end());
     }
     ct_off[SPEC_CT_PLANS] = (int32_t)ct_list.size();
-    HIPCHK(ctx, ctx->spec_ct_list.ensure(ct_list.size()));
-    HIPCHK(ctx, ctx->spec3_list.ensure(spec3.size()));
-    HIPCHK(ctx, h2d(ctx->spec3_list.p, spec3.data(), sizeof(int32_t) * spec3.size()));
-    HIPCHK(ctx, h2d(ctx->spec_ct_list.p, ct_list.data(), sizeof(int32_t) * ct_list.size()));
-    HIPCHK(ctx, h2d(ctx->tile_begin.p, tile_begin.data(), sizeof(int32_t) * P));
-    HIPCHK(ctx, h2d(ctx->fir_begin.p, fir_begin.data(), sizeof(int32_t) * P));
-    HIPCHK(ctx, h2d(ctx->fir_jobs.p, fir_jobs.data(), sizeof(int2) * fir_jobs.size()));
-    HIPCHK(ctx, h2d(ctx->h_begin.p, h_begin.data(), sizeof(int32_t) * P));
-    HIPCHK(ctx, h2d(ctx->st_begin.p, st_begin.data(), sizeof(int32_t) * P));
-    HIPCHK(ctx, h2d(ctx->fir_plan_of.p, fir_plan_of.data(), sizeof(int32_t) * P));
-    HIPCHK(ctx, h2d(ctx->irbank.p, irbank.data(), sizeof(double) * irbank.size()));
-    HIPCHK(ctx, h2d(ctx->irjobs.p, ir_jobs.data(), sizeof(int64_t) * ir_jobs.size()));
-    HIPCHK(ctx, h2d(ctx->conv_list.p, conv_list.data(), sizeof(int32_t) * conv_list.size()));
+    HIPCHK(ctx, h2d(&ctx->spec3_list.p, spec3.data(), sizeof(int32_t) * spec3.size()));
+    HIPCHK(ctx, h2d(&ctx->spec_ct_list.p, ct_list.data(), sizeof(int32_t) * ct_list.size()));
+    HIPCHK(ctx, h2d(&ctx->tile_begin.p, tile_begin.data(), sizeof(int32_t) * P));
+    HIPCHK(ctx, h2d(&ctx->fir_begin.p, fir_begin.data(), sizeof(int32_t) * P));
+    HIPCHK(ctx, h2d(&ctx->fir_jobs.p, fir_jobs.data(), sizeof(int2) * fir_jobs.size()));
+    HIPCHK(ctx, h2d(&ctx->h_begin.p, h_begin.data(), sizeof(int32_t) * P));
+    HIPCHK(ctx, h2d(&ctx->st_begin.p, st_begin.data(), sizeof(int32_t) * P));
+    HIPCHK(ctx, h2d(&ctx->fir_plan_of.p, fir_plan_of.data(), sizeof(int32_t) * P));
+    HIPCHK(ctx, h2d(&ctx->irbank.p, irbank.data(), sizeof(double) * irbank.size()));
+    HIPCHK(ctx, h2d(&ctx->irjobs.p, ir_jobs.data(), sizeof(int64_t) * ir_jobs.size()));
+    HIPCHK(ctx, h2d(&ctx->conv_list.p, conv_list.data(), sizeof(int32_t) * conv_list.size()));
     HIPCHK(ctx, hipMemsetAsync(ctx->maxbits.p, 0, sizeof(unsigned) * P, s));
-    HIPCHK(ctx, h2d(ctx->ev64.p, ev64.data(), sizeof(Ev64) * ev64.size()));
-    HIPCHK(ctx, h2d(ctx->g64_list.p, g64_list.data(), sizeof(int32_t) * g64_list.size()));
-    HIPCHK(ctx, h2d(ctx->gen64_list.p, gen64_list.data(), sizeof(int32_t) * gen64_list.size()));
-    HIPCHK(ctx, h2d(ctx->gen64_off.p, gen64_off.data(), sizeof(int64_t) * gen64_off.size()));
-    HIPCHK(ctx, h2d(ctx->chains.p, chains.data(), sizeof(Chain64) * chains.size()));
-    HIPCHK(ctx, h2d(ctx->imgbank.p, imgbank.data(), imgbank.size()));
+    HIPCHK(ctx, h2d(&ctx->ev64.p, ev64.data(), sizeof(Ev64) * ev64.size()));
+    HIPCHK(ctx, h2d(&ctx->g64_list.p, g64_list.data(), sizeof(int32_t) * g64_list.size()));
+    HIPCHK(ctx, h2d(&ctx->gen64_list.p, gen64_list.data(), sizeof(int32_t) * gen64_list.size()));
+    HIPCHK(ctx, h2d(&ctx->gen64_off.p, gen64_off.data(), sizeof(int64_t) * gen64_off.size()));
+    HIPCHK(ctx, h2d(&ctx->chains.p, chains.data(), sizeof(Chain64) * chains.size()));
+    HIPCHK(ctx, h2d(&ctx->imgbank.p, imgbank.data(), imgbank.size()));
+    const auto h2 = hclock::now();
     HIPCHK(ctx, ctx->staging.flush(s));
+    if (ctx->profiling) {
+        const auto h3 = hclock::now();
+        ctx->host_sum[0] += std::chrono::duration<double, std::milli>(h1 - h0).count();
+        ctx->host_sum[1] += std::chrono::duration<double, std::milli>(h2 - h1).count();
+        ctx->host_sum[2] += std::chrono::duration<double, std::milli>(h3 - h2).count();
+        ++ctx->host_cnt;
+    }
 
     // ---- generate ----
     stage_mark(ctx, 2, s);

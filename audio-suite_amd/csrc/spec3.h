@@ -111,7 +111,9 @@ template <class P> MSG_DEV void s3_pass2(float2* buf, const float2* tab) {
 template <class P> MSG_DEV void s3_pass3(const float2* buf, const float2* tab, float2 (&v)[P::R3], int j) {
 #pragma unroll
     for (int r = 0; r < P::R3; ++r) v[r] = buf[j + r * (P::NB3 + P::PADB)];
-    twiddle_pow<P::R3>(v, s3_wM<P>(tab, j));
+    constexpr int B = tw_base<P::R3>();
+    static_assert(B * (P::NB3 - 1) < P::M, "w^(B j) index within the table");
+    twiddle_pow_ab<P::R3, B>(v, s3_wM<P>(tab, j), s3_wM<P>(tab, B * j));
     Dft<P::R3, false>::run(v);
 }
 

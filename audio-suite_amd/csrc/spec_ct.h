@@ -64,7 +64,10 @@ MSG_DEV void ct_pass(float2* buf, const float2* tab) {
         const int j = t + b * T;
         if (NB % T == 0 || j < NB) {
             const int k = j % NS, q = j / NS;
-            if (NS > 1) twiddle_pow<R>(v[b], ct_wM<P>(tab, k * TWS));
+            if (NS > 1) {
+                constexpr int B = tw_base<R>();          // k TWS B < M: B <= R, k < NS
+                twiddle_pow_ab<R, B>(v[b], ct_wM<P>(tab, k * TWS), ct_wM<P>(tab, k * TWS * B));
+            }
             Dft<R, false>::run(v[b]);
 #pragma unroll
             for (int r = 0; r < R; ++r) buf[q * NS * R + k + r * NS] = v[b][r];

@@ -50,8 +50,8 @@ class Engine:
         L.check(L.lib().msg_set_profiling(self._ctx, 1 if on else 0), self._ctx)
 
     def stage_times(self):
-        arr = (C.c_float * 10)()
-        L.check(L.lib().msg_stage_times(self._ctx, arr, 10), self._ctx)
+        arr = (C.c_float * 13)()
+        L.check(L.lib().msg_stage_times(self._ctx, arr, 13), self._ctx)
         return list(arr)
 
     def alloc_output(self, packed: PackedBatch):

@@ -48,7 +48,7 @@ PROFILES = os.path.join(REPO, "profiles")
 STAGE_KERNEL = {"generate": "k_gen_normal", "spectral": "k_spectral", "overlap_add": "k_ola_env",
                 "fir_kernel": "k_fir2<", "stereo": "k_stereo_out"}
 STAGE_NAMES = ["plan", "host_prep", "generate", "spectral", "overlap_add", "fir", "stereo", "total",
-               "fir_kernel", "fir_h"]
+               "fir_kernel", "fir_h", "host_plan_wall", "host_records_wall", "host_upload_wall"]
 KERNEL_STAGES = ["generate", "spectral", "overlap_add", "fir_kernel", "stereo"]
 # host cores of the GPU box available to one job (its CPU share; nproc shows the machine)
 BOX_CORES = 16

@@ -150,7 +150,9 @@ int msg_last_meta(msg_ctx* ctx, int32_t preset, double* micro, double* grain,
  * [0] device plan + read-back, [1] host prep + uploads, [2] generate,
  * [3] spectral (float32 and float64 chains), [4] overlap-add x ADSR,
  * [5] FIR (h build + FIR), [6] stereo+clip+normalise, [7] total,
- * [8] the FIR kernel alone, [9] the h build (IR spectra + h spectra).
+ * [8] the FIR kernel alone, [9] the h build (IR spectra + h spectra);
+ * with n >= 13 also the host wall clock per batch: [10] plan (host pool),
+ * [11] runtime records, [12] pinned staging + upload enqueue.
  * Events are read lazily, so profiling does not block the host.             */
 int msg_set_profiling(msg_ctx* ctx, int32_t on);
 int msg_stage_times(msg_ctx* ctx, float* ms, int32_t n);
