@@ -244,27 +244,36 @@ k_fir2(const PresetRt* __restrict__ rt, const int2* __restrict__ jobs, const flo
                                               fir_wM(tab, G::OFF_MLO, G::OFF_MHI, (js[h] * tw_base<R3>()) & (M - 1)));
             Dft<R3, false>::run(v[h]);
         }
-        // ---- real split, X . H_q accumulated in registers (slot layout, fir_slots)
+        // ---- real split, X . H_q accumulated in registers.  Every thread but 0
+        // pairs bins k (butterfly j, slot r) and M - k (butterfly NB3 - j, slot
+        // R3-1-r); thread 0 holds the self-paired butterflies (DC/Nyquist and bin
+        // M/2) and runs its own branch (slot layout, fir_slots) instead of every
+        // thread paying selects for it.
         const float2* H = hspec + pr.h_off + (int64_t)q * (M + 1);
-        float2 a[R3], bb[R3];
-        fir_slots<R3>(v, a, bb, t0z);
-        const float2 wA = fir_wM(tab, G::OFF_PLO, G::OFF_PHI, js[0]);
-        const float2 hmid = H[M / 2];
+        if (!t0z) {
+            const float2 wA = fir_wM(tab, G::OFF_PLO, G::OFF_PHI, js[0]);
 #pragma unroll
-        for (int r = 0; r < R3; ++r) {
-            const int kA = t0z ? fir_k0<M, R3>(r) : js[0] + r * NB3;
-            const float2 hk = H[(uint32_t)kA], hm = H[(uint32_t)(M - kA)];
-            const float2 wk = t0z ? fir_w0<M, R3>(r) : cmul(wA, fir_cr<R3>(r));
-            if (r < R3 - 1) {
-                fir_pair_mac(a[r], bb[R3 - 1 - r], wk, hk, hm, acc[0][r], acc[1][R3 - 1 - r]);
-            } else {   // thread 0: DC/Nyquist packed as (Y[0], Y[M]) and bin M/2
-                float2 dk = make_float2(0.f, 0.f), dm = dk;
-                fir_pair_mac(a[r], bb[0], wk, hk, hm, dk, dm);
-                const float2 z0 = a[r];
-                const float2 dc = make_float2((z0.x + z0.y) * hk.x, (z0.x - z0.y) * hm.x);
-                const float2 mid = cmul(cconj(bb[0]), hmid);
-                acc[0][r] = cadd(acc[0][r], t0z ? dc : dk);
-                acc[1][0] = cadd(acc[1][0], t0z ? mid : dm);
+            for (int r = 0; r < R3; ++r) {
+                const int kA = js[0] + r * NB3;
+                const float2 hk = H[(uint32_t)kA], hm = H[(uint32_t)(M - kA)];
+                fir_pair_mac(v[0][r], v[1][R3 - 1 - r], cmul(wA, fir_cr<R3>(r)), hk, hm, acc[0][r],
+                             acc[1][R3 - 1 - r]);
+            }
+        } else {
+            float2 a[R3], bb[R3];
+            fir_slots<R3>(v, a, bb, true);
+            const float2 hmid = H[M / 2];
+#pragma unroll
+            for (int r = 0; r < R3; ++r) {
+                const int kA = fir_k0<M, R3>(r);
+                const float2 hk = H[(uint32_t)kA], hm = H[(uint32_t)(M - kA)];
+                if (r < R3 - 1) {
+                    fir_pair_mac(a[r], bb[R3 - 1 - r], fir_w0<M, R3>(r), hk, hm, acc[0][r], acc[1][R3 - 1 - r]);
+                } else {   // DC/Nyquist packed as (Y[0], Y[M]) and bin M/2
+                    const float2 z0 = a[r];
+                    acc[0][r] = cadd(acc[0][r], make_float2((z0.x + z0.y) * hk.x, (z0.x - z0.y) * hm.x));
+                    acc[1][0] = cadd(acc[1][0], cmul(cconj(bb[0]), hmid));
+                }
             }
         }
     }
@@ -272,23 +281,17 @@ k_fir2(const PresetRt* __restrict__ rt, const int2* __restrict__ jobs, const flo
     // ---- inverse: conj Z' from Y in registers, back to the natural butterflies
     {
         const int t = otid();
-        const bool t0z = (t == 0);
-        const float2 wA = fir_wM(tab, G::OFF_PLO, G::OFF_PHI, t);
+        if (t != 0) {
+            const float2 wA = fir_wM(tab, G::OFF_PLO, G::OFF_PHI, t);
 #pragma unroll
-        for (int r = 0; r < R3; ++r) {
-            const float2 wk = t0z ? fir_w0<M, R3>(r) : cmul(wA, fir_cr<R3>(r));
-            if (r < R3 - 1) {
-                fir_pair_pre(acc[0][r], acc[1][R3 - 1 - r], wk);
-            } else {
-                float2 yk = acc[0][r], ym = acc[1][0];
-                fir_pair_pre(yk, ym, wk);
-                const float y0 = acc[0][r].x, yN = acc[0][r].y;
-                const float2 dc = make_float2(0.5f * (y0 + yN), -0.5f * (y0 - yN));
-                acc[0][r] = t0z ? dc : yk;
-                acc[1][0] = t0z ? acc[1][0] : ym;   // bin M/2: conj Z' = Y
-            }
+            for (int r = 0; r < R3; ++r) fir_pair_pre(acc[0][r], acc[1][R3 - 1 - r], cmul(wA, fir_cr<R3>(r)));
+        } else {
+#pragma unroll
+            for (int r = 0; r < R3 - 1; ++r) fir_pair_pre(acc[0][r], acc[1][R3 - 1 - r], fir_w0<M, R3>(r));
+            const float y0 = acc[0][R3 - 1].x, yN = acc[0][R3 - 1].y;
+            acc[0][R3 - 1] = make_float2(0.5f * (y0 + yN), -0.5f * (y0 - yN));   // bin M/2: conj Z' = Y
+            fir_unslots<R3>(acc, true);
         }
-        fir_unslots<R3>(acc, t0z);
     }
     // ---- pass 1': registers -> DFT_R3 -> LDS C
     const int js[2] = {t, t == 0 ? NB3 / 2 : NB3 - t};

@@ -44,9 +44,9 @@ HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: 8.0 TB/s spec
 # per the gfx950 correction + WRITE_SIZE), written by tools/pmc_traffic.py:
 # profiles/traffic_<config>.json, or profiles/traffic.json (C3, round 1).
 PROFILES = os.path.join(REPO, "profiles")
-# bench stage -> the kernel it times (rocprofv3 kernel-name prefix)
-STAGE_KERNEL = {"generate": "k_gen_normal", "spectral": "k_spectral", "overlap_add": "k_ola_env",
-                "fir_kernel": "k_fir2<", "stereo": "k_stereo_out"}
+# bench stage -> the kernels it times (rocprofv3 kernel-name prefixes)
+STAGE_KERNEL = {"generate": ("k_gen_normal",), "spectral": ("k_spec3", "k_spectral"), "overlap_add": ("k_ola_env",),
+                "fir_kernel": ("k_fir2<",), "stereo": ("k_stereo_max", "k_stereo_out")}
 STAGE_NAMES = ["plan", "host_prep", "generate", "spectral", "overlap_add", "fir", "stereo", "total",
                "fir_kernel", "fir_h", "host_plan_wall", "host_records_wall", "host_upload_wall"]
 KERNEL_STAGES = ["generate", "spectral", "overlap_add", "fir_kernel", "stereo"]
@@ -94,9 +94,10 @@ def stage_bytes(infos):
     }
 
 
-def measured_traffic(kernel, cfg, batch):
-    """HBM bytes per launch of `kernel` from the committed PMC summary of this
-    workload, or None when there is none (bench cannot read PMC itself)."""
+def measured_traffic(prefixes, cfg, batch):
+    """HBM bytes per launch of the stage's kernels (name prefixes) from the
+    committed PMC summary of this workload, or None when there is none (bench
+    cannot read PMC itself)."""
     for path in (os.path.join(PROFILES, f"traffic_{cfg}.json"), os.path.join(PROFILES, "traffic.json")):
         try:
             with open(path) as f:
@@ -105,10 +106,15 @@ def measured_traffic(kernel, cfg, batch):
             continue
         if t.get("config") != cfg or int(t.get("batch", -1)) != batch:
             continue
-        for name, rec in t.get("kernels", {}).items():
-            if name.startswith(kernel):
-                return rec.get("hbm_bytes_per_launch")
+        tot = [rec.get("hbm_bytes_per_launch") for name, rec in t.get("kernels", {}).items()
+               if name.startswith(tuple(prefixes))]
+        if tot and all(v is not None for v in tot):
+            return sum(tot)
     return None
+
+
+def kernel_label(stage):
+    return "+".join(k.rstrip("<") for k in STAGE_KERNEL[stage])
 
 
 # ---------------------------------------------------------------------------
@@ -456,7 +462,7 @@ def measure(runner, cfg, seeds, sub, steps, warmup, comm, irs, golden, iso_steps
         "workload": WORKLOAD.get(cfg, cfg), "presets_per_gpu": len(seeds), "sub_batches": nsub,
         "frames_per_gpu_step": w.frames, "events_per_gpu_step": n_ev, "design_samples_per_gpu_step": sum_n,
         "design_msamples_per_s": round(sum_n * world * steps / elapsed / 1e6, 1),
-        "roofline": {"bound": "hbm", "kernel": STAGE_KERNEL[dom].rstrip("<"),
+        "roofline": {"bound": "hbm", "kernel": kernel_label(dom),
                      "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": measured_traffic(STAGE_KERNEL[dom], cfg, launch_batch),
@@ -493,7 +499,7 @@ def isolated(runner, w, iso_steps, sb, cfg):
     dom = max(KERNEL_STAGES, key=lambda k: iso[k])
     ach = sb[dom] / (iso[dom] * 1e-3) / 1e9
     del o
-    return {"kernel": STAGE_KERNEL[dom].rstrip("<"), "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
+    return {"kernel": kernel_label(dom), "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
             "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "algorithmic_bytes": sb[dom],
             "kernel_ms": iso[dom], "traffic": measured_traffic(STAGE_KERNEL[dom], cfg, len(w.params)),
             "stage_ms": iso, "note": f"whole batch on one stream, {iso_steps} renders after the timed region"}
