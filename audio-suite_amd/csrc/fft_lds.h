@@ -57,11 +57,110 @@ struct RealPlan {
 typedef float f2v __attribute__((ext_vector_type(2)));
 MSG_DEV f2v vv(float2 a) { return f2v{a.x, a.y}; }
 MSG_DEV float2 ff(f2v a) { return make_float2(a.x, a.y); }
-MSG_DEV float2 cmul(float2 a, float2 b) {
+// Products of two register values are written as the two packed instructions
+// directly: from the vector form the compiler often materialises (-a.y, a.y)
+// with a v_xor + v_mov per product instead of folding the negation and the
+// broadcast into neg_lo/op_sel (k_fir2: 451 v_xor + 836 v_mov of 4952 VALU).
+// Products with compile-time constants (twc) keep the vector form, whose
+// constants the compiler places in SGPRs.
+#ifndef MSG_ASM_CMUL
+#define MSG_ASM_CMUL 1
+#endif
+MSG_DEV float2 cmul_v(float2 a, float2 b) {
     return ff(f2v{a.x, a.x} * f2v{b.x, b.y} + f2v{-a.y, a.y} * f2v{b.y, b.x});
 }
+MSG_DEV float2 cmul(float2 a, float2 b) {
+#if MSG_ASM_CMUL
+    const f2v x = vv(a), y = vv(b);
+    f2v r, t;
+    // t = (a.x b.x, a.x b.y);  r = (-a.y b.y + t.x, a.y b.x + t.y)
+    asm("v_pk_mul_f32 %1, %2, %3 op_sel_hi:[0,1]\n\t"
+        "v_pk_fma_f32 %0, %2, %3, %1 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_lo:[1,0,0]"
+        : "=v"(r), "=&v"(t) : "v"(x), "v"(y));
+    return ff(r);
+#else
+    return cmul_v(a, b);
+#endif
+}
+// a * b for a wave-uniform (compile-time) b, held in an SGPR pair
+MSG_DEV float2 cmul_k(float2 a, float2 b) {
+#if MSG_ASM_CMUL
+    const f2v x = vv(a), y = vv(b);
+    f2v r, t;
+    asm("v_pk_mul_f32 %1, %2, %3 op_sel_hi:[0,1]\n\t"
+        "v_pk_fma_f32 %0, %2, %3, %1 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_lo:[1,0,0]"
+        : "=v"(r), "=&v"(t) : "v"(x), "s"(y));
+    return ff(r);
+#else
+    return cmul_v(a, b);
+#endif
+}
+// a + (-+i) d and a - (-+i) d (forward sign -1, inverse +1) as single packed adds
+template <bool INV> MSG_DEV f2v add_mi(f2v a, f2v d) {
+#if MSG_ASM_CMUL
+    f2v r;
+    if (INV) asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0] neg_lo:[0,1]" : "=v"(r) : "v"(a), "v"(d));
+    else asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0] neg_hi:[0,1]" : "=v"(r) : "v"(a), "v"(d));
+    return r;
+#else
+    return a + f2v{d.y, d.x} * (INV ? f2v{-1.f, 1.f} : f2v{1.f, -1.f});
+#endif
+}
+template <bool INV> MSG_DEV f2v sub_mi(f2v a, f2v d) { return add_mi<!INV>(a, d); }
+// acc + (b.y, b.x) * (s, -s): the odd-radix sine term, s wave-uniform
+MSG_DEV f2v fma_swap_k(f2v b, f2v sv, f2v acc) {
+#if MSG_ASM_CMUL
+    f2v r;
+    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,0,0] op_sel_hi:[0,1,1]" : "=v"(r) : "v"(b), "s"(sv), "v"(acc));
+    return r;
+#else
+    return acc + f2v{b.y, b.x} * sv;
+#endif
+}
+// acc + a * b (complex multiply-accumulate in two packed FMAs)
+MSG_DEV float2 cfma(float2 acc, float2 a, float2 b) {
+#if MSG_ASM_CMUL
+    const f2v x = vv(a), y = vv(b), c = vv(acc);
+    f2v r, t;
+    asm("v_pk_fma_f32 %1, %2, %3, %4 op_sel_hi:[0,1,1]\n\t"
+        "v_pk_fma_f32 %0, %2, %3, %1 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_lo:[1,0,0]"
+        : "=v"(r), "=&v"(t) : "v"(x), "v"(y), "v"(c));
+    return ff(r);
+#else
+    return ff(vv(acc) + vv(cmul_v(a, b)));
+#endif
+}
+// (a.x + b.x, a.y - b.y) and (a.x - b.x, a.y + b.y): a + conj(b), a - conj(b)
+MSG_DEV f2v add_conj(f2v a, f2v b) {
+#if MSG_ASM_CMUL
+    f2v r;
+    asm("v_pk_add_f32 %0, %1, %2 neg_hi:[0,1]" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+#else
+    return f2v{a.x + b.x, a.y - b.y};
+#endif
+}
+MSG_DEV f2v sub_conj(f2v a, f2v b) {
+#if MSG_ASM_CMUL
+    f2v r;
+    asm("v_pk_add_f32 %0, %1, %2 neg_lo:[0,1]" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+#else
+    return f2v{a.x - b.x, a.y + b.y};
+#endif
+}
 MSG_DEV float2 cmulc(float2 a, float2 b) {   // a * conj(b)
+#if MSG_ASM_CMUL
+    const f2v x = vv(a), y = vv(b);
+    f2v r, t;
+    // t = (a.x b.x, a.y b.x);  r = (a.y b.y + t.x, -a.x b.y + t.y)
+    asm("v_pk_mul_f32 %1, %2, %3 op_sel_hi:[1,0]\n\t"
+        "v_pk_fma_f32 %0, %2, %3, %1 op_sel:[1,1,0] op_sel_hi:[0,1,1] neg_hi:[1,0,0]"
+        : "=v"(r), "=&v"(t) : "v"(x), "v"(y));
+    return ff(r);
+#else
     return ff(f2v{a.x, a.y} * f2v{b.x, b.x} + f2v{a.y, -a.x} * f2v{b.y, b.y});
+#endif
 }
 MSG_DEV float2 cadd(float2 a, float2 b) { return ff(vv(a) + vv(b)); }
 MSG_DEV float2 csub(float2 a, float2 b) { return ff(vv(a) - vv(b)); }
@@ -79,10 +178,9 @@ template <bool INV> struct Dft<4, INV> {
     static MSG_DEV void run(float2* v) {
         const f2v a0 = vv(v[0]) + vv(v[2]), a1 = vv(v[0]) - vv(v[2]);
         const f2v b0 = vv(v[1]) + vv(v[3]), d = vv(v[1]) - vv(v[3]);
-        // b1 = -+i d: (d.y, -d.x) forward, (-d.y, d.x) inverse
-        const f2v b1 = f2v{d.y, d.x} * (INV ? f2v{-1.f, 1.f} : f2v{1.f, -1.f});
+        // v1 = a1 + (-+i) d, v3 = a1 - (-+i) d
         v[0] = ff(a0 + b0); v[2] = ff(a0 - b0);
-        v[1] = ff(a1 + b1); v[3] = ff(a1 - b1);
+        v[1] = ff(add_mi<INV>(a1, d)); v[3] = ff(sub_mi<INV>(a1, d));
     }
 };
 template <int R, bool INV> struct DftOdd {   // odd prime radices, symmetric-pair form
@@ -109,7 +207,7 @@ template <int R, bool INV> struct DftOdd {   // odd prime radices, symmetric-pai
                 const float sn = (float)__builtin_sin(2.0 * 3.14159265358979323846 * jk / R);
                 re += a[j - 1] * c;
                 // -+i sn b: (b.y sn, -b.x sn) forward, (-b.y sn, b.x sn) inverse
-                im += f2v{b[j - 1].y, b[j - 1].x} * (INV ? f2v{-sn, sn} : f2v{sn, -sn});
+                im = fma_swap_k(b[j - 1], INV ? f2v{-sn, sn} : f2v{sn, -sn}, im);
             }
             out[k] = ff(re + im);
             out[R - k] = ff(re - im);
@@ -131,7 +229,7 @@ template <bool INV> MSG_DEV float2 twc(float2 a, int e, int N) {
     if (4 * e == 3 * N) return mul_mi<!INV>(a);
     const float c = (float)__builtin_cos(2.0 * 3.14159265358979323846 * e / N);
     const float s = (float)__builtin_sin(2.0 * 3.14159265358979323846 * e / N);
-    return cmul(a, make_float2(c, INV ? s : -s));
+    return cmul_k(a, make_float2(c, INV ? s : -s));
 }
 
 // Composite radix R1*R2 by Cooley-Tukey in registers: input n = R2*n1 + n2,
@@ -430,8 +528,8 @@ MSG_DEV void rtransform(float2* buf, const RealPlan& rp, const TwLds& tw, bool i
             const float2 e2 = cscale(cadd(zm, cconj(zk)), 0.5f);
             const float2 d2 = csub(zm, cconj(zk));
             const float2 o2 = make_float2(0.5f * d2.y, -0.5f * d2.x);
-            cx(buf, k) = cadd(e1, cmul(rtw_at(tw, k), o1));
-            cx(buf, m - k) = cadd(e2, cmul(rtw_at(tw, m - k), o2));
+            cx(buf, k) = cfma(e1, rtw_at(tw, k), o1);
+            cx(buf, m - k) = cfma(e2, rtw_at(tw, m - k), o2);
         }
         __syncthreads();
     } else {

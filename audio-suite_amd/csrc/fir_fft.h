@@ -100,25 +100,57 @@ MSG_DEV float2 fir_wM(const float2* tab, int lo, int hi, int j) {   // two-level
     return cmul(tab[hi + (j >> 7)], tab[lo + (j & 127)]);
 }
 
-// forward real-FFT split of bins k, M-k and the multiply-accumulate with H
-MSG_DEV void fir_pair_mac(float2 zk, float2 zm, float2 wk, float2 hk, float2 hm, float2& ak, float2& am) {
-    const float2 e = make_float2(0.5f * (zk.x + zm.x), 0.5f * (zk.y - zm.y));   // (Zk + conj Zm) / 2
-    const float2 d = make_float2(zk.x - zm.x, zk.y + zm.y);                     // Zk - conj Zm
-    const float2 o = make_float2(0.5f * d.y, -0.5f * d.x);                      // d / 2i
-    const float2 wo = cmul(wk, o);
-    const float2 xk = cadd(e, wo);
-    const float2 xm = make_float2(e.x - wo.x, wo.y - e.y);                      // conj(e - wo)
-    ak = cadd(ak, cmul(xk, hk));
-    am = cadd(am, cmul(xm, hm));
+// Real-FFT split of bins k, M-k of the packed spectrum Z:
+//     X[k] = E + W o,  X[M-k] = conj(E - W o),  E = (Zk + conj Zm)/2,
+//     o = (Zk - conj Zm)/2i.
+// With S = Zk + conj Zm, P = W (Zk - conj Zm) and t = (P.y, -P.x)/2 = W o:
+//     X[k] = S/2 + t,  X[M-k] = (S.x/2 - t.x, t.y - S.y/2)
+// -- seven packed instructions, the halvings folded into the FMAs.
+MSG_DEV void fir_split(float2 zk, float2 zm, float2 wk, float2& xk, float2& xm) {
+    const f2v S = add_conj(vv(zk), vv(zm));
+    const f2v P = vv(cmul(wk, ff(sub_conj(vv(zk), vv(zm)))));
+#if MSG_ASM_CMUL
+    f2v t, a, b;
+    asm("v_pk_mul_f32 %2, %4, 0.5 op_sel:[1,0] op_sel_hi:[0,0] neg_hi:[1,0]\n\t"
+        "v_pk_fma_f32 %0, %3, 0.5, %2 op_sel_hi:[1,0,1]\n\t"
+        "v_pk_fma_f32 %1, %3, 0.5, %2 op_sel_hi:[1,0,1] neg_lo:[0,0,1] neg_hi:[1,0,0]"
+        : "=&v"(a), "=v"(b), "=&v"(t) : "v"(S), "v"(P));
+    xk = ff(a); xm = ff(b);
+#else
+    const f2v t = f2v{0.5f * P.y, -0.5f * P.x};
+    xk = ff(0.5f * S + t);
+    xm = make_float2(0.5f * S.x - t.x, t.y - 0.5f * S.y);
+#endif
 }
 
-// inverse pre-step: Y[k], Y[M-k] -> conj Z'[k], conj Z'[M-k] (irfft packing)
+// forward real-FFT split of bins k, M-k and the multiply-accumulate with H
+MSG_DEV void fir_pair_mac(float2 zk, float2 zm, float2 wk, float2 hk, float2 hm, float2& ak, float2& am) {
+    float2 xk, xm;
+    fir_split(zk, zm, wk, xk, xm);
+    ak = cfma(ak, xk, hk);
+    am = cfma(am, xm, hm);
+}
+
+// inverse pre-step: Y[k], Y[M-k] -> conj Z'[k], conj Z'[M-k] (irfft packing):
+//     e = (Yk + conj Ym)/2, o = (Yk - conj Ym) conj(W)/2,
+//     Z'k* = (e.x - o.y, -(e.y + o.x)),  Z'm* = (e.x + o.y, e.y - o.x).
+// With S = Yk + conj Ym, t = (Pc.y, Pc.x)/2, Pc = (Yk - conj Ym) conj(W):
+//     Z'k* = (S.x/2 - t.x, -S.y/2 - t.y),  Z'm* = (S.x/2 + t.x, S.y/2 - t.y).
 MSG_DEV void fir_pair_pre(float2& yk, float2& ym, float2 wk) {
-    const float2 e = make_float2(0.5f * (yk.x + ym.x), 0.5f * (yk.y - ym.y));
-    const float2 d = make_float2(yk.x - ym.x, yk.y + ym.y);                     // Yk - conj Ym
-    const float2 o = cscale(cmulc(d, wk), 0.5f);                                // d conj(wk) / 2
-    yk = make_float2(e.x - o.y, -(e.y + o.x));
-    ym = make_float2(e.x + o.y, e.y - o.x);
+    const f2v S = add_conj(vv(yk), vv(ym));
+    const f2v Pc = vv(cmulc(ff(sub_conj(vv(yk), vv(ym))), wk));
+#if MSG_ASM_CMUL
+    f2v t, a, b;
+    asm("v_pk_mul_f32 %2, %4, 0.5 op_sel:[1,0] op_sel_hi:[0,0]\n\t"
+        "v_pk_fma_f32 %0, %3, 0.5, %2 op_sel_hi:[1,0,1] neg_lo:[0,0,1] neg_hi:[1,0,1]\n\t"
+        "v_pk_fma_f32 %1, %3, 0.5, %2 op_sel_hi:[1,0,1] neg_hi:[0,0,1]"
+        : "=&v"(a), "=v"(b), "=&v"(t) : "v"(S), "v"(Pc));
+    yk = ff(a); ym = ff(b);
+#else
+    const f2v t = f2v{0.5f * Pc.y, 0.5f * Pc.x};
+    yk = make_float2(0.5f * S.x - t.x, -0.5f * S.y - t.y);
+    ym = make_float2(0.5f * S.x + t.x, 0.5f * S.y - t.y);
+#endif
 }
 
 // exp(-pi i r / R3): the post-twiddle step between the butterflies' bins
@@ -256,7 +288,7 @@ k_fir2(const PresetRt* __restrict__ rt, const int2* __restrict__ jobs, const flo
             for (int r = 0; r < R3; ++r) {
                 const int kA = js[0] + r * NB3;
                 const float2 hk = H[(uint32_t)kA], hm = H[(uint32_t)(M - kA)];
-                fir_pair_mac(v[0][r], v[1][R3 - 1 - r], cmul(wA, fir_cr<R3>(r)), hk, hm, acc[0][r],
+                fir_pair_mac(v[0][r], v[1][R3 - 1 - r], cmul_k(wA, fir_cr<R3>(r)), hk, hm, acc[0][r],
                              acc[1][R3 - 1 - r]);
             }
         } else {
@@ -272,7 +304,7 @@ k_fir2(const PresetRt* __restrict__ rt, const int2* __restrict__ jobs, const flo
                 } else {   // DC/Nyquist packed as (Y[0], Y[M]) and bin M/2
                     const float2 z0 = a[r];
                     acc[0][r] = cadd(acc[0][r], make_float2((z0.x + z0.y) * hk.x, (z0.x - z0.y) * hm.x));
-                    acc[1][0] = cadd(acc[1][0], cmul(cconj(bb[0]), hmid));
+                    acc[1][0] = cfma(acc[1][0], cconj(bb[0]), hmid);
                 }
             }
         }
@@ -284,7 +316,7 @@ k_fir2(const PresetRt* __restrict__ rt, const int2* __restrict__ jobs, const flo
         if (t != 0) {
             const float2 wA = fir_wM(tab, G::OFF_PLO, G::OFF_PHI, t);
 #pragma unroll
-            for (int r = 0; r < R3; ++r) fir_pair_pre(acc[0][r], acc[1][R3 - 1 - r], cmul(wA, fir_cr<R3>(r)));
+            for (int r = 0; r < R3; ++r) fir_pair_pre(acc[0][r], acc[1][R3 - 1 - r], cmul_k(wA, fir_cr<R3>(r)));
         } else {
 #pragma unroll
             for (int r = 0; r < R3 - 1; ++r) fir_pair_pre(acc[0][r], acc[1][R3 - 1 - r], fir_w0<M, R3>(r));
@@ -340,12 +372,7 @@ k_fir2(const PresetRt* __restrict__ rt, const int2* __restrict__ jobs, const flo
 // ---------------------------------------------------------------------------
 // real-FFT split of bins k, M-k from the packed Z (the first half of fir_pair_mac)
 MSG_DEV void fir_pair_split(float2 zk, float2 zm, float2 wk, float2& xk, float2& xm) {
-    const float2 e = make_float2(0.5f * (zk.x + zm.x), 0.5f * (zk.y - zm.y));
-    const float2 d = make_float2(zk.x - zm.x, zk.y + zm.y);
-    const float2 o = make_float2(0.5f * d.y, -0.5f * d.x);
-    const float2 wo = cmul(wk, o);
-    xk = cadd(e, wo);
-    xm = make_float2(e.x - wo.x, wo.y - e.y);
+    fir_split(zk, zm, wk, xk, xm);
 }
 
 template <int M>
@@ -413,7 +440,7 @@ k_fdl_fwd(const PresetRt* __restrict__ rt, const int2* __restrict__ jobs, const 
 #pragma unroll
     for (int r = 0; r < R3; ++r) {
         const int kA = t0z ? fir_k0<M, R3>(r) : js[0] + r * NB3;
-        const float2 wk = t0z ? fir_w0<M, R3>(r) : cmul(wA, fir_cr<R3>(r));
+        const float2 wk = t0z ? fir_w0<M, R3>(r) : cmul_v(wA, fir_cr<R3>(r));
         if (t0z && r == R3 - 1) {          // DC and Nyquist (packed in z0), bin M/2
             const float2 z0 = a[r];
             X[0] = make_float2(z0.x + z0.y, 0.f);
@@ -462,10 +489,10 @@ k_fdl_mac(const PresetRt* __restrict__ rt, const int2* __restrict__ jobs, const 
                 if (t0z && r == R3 - 1) {
                     const float2 x0 = X[0], xM = X[M], h0 = H[0], hM = H[M];
                     acc[0][r] = cadd(acc[0][r], make_float2(x0.x * h0.x, xM.x * hM.x));   // (Y[0], Y[M]) packed
-                    acc[1][0] = cadd(acc[1][0], cmul(X[M / 2], H[M / 2]));
+                    acc[1][0] = cfma(acc[1][0], X[M / 2], H[M / 2]);
                 } else {
-                    acc[0][r] = cadd(acc[0][r], cmul(X[(uint32_t)kA], H[(uint32_t)kA]));
-                    acc[1][R3 - 1 - r] = cadd(acc[1][R3 - 1 - r], cmul(X[(uint32_t)(M - kA)], H[(uint32_t)(M - kA)]));
+                    acc[0][r] = cfma(acc[0][r], X[(uint32_t)kA], H[(uint32_t)kA]);
+                    acc[1][R3 - 1 - r] = cfma(acc[1][R3 - 1 - r], X[(uint32_t)(M - kA)], H[(uint32_t)(M - kA)]);
                 }
             }
         }
@@ -478,7 +505,7 @@ k_fdl_mac(const PresetRt* __restrict__ rt, const int2* __restrict__ jobs, const 
         const float2 wA = fir_wM(tab, G::OFF_PLO, G::OFF_PHI, tt);
 #pragma unroll
         for (int r = 0; r < R3; ++r) {
-            const float2 wk = t0z ? fir_w0<M, R3>(r) : cmul(wA, fir_cr<R3>(r));
+            const float2 wk = t0z ? fir_w0<M, R3>(r) : cmul_v(wA, fir_cr<R3>(r));
             if (r < R3 - 1) {
                 fir_pair_pre(acc[0][r], acc[1][R3 - 1 - r], wk);
             } else {

@@ -42,7 +42,7 @@ __global__ void k_plan_events(const msg_preset* __restrict__ presets, int n_pres
 // emitted sequence is exactly NumPy's standard_normal(n).
 // ---------------------------------------------------------------------------
 #ifndef MSG_GEN_G
-#define MSG_GEN_G 4
+#define MSG_GEN_G 8
 #endif
 constexpr int GEN_G = MSG_GEN_G;   // chunks of 64 draws classified per pass
 struct JumpTab { nprng::u128 a[GEN_T]; nprng::u128 s[GEN_T]; nprng::u128 a64, s64, aG, sG; };
@@ -66,7 +66,13 @@ MSG_DEV double slow_normal(nprng::u128 st, nprng::u128 inc, uint64_t rabs, int i
         }
         const double u = nprng::next_double(g);
         c += 1;
-        if (((z.fi[idx - 1] - z.fi[idx]) * u + z.fi[idx]) < exp(-0.5 * x * x)) { consumed = c; return x; }
+        // the wedge test lhs < exp(-x^2/2): decided by the hardware exp2 unless the
+        // two sides are within 1e-5 (its error is ~1e-6 relative), then in float64
+        const double lhs = (z.fi[idx - 1] - z.fi[idx]) * u + z.fi[idx];
+        const double ef = (double)__builtin_amdgcn_exp2f((float)(-0.72134752044448170 * x * x));
+        const double dd = lhs - ef;
+        const bool accept = fabs(dd) > 1e-5 * ef ? dd < 0.0 : lhs < exp(-0.5 * x * x);
+        if (accept) { consumed = c; return x; }
         uint64_t r = nprng::next_u64(g);
         c += 1;
         idx = (int)(r & 0xff);
@@ -118,6 +124,11 @@ MSG_DEV float gen_basic_sample(const GenBasicConst& c, int j, float nrm) {
     if (j >= c.n - c.fade) x *= (float)(j - (c.n - c.fade)) * -c.inv_fade + 1.0f;
     return x;
 }
+MSG_DEV float gen_fade(const GenBasicConst& c, int j, float x) {
+    if (j < c.fade) x *= (float)j * c.inv_fade;
+    if (j >= c.n - c.fade) x *= (float)(j - (c.n - c.fade)) * -c.inv_fade + 1.0f;
+    return x;
+}
 
 // RAW64: raw float64 normals for the float64 chain; else the float32 grain.
 // The float32 path forms the fast-path normal in float32 from the top 32 bits
@@ -134,14 +145,15 @@ k_gen_normal(const msg_preset* __restrict__ presets, const msg_event* __restrict
              double* __restrict__ pool64, const int64_t* __restrict__ off64) {
     __shared__ uint64_t s_ki[256];
     __shared__ double s_wi[256];
-    __shared__ float s_wf[256];          // wi * 2^20 in float32
+    __shared__ uint2 s_kw[256];          // (ki >> 20, wi * 2^20 as float32 bits): the fast path's one read
+    __shared__ float4 s_rot[64];         // resonant: (cos, sin)(2 pi r f/sr), 2^(r k_ring), 2^(r k_exc), r < 64
     const int li = blockIdx.x;
     if (li >= n_list) return;
     const int lane = threadIdx.x;
     for (int i = lane; i < 256; i += GEN_T) {
         s_ki[i] = z.ki[i];
         s_wi[i] = z.wi[i];
-        s_wf[i] = (float)(z.wi[i] * 1048576.0);
+        s_kw[i] = make_uint2((uint32_t)(z.ki[i] >> 20), __float_as_uint((float)(z.wi[i] * 1048576.0)));
     }
     const msg_event& e = events[ev_list[li]];
     const msg_preset& pr = presets[e.preset];
@@ -165,6 +177,16 @@ k_gen_normal(const msg_preset* __restrict__ presets, const msg_event* __restrict
     c.k_exc = (float)(-inv_sr / fmax(1e-6, (pr.micro_ms / 1000.0) * 0.15) * log2e);
     const int sigma = (int)(0.0025 * n) > 1 ? (int)(0.0025 * n) : 1;
     c.inv_sigma = (float)(1.0 / (double)sigma);
+    // Resonant strike: sample j = j0 + r of a chunk (j0 = samples already
+    // emitted, r = the lane's rank) from the chunk's uniform sin/cos and decay
+    // at j0 and the per-rank rotation/decay table (angle addition, one ds_read
+    // per sample instead of the phase reduction, a sine and two exponentials).
+    if (!RAW64 && c.mode == MSG_GEN_RESONANT) {
+        const float rf = (float)lane;
+        const float ph = ring_phase(rf, c.fa, c.fb);
+        s_rot[lane] = make_float4(__builtin_amdgcn_cosf(ph), __builtin_amdgcn_sinf(ph),
+                                  __builtin_amdgcn_exp2f(rf * c.k_ring), __builtin_amdgcn_exp2f(rf * c.k_exc));
+    }
 
     // default_rng(seed + i): every lane computes the (uniform) seed state.
     const nprng::Pcg64 g0 = nprng::default_rng((uint64_t)(pr.seed + e.index));
@@ -193,36 +215,58 @@ k_gen_normal(const msg_preset* __restrict__ presets, const msg_event* __restrict
         using XT = typename std::conditional<RAW64, double, float>::type;
         uint64_t rabs[G], F[G];
         int idx[G], consumed[G];
+        (void)rabs; (void)idx;
         XT x[G];
         unsigned slow = 0;
 #pragma unroll
         for (int g = 0; g < G; ++g) {
-            const uint64_t raw = nprng::xsl_rr(st[g]);
-            const int id = (int)(raw & 0xff);
-            const uint64_t rr = raw >> 8;
-            rabs[g] = (rr >> 1) & 0x000fffffffffffffULL;
-            idx[g] = id | (int)((rr & 1) << 8);               // sign in bit 8
-            if constexpr (RAW64) x[g] = (double)rabs[g] * s_wi[id];
-            else x[g] = (float)(uint32_t)(rabs[g] >> 20) * s_wf[id];
-            if (rr & 1) x[g] = -x[g];
-            const bool fast = rabs[g] < s_ki[id];
-            F[g] = __ballot(fast);
             consumed[g] = 1;
+            bool fast;
+            if constexpr (RAW64) {
+                const uint64_t raw = nprng::xsl_rr(st[g]);
+                const int id = (int)(raw & 0xff);
+                const uint64_t rr = raw >> 8;
+                rabs[g] = (rr >> 1) & 0x000fffffffffffffULL;
+                idx[g] = id | (int)((rr & 1) << 8);               // sign in bit 8
+                x[g] = (double)rabs[g] * s_wi[id];
+                if (rr & 1) x[g] = -x[g];
+                fast = rabs[g] < s_ki[id];
+            } else {
+                // XSL-RR output in 32-bit halves: rotr64(hi ^ lo, hi >> 58) by
+                // two alignbits.  The fast test compares bits 29..60 of the draw
+                // (rabs >> 20) with ki >> 20; a tie is left to the slow pass,
+                // which repeats the exact 52-bit test.
+                const uint64_t hi = (uint64_t)(st[g] >> 64), lo = (uint64_t)st[g];
+                const uint32_t rot = (uint32_t)(hi >> 58);
+                uint32_t xl = (uint32_t)(hi ^ lo), xh = (uint32_t)((hi ^ lo) >> 32);
+                if (rot & 32) { const uint32_t tmp = xl; xl = xh; xh = tmp; }
+                const uint32_t olo = __builtin_amdgcn_alignbit(xh, xl, rot);
+                const uint32_t ohi = __builtin_amdgcn_alignbit(xl, xh, rot);
+                const uint32_t r32 = __builtin_amdgcn_alignbit(ohi, olo, 29);
+                const int id = (int)(olo & 0xff);
+                const uint2 kw = s_kw[id];
+                const float xf = (float)r32 * __uint_as_float(kw.y);
+                x[g] = (olo & 0x100) ? -xf : xf;
+                fast = r32 < kw.x;
+            }
+            F[g] = __ballot(fast);
             if (!fast) slow |= 1u << g;
         }
         while (slow) {                            // divergent: each lane walks its own slow draws
             const int gs = __builtin_ctz(slow);
             slow &= slow - 1;
             nprng::u128 s0 = st[0];
-            uint64_t ra = rabs[0];
-            int id = idx[0];
 #pragma unroll
             for (int g = 1; g < G; ++g)
-                if (gs == g) { s0 = st[g]; ra = rabs[g]; id = idx[g]; }
-            double xv = (double)ra * s_wi[id & 0xff];
-            if (id >> 8) xv = -xv;
+                if (gs == g) s0 = st[g];
+            const uint64_t raw = nprng::xsl_rr(s0);
+            const int id = (int)(raw & 0xff);
+            const uint64_t ra = (raw >> 9) & 0x000fffffffffffffULL;
+            if (!RAW64 && ra < s_ki[id]) continue;   // a tie of the 32-bit test: fast after all
+            double xv = (double)ra * s_wi[id];
+            if ((raw >> 8) & 1) xv = -xv;
             int cn = 1;
-            const double v = slow_normal(s0, inc, ra, id & 0xff, xv, z, cn);
+            const double v = slow_normal(s0, inc, ra, id, xv, z, cn);
 #pragma unroll
             for (int g = 0; g < G; ++g)
                 if (gs == g) { x[g] = (XT)v; consumed[g] = cn; }
@@ -243,11 +287,33 @@ k_gen_normal(const msg_preset* __restrict__ presets, const msg_event* __restrict
                 if (end >= 64) { pos = end; break; }
                 S &= ~0ULL << end;
             }
-            if ((valid >> lane) & 1) {
-                const int j = produced + __popcll(valid & ((1ULL << lane) - 1));
-                if (j < n) {
-                    if constexpr (RAW64) out64[j] = x[g];
-                    else out[j] = gen_basic_sample(c, j, (float)x[g]);
+            if constexpr (RAW64) {
+                if ((valid >> lane) & 1) {
+                    const int j = produced + __popcll(valid & ((1ULL << lane) - 1));
+                    if (j < n) out64[j] = x[g];
+                }
+            } else if (c.mode == MSG_GEN_RESONANT) {
+                // chunk-uniform phase and decays at j0 = produced
+                const float j0 = (float)produced;
+                const float ph0 = ring_phase(j0, c.fa, c.fb);
+                const float s0 = __builtin_amdgcn_sinf(ph0), c0 = __builtin_amdgcn_cosf(ph0);
+                const float dA = __builtin_amdgcn_exp2f(fmaxf(j0 * c.k_ring, -126.f));
+                const float dE = __builtin_amdgcn_exp2f(fmaxf(j0 * c.k_exc, -126.f));
+                const bool edge = produced < c.fade || produced + 64 > c.n - c.fade;
+                if ((valid >> lane) & 1) {
+                    const int rk = __popcll(valid & ((1ULL << lane) - 1));
+                    const int j = produced + rk;
+                    if (j < n) {
+                        const float4 tb = s_rot[rk];
+                        float v = 0.9f * fmaf(s0, tb.x, c0 * tb.y) * (dA * tb.z) + 0.25f * x[g] * (dE * tb.w);
+                        if (edge) v = gen_fade(c, j, v);
+                        out[j] = v;
+                    }
+                }
+            } else {
+                if ((valid >> lane) & 1) {
+                    const int j = produced + __popcll(valid & ((1ULL << lane) - 1));
+                    if (j < n) out[j] = gen_basic_sample(c, j, (float)x[g]);
                 }
             }
             produced += __popcll(valid);
@@ -436,13 +502,17 @@ MSG_DEV void stereo_r4(const PresetRt& r, const float* w, int u, float (&R)[4], 
         const float4 q = w4[i];
         x[4 * i] = q.x; x[4 * i + 1] = q.y; x[4 * i + 2] = q.z; x[4 * i + 3] = q.w;
     }
+    // outputs (u, u+1) and (u+2, u+3) as packed pairs: the pair (x[k+2m], x[k+1+2m])
+    // is one aligned register pair, so each tap is one v_pk_fma per pair
+    typedef float f2 __attribute__((ext_vector_type(2)));
+    f2 a01 = f2{0.f, 0.f}, a23 = f2{0.f, 0.f};
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        float acc = 0.f;
-#pragma unroll
-        for (int m = 0; m < 25; ++m) acc = fmaf(r.bess[m], x[k + 2 * m], acc);
-        R[k] = acc;
+    for (int m = 0; m < 25; ++m) {
+        const f2 b = f2{r.bess[m], r.bess[m]};
+        a01 = __builtin_elementwise_fma(b, f2{x[2 * m], x[2 * m + 1]}, a01);
+        a23 = __builtin_elementwise_fma(b, f2{x[2 * m + 2], x[2 * m + 3]}, a23);
     }
+    R[0] = a01.x; R[1] = a01.y; R[2] = a23.x; R[3] = a23.y;
 }
 
 __global__ void __launch_bounds__(ST_T)

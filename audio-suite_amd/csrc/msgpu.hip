@@ -1029,6 +1029,34 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
         }
         HIPCHK(ctx, hipStreamSynchronize(s));
     }
+    // Early-reflection taps whose rounded delays coincide are merged here, in tap
+    // order and in float64 (the order MS:416-420 adds them), so the FIR kernels
+    // scatter at most one tap per offset: LDS float atomics on a shared offset
+    // sum in arbitrary order, and a last-ulp change of h re-rounds the whole
+    // float32 convolution (renders of one batch differed by up to 1.2e-5).
+    {
+        auto merge = [&](int p) {
+            if (!(presets[p].flags & MSG_F_ER_CLOUD)) return;
+            const int nt = std::max(1, presets[p].er_taps);
+            int32_t* off = ctx->h_er_off.data() + tap_base[p];
+            double* g = ctx->h_er_gain.data() + tap_base[p];
+            std::vector<int> ix(nt);
+            for (int k = 0; k < nt; ++k) ix[k] = k;
+            std::stable_sort(ix.begin(), ix.end(), [&](int a, int b) { return off[a] < off[b]; });
+            for (int i = 0; i < nt;) {
+                int j = i + 1;
+                while (j < nt && off[ix[j]] == off[ix[i]]) ++j;
+                if (j - i > 1 && off[ix[i]] > 0) {
+                    double acc = g[ix[i]];
+                    for (int u = i + 1; u < j; ++u) { acc += g[ix[u]]; off[ix[u]] = -1; }
+                    g[ix[i]] = acc;
+                }
+                i = j;
+            }
+        };
+        if (ctx->device_plan) for (int p = 0; p < P; ++p) merge(p);
+        else HostPool::get().run(P, merge);
+    }
     stage_mark(ctx, 1, s);
     const auto h1 = hclock::now();
     ctx->staging.add(&ctx->presets.p, presets, sizeof(msg_preset) * P);
