@@ -596,6 +596,24 @@ MSG_DEV float tanh_fast(float x) {
     return copysignf(t, x);
 }
 MSG_DEV float sat(float v, float d, float inv_td) { return d > 0.f ? tanh_fast(v * d) * inv_td : v; }
+// tanh_fast of an (L, R) pair in the packed form: the arithmetic runs as
+// v_pk_* pairs, the four transcendentals stay scalar (same operations and
+// rounding as tanh_fast on each lane).
+typedef float f2p __attribute__((ext_vector_type(2)));
+MSG_DEV f2p tanh_fast2(f2p x) {
+    const f2p ax = __builtin_elementwise_abs(x);
+    const f2p a = __builtin_elementwise_min(2.8853900817779268f * ax, f2p{126.f, 126.f});
+    const f2p e1 = f2p{__builtin_amdgcn_exp2f(a.x), __builtin_amdgcn_exp2f(a.y)} + 1.0f;
+    const f2p r = f2p{__builtin_amdgcn_rcpf(e1.x), __builtin_amdgcn_rcpf(e1.y)};
+    f2p t = 1.0f - 2.0f * r;
+    const f2p x2 = ax * ax;
+    const f2p tp = ax * __builtin_elementwise_fma(x2, __builtin_elementwise_fma(x2, f2p{0.13333333f, 0.13333333f},
+                                                                                f2p{-0.33333333f, -0.33333333f}),
+                                                  f2p{1.0f, 1.0f});
+    t.x = ax.x < 0.05f ? tp.x : t.x;
+    t.y = ax.y < 0.05f ? tp.y : t.y;
+    return __builtin_elementwise_copysign(t, x);
+}
 
 __global__ void __launch_bounds__(ST_T)
 k_stereo_out(const PresetRt* __restrict__ rt, const int32_t* __restrict__ st_begin, int n_presets,
@@ -640,8 +658,16 @@ k_stereo_out(const PresetRt* __restrict__ rt, const int32_t* __restrict__ st_beg
                 R[k] = r.stereo_fir == 2 ? (u + k < st.cnt ? rbuf[r.r2_off + st.t0 + u + k] : 0.f) : L[k];
         }
         float2 v[4];
+        if (d > 0.f) {
 #pragma unroll
-        for (int k = 0; k < 4; ++k) v[k] = make_float2(sat(L[k], d, inv_td) * scale, sat(R[k], d, inv_td) * scale);
+            for (int k = 0; k < 4; ++k) {
+                const f2p t = tanh_fast2(f2p{L[k], R[k]} * d) * inv_td * scale;
+                v[k] = make_float2(t.x, t.y);
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) v[k] = make_float2(L[k] * scale, R[k] * scale);
+        }
         if (o16 && u + 4 <= st.cnt) {
             float4* o4 = reinterpret_cast<float4*>(o + u);
             o4[0] = make_float4(v[0].x, v[0].y, v[1].x, v[1].y);

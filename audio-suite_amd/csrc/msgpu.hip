@@ -968,6 +968,9 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
             tap_base[p] = (int32_t)ntaps;
             nslots += info[p].n_slots;
             if (presets[p].flags & MSG_F_ER_CLOUD) ntaps += std::max(1, presets[p].er_taps);
+            // kernels index a preset's frames with 32-bit integers (and 32-bit byte
+            // offsets of its float32 mono buffer)
+            if (info[p].out_n > (int64_t)1 << 29) return fail(ctx, MSG_E_UNSUPPORTED, "output longer than 2^29 frames");
         }
         if (nslots > INT32_MAX / 2) return fail(ctx, MSG_E_UNSUPPORTED, "too many events in one batch");
         return MSG_OK;
