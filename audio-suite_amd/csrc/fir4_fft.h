@@ -1,0 +1,263 @@
+// fir4_fft.h — four-pass variant of the overlap-save FIR kernel (TU: k_fir.hip).
+//
+// k_fir2<16384> runs its 16384-point transforms as three radix (32, 32, 16)
+// passes on 512 threads: 224 VGPRs, 8 waves per CU (2 per SIMD) and, per the
+// r02q SQ counters, ~50 % VALU-busy -- the rest is barrier / LDS / HBM latency
+// that two waves per SIMD cannot cover.  k_fir4<16384> runs the same
+// algorithm (same blocks, partitions, real split and multiply-accumulate) as
+// four radix (16, 16, 8, 8) passes on 1024 threads: at most 128 VGPRs, 16
+// waves per CU (4 per SIMD), for one more LDS exchange per transform.
+//
+// Stockham pass p (radix R, NS = product of the earlier radices, NB = M/R):
+// butterfly j reads logical j + r NB, multiplies by w_{NS R}^{(j mod NS) r},
+// runs DFT_R and writes logical (j / NS) NS R + (j mod NS) + r NS.
+// Forward (16, 16, 8, 8): pass 1 reads HBM, pass 4 leaves butterflies j and
+// NB4 - j in registers (bins k and M - k of the packed spectrum, as in
+// k_fir2).  Inverse: the same engine on conj Z' with radices (8, 8, 16, 16),
+// pass 1' from registers, pass 4' to HBM.
+//
+// Exchange layouts phys(x) = x + x / S (S = 0: identity), chosen per exchange
+// with the LDS bank model of MI355X_MICROARCH.md (ds_write_b64: 16-lane groups
+// over 32 banks; ds_read_b64: 32-lane groups over 64 banks), extra cycles per
+// transform (write, read): E1 S=16 (0, 512), E2 S=0 (0, 0), E3 S=0 (0, 0),
+// E1' S=8 (0, 512), E2' S=8 (0, 512), E3' S=0 (0, 0).
+#pragma once
+#include "fir_fft.h"
+
+template <int M> struct Fir4Cfg;
+template <> struct Fir4Cfg<16384> { static constexpr int R1 = 16, R2 = 16, R3 = 8, R4 = 8; };
+
+template <int S> MSG_HD constexpr int pads(int x) { return S ? x + x / S : x; }
+
+template <int M> struct Fir4Geo {
+    static constexpr int R1 = Fir4Cfg<M>::R1, R2 = Fir4Cfg<M>::R2, R3 = Fir4Cfg<M>::R3, R4 = Fir4Cfg<M>::R4;
+    static_assert(R1 * R2 * R3 * R4 == M, "four passes");
+    static constexpr int T = M / (2 * R4);
+    static constexpr int NB1 = M / R1, NB2 = M / R2, NB3 = M / R3, NB4 = M / R4;
+    static constexpr int BP1 = NB1 / T, BP2 = NB2 / T, BP3 = NB3 / T;
+    static_assert(NB1 % T == 0 && NB2 % T == 0 && NB3 % T == 0 && NB4 == 2 * T, "FIR4 plan");
+    // exchange pads: forward E1..E3, inverse E1'..E3'
+    static constexpr int S1 = 16, S2 = 0, S3 = 0, S1I = 8, S2I = 8, S3I = 0;
+    static_assert(S1 == R1 && S1I == R4, "pass-1 writes of R consecutive elements: pad S = R");
+    // twiddle tables at LDS offset 0 (float2 entries): exact [r][k] tables for the
+    // two passes with small NS, two-level w_M and w_2M tables for the rest
+    static constexpr int OFF_TA = 0;                    // forward pass 2: radix R2, NS = R1, [R2][R1]
+    static constexpr int OFF_TB = OFF_TA + R2 * R1;     // inverse pass 2': radix R3, NS = R4, [R3][R4]
+    static constexpr int OFF_MLO = OFF_TB + R3 * R4;    // w_M^x, x < 128
+    static constexpr int OFF_MHI = OFF_MLO + 128;       // w_M^(128 x), x < M / 128
+    static constexpr int OFF_PLO = OFF_MHI + M / 128;   // w_2M^x, x < 128
+    static constexpr int OFF_PHI = OFF_PLO + 128;       // w_2M^(128 x), 128 x <= NB4
+    static constexpr int TAB_USED = OFF_PHI + NB4 / 128 + 1;
+    static constexpr int TAB = (TAB_USED + 15) & ~15;
+    static constexpr int BUF = M + M / 8;
+    static constexpr int LDS_BYTES = (TAB + BUF) * 8;
+    static_assert(LDS_BYTES <= 163840, "FIR4 LDS budget");
+};
+
+// One radix-R Stockham pass LDS -> LDS on the 1024-thread grid.  TW: the
+// twiddles w_{NS R}^{k r} from the exact [r][k] table at OFF_T (TAB = true) or
+// as powers of w_M^{k M/(NS R)} from the two-level w_M table.
+template <int M, int R, int NS, int BP, int SI, int SO, bool TAB, int OFF_T>
+MSG_DEV void fir4_pass_lds(float2* buf, const float2* tab, int t) {
+    using G = Fir4Geo<M>;
+    constexpr int NB = M / R, T = G::T, STEP = M / (NS * R);
+    static_assert(SI == 0 || NB % SI == 0, "additive read addresses");
+    float2 v[BP][R];
+#pragma unroll
+    for (int b = 0; b < BP; ++b) {
+        const int base = pads<SI>(t + b * T);
+#pragma unroll
+        for (int r = 0; r < R; ++r) v[b][r] = buf[base + pads<SI>(r * NB)];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int b = 0; b < BP; ++b) {
+        const int j = t + b * T;
+        const int k = j & (NS - 1), q = j / NS;
+        if constexpr (TAB) {
+#pragma unroll
+            for (int r = 1; r < R; ++r) v[b][r] = cmul(v[b][r], tab[OFF_T + r * NS + k]);
+        } else {
+            constexpr int B = tw_base<R>();
+            twiddle_pow_ab<R, B>(v[b], fir_wM(tab, G::OFF_MLO, G::OFF_MHI, k * STEP),
+                                 fir_wM(tab, G::OFF_MLO, G::OFF_MHI, (k * STEP * B) & (M - 1)));
+        }
+        Dft<R, false>::run(v[b]);
+        const int lo = q * NS * R + k;
+#pragma unroll
+        for (int r = 0; r < R; ++r) buf[pads<SO>(lo + r * NS)] = v[b][r];
+    }
+}
+
+template <int M>
+__global__ void __launch_bounds__(Fir4Geo<M>::T)
+k_fir4(const PresetRt* __restrict__ rt, const int2* __restrict__ jobs, const float2* __restrict__ tables,
+       const float2* __restrict__ hspec, const float* __restrict__ x_in, float* __restrict__ y_out) {
+    using G = Fir4Geo<M>;
+    constexpr int T = G::T, R1 = G::R1, R2 = G::R2, R3 = G::R3, R4 = G::R4;
+    constexpr int NB1 = G::NB1, NB4 = G::NB4;
+    extern __shared__ __attribute__((aligned(16))) float2 lds[];
+    float2* tab = lds;
+    float2* buf = lds + G::TAB;
+    const int2 job = jobs[xcd_block(blockIdx.x, gridDim.x)];
+    const PresetRt& pr = rt[job.x];
+    const int P = pr.fir_P, Q = pr.fir_Q;
+    const int64_t n = pr.out_n;
+    const int64_t t0 = (int64_t)job.y * pr.fir_B;
+    const float* x = x_in + pr.y_off;
+    for (int i = threadIdx.x; i < G::TAB_USED; i += T) tab[i] = tables[i];   // visible after the first exchange
+
+    float2 acc[2][R4];
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int r = 0; r < R4; ++r) acc[h][r] = make_float2(0.f, 0.f);
+
+    for (int q = 0; q < Q; ++q) {
+        const int t = otid();
+        const bool t0z = (t == 0);
+        const int js[2] = {t, t0z ? NB4 / 2 : NB4 - t};
+        // ---- pass 1: x segment (zero outside [0, n)) -> DFT_R1 -> LDS (E1)
+        const int64_t s0 = t0 - (int64_t)q * P - (P - 1);
+        const bool fast = s0 >= 0 && s0 + 2 * M <= n && (((uintptr_t)(x + s0)) & 7) == 0;
+        {
+            float2 v[R1];
+            if (fast) {
+                const float2* z = reinterpret_cast<const float2*>(x + s0);
+#pragma unroll
+                for (int r = 0; r < R1; ++r) v[r] = z[(uint32_t)(t + r * NB1)];
+            } else {
+#pragma unroll
+                for (int r = 0; r < R1; ++r) {
+                    const int64_t a = s0 + 2 * (int64_t)(t + r * NB1);
+                    const bool in0 = a >= 0 && a < n, in1 = a + 1 >= 0 && a + 1 < n;
+                    const float x0 = x[(uint32_t)(in0 ? a : 0)], x1 = x[(uint32_t)(in1 ? a + 1 : 0)];
+                    v[r] = make_float2(in0 ? x0 : 0.f, in1 ? x1 : 0.f);
+                }
+            }
+            Dft<R1, false>::run(v);
+            const int base = pads<G::S1>(t * R1);
+#pragma unroll
+            for (int r = 0; r < R1; ++r) buf[base + r] = v[r];
+        }
+        __syncthreads();
+        // ---- passes 2, 3: LDS -> LDS (E1 -> E2 -> E3)
+        fir4_pass_lds<M, R2, R1, G::BP2, G::S1, G::S2, true, G::OFF_TA>(buf, tab, t);
+        __syncthreads();
+        fir4_pass_lds<M, R3, R1 * R2, G::BP3, G::S2, G::S3, false, 0>(buf, tab, t);
+        __syncthreads();
+        // ---- pass 4: LDS (E3) -> registers, butterflies j and NB4 - j
+        float2 v[2][R4];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+#pragma unroll
+            for (int r = 0; r < R4; ++r) v[h][r] = buf[pads<G::S3>(js[h] + r * NB4)];
+        }
+        __syncthreads();   // LDS free for the next segment / the inverse
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            twiddle_pow_ab<R4, tw_base<R4>()>(v[h], fir_wM(tab, G::OFF_MLO, G::OFF_MHI, js[h]),
+                                              fir_wM(tab, G::OFF_MLO, G::OFF_MHI, (js[h] * tw_base<R4>()) & (M - 1)));
+            Dft<R4, false>::run(v[h]);
+        }
+        // ---- real split, X . H_q accumulated in registers (k_fir2's pairing)
+        const float2* H = hspec + pr.h_off + (int64_t)q * (M + 1);
+        if (!t0z) {
+            const float2 wA = fir_wM(tab, G::OFF_PLO, G::OFF_PHI, js[0]);
+#pragma unroll
+            for (int r = 0; r < R4; ++r) {
+                const int kA = js[0] + r * NB4;
+                const float2 hk = H[(uint32_t)kA], hm = H[(uint32_t)(M - kA)];
+                fir_pair_mac(v[0][r], v[1][R4 - 1 - r], cmul_k(wA, fir_cr<R4>(r)), hk, hm, acc[0][r],
+                             acc[1][R4 - 1 - r]);
+            }
+        } else {
+            float2 a[R4], bb[R4];
+            fir_slots<R4>(v, a, bb, true);
+            const float2 hmid = H[M / 2];
+#pragma unroll
+            for (int r = 0; r < R4; ++r) {
+                const int kA = fir_k0<M, R4>(r);
+                const float2 hk = H[(uint32_t)kA], hm = H[(uint32_t)(M - kA)];
+                if (r < R4 - 1) {
+                    fir_pair_mac(a[r], bb[R4 - 1 - r], fir_w0<M, R4>(r), hk, hm, acc[0][r], acc[1][R4 - 1 - r]);
+                } else {   // DC/Nyquist packed as (Y[0], Y[M]) and bin M/2
+                    const float2 z0 = a[r];
+                    acc[0][r] = cadd(acc[0][r], make_float2((z0.x + z0.y) * hk.x, (z0.x - z0.y) * hm.x));
+                    acc[1][0] = cfma(acc[1][0], cconj(bb[0]), hmid);
+                }
+            }
+        }
+    }
+
+    // ---- inverse: conj Z' from Y in registers, back to the natural butterflies
+    {
+        const int t = otid();
+        if (t != 0) {
+            const float2 wA = fir_wM(tab, G::OFF_PLO, G::OFF_PHI, t);
+#pragma unroll
+            for (int r = 0; r < R4; ++r) fir_pair_pre(acc[0][r], acc[1][R4 - 1 - r], cmul_k(wA, fir_cr<R4>(r)));
+        } else {
+#pragma unroll
+            for (int r = 0; r < R4 - 1; ++r) fir_pair_pre(acc[0][r], acc[1][R4 - 1 - r], fir_w0<M, R4>(r));
+            const float y0 = acc[0][R4 - 1].x, yN = acc[0][R4 - 1].y;
+            acc[0][R4 - 1] = make_float2(0.5f * (y0 + yN), -0.5f * (y0 - yN));   // bin M/2: conj Z' = Y
+            fir_unslots<R4>(acc, true);
+        }
+    }
+    const int t = otid();
+    const int js[2] = {t, t == 0 ? NB4 / 2 : NB4 - t};
+    // ---- pass 1': registers -> DFT_R4 -> LDS (E1')
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        Dft<R4, false>::run(acc[h]);
+        const int base = pads<G::S1I>(js[h] * R4);
+#pragma unroll
+        for (int r = 0; r < R4; ++r) buf[base + r] = acc[h][r];
+    }
+    __syncthreads();
+    // ---- passes 2', 3': LDS -> LDS (E1' -> E2' -> E3')
+    fir4_pass_lds<M, R3, R4, G::BP3, G::S1I, G::S2I, true, G::OFF_TB>(buf, tab, t);
+    __syncthreads();
+    fir4_pass_lds<M, R2, R4 * R3, G::BP2, G::S2I, G::S3I, false, 0>(buf, tab, t);
+    __syncthreads();
+    // ---- pass 4': LDS (E3') -> DFT_R1 -> output block (samples u >= P-1 of the segment)
+    float* y = y_out + pr.y_off;
+    const float s = 1.0f / (float)M;
+    {
+        float2 v[R1];
+#pragma unroll
+        for (int r = 0; r < R1; ++r) v[r] = buf[pads<G::S3I>(t + r * NB1)];
+        twiddle_pow_ab<R1, tw_base<R1>()>(v, fir_wM(tab, G::OFF_MLO, G::OFF_MHI, t),
+                                          fir_wM(tab, G::OFF_MLO, G::OFF_MHI, (t * tw_base<R1>()) & (M - 1)));
+        Dft<R1, false>::run(v);
+#pragma unroll
+        for (int r = 0; r < R1; ++r) {
+            const int u = 2 * (t + r * NB1);                 // z[u/2] = x[u] + i x[u+1]
+            const int64_t o = t0 + u - (P - 1);
+            if (u >= P - 1 && o < n) y[(uint32_t)o] = v[r].x * s;
+            if (u + 1 >= P - 1 && o + 1 < n) y[(uint32_t)(o + 1)] = -v[r].y * s;
+        }
+    }
+}
+
+// Host: the twiddle tables of Fir4Geo<M> (float64-built, rounded once).
+template <int M>
+inline void fir4_tables(std::vector<float>& out) {
+    using G = Fir4Geo<M>;
+    out.assign(2 * (size_t)G::TAB_USED, 0.f);
+    const long double PI = 3.14159265358979323846264338327950288L;
+    auto put = [&](int at, long double num, long double den) {
+        const long double a = -2.0L * PI * num / den;
+        out[2 * at] = (float)cosl(a);
+        out[2 * at + 1] = (float)sinl(a);
+    };
+    for (int r = 0; r < G::R2; ++r)
+        for (int k = 0; k < G::R1; ++k) put(G::OFF_TA + r * G::R1 + k, (long double)k * r, (long double)G::R1 * G::R2);
+    for (int r = 0; r < G::R3; ++r)
+        for (int k = 0; k < G::R4; ++k) put(G::OFF_TB + r * G::R4 + k, (long double)k * r, (long double)G::R4 * G::R3);
+    for (int x = 0; x < 128; ++x) put(G::OFF_MLO + x, x, M);
+    for (int x = 0; x < M / 128; ++x) put(G::OFF_MHI + x, 128.0L * x, M);
+    for (int x = 0; x < 128; ++x) put(G::OFF_PLO + x, x, 2.0L * M);
+    for (int x = 0; x <= G::NB4 / 128; ++x) put(G::OFF_PHI + x, 128.0L * x, 2.0L * M);
+}

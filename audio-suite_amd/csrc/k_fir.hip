@@ -1,6 +1,7 @@
 // k_fir.hip — translation unit of the space FIR kernels.
 #include "kernels_fir.h"
 #include "fir_fft.h"
+#include "fir4_fft.h"
 #include "launch.h"
 
 template <int M> static void fir2_attr() {
@@ -13,6 +14,8 @@ template <int M> static void fir2_attr() {
 }
 
 void fir_init_attrs() {
+    (void)hipFuncSetAttribute((const void*)k_fir4<16384>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              Fir4Geo<16384>::LDS_BYTES);
     fir2_attr<1024>(); fir2_attr<2048>(); fir2_attr<4096>(); fir2_attr<8192>(); fir2_attr<16384>();
     (void)hipFuncSetAttribute((const void*)k_fir_h<FIR_T, FIR_M>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
     (void)hipFuncSetAttribute((const void*)k_fir_hconv<FIR_T, FIR_M>, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -74,6 +77,20 @@ hipError_t launch_fir2(int M, unsigned grid, hipStream_t s, const PresetRt* rt, 
         case 16384: return fir2_go<16384>(grid, s, rt, jobs, tables, hspec, x_in, y_out);
         default: return hipErrorInvalidValue;
     }
+}
+
+bool fir4_tables_host(int M, std::vector<float>& out) {
+    if (M != 16384) return false;
+    fir4_tables<16384>(out);
+    return true;
+}
+
+hipError_t launch_fir4(int M, unsigned grid, hipStream_t s, const PresetRt* rt, const int2* jobs,
+                       const float2* tables, const float2* hspec, const float* x_in, float* y_out) {
+    if (M != 16384) return hipErrorInvalidValue;
+    hipLaunchKernelGGL((k_fir4<16384>), dim3(grid), dim3(Fir4Geo<16384>::T), Fir4Geo<16384>::LDS_BYTES, s, rt, jobs,
+                       tables, hspec, x_in, y_out);
+    return hipGetLastError();
 }
 
 template <int M>

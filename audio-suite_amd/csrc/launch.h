@@ -55,6 +55,10 @@ hipError_t launch_fdl(int M, unsigned grid, hipStream_t s, const PresetRt* rt, c
                       const float2* hspec, float2* xspec, const float* x_in, float* y_out);
 hipError_t launch_fir2(int M, unsigned grid, hipStream_t s, const PresetRt* rt, const int2* jobs,
                        const float2* tables, const float2* hspec, const float* x_in, float* y_out);
+// four-pass variant on 1024 threads (M = 16384 only; fir4_fft.h), same jobs and spectra as k_fir2
+bool fir4_tables_host(int M, std::vector<float>& out);
+hipError_t launch_fir4(int M, unsigned grid, hipStream_t s, const PresetRt* rt, const int2* jobs,
+                       const float2* tables, const float2* hspec, const float* x_in, float* y_out);
 
 void fft_bench_init_attrs();
 hipError_t launch_fft_bench(bool po2, unsigned grid, int lds_bytes, hipStream_t s, const RealPlan* plans, int plan,

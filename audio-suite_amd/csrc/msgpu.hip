@@ -252,6 +252,8 @@ struct msg_ctx {
     uint64_t* d_ke = nullptr; double* d_we = nullptr; double* d_fe = nullptr;
     JumpTab* d_jump = nullptr;
     float2* d_fir2tab[5] = {};   // k_fir2 twiddle tables, M = 1024 << i
+    float2* d_fir4tab = nullptr; // k_fir4 twiddle tables (M = 16384)
+    bool fir4 = true;            // M = 16384 blocks on k_fir4 (MSGPU_FIR4=0: k_fir2, A/B and tests)
     float2* d_spec_ct_tab[SPEC_CT_PLANS] = {};   // compile-time spectral plans (spec_ct.h)
     float2* d_spec3_tab = nullptr;               // band-pruned spectral kernel (spec3.h)
     Slice<int32_t> spec3_list;
@@ -623,6 +625,14 @@ msg_ctx* msg_create(int device_ordinal) {
             return nullptr;
         }
     }
+    {
+        std::vector<float> tab;
+        if (!fir4_tables_host(16384, tab) || !up(ctx->d_fir4tab, reinterpret_cast<float2*>(tab.data()), tab.size() / 2)) {
+            g_err = "uploading FIR4 twiddle tables failed";
+            return nullptr;
+        }
+    }
+    if (const char* e = getenv("MSGPU_FIR4")) ctx->fir4 = e[0] != '0';
     for (int i = 0; i < SPEC_CT_PLANS; ++i) {
         std::vector<float> tab;
         if (!spectral_ct_tables(i, tab) || !up(ctx->d_spec_ct_tab[i], reinterpret_cast<float2*>(tab.data()),
@@ -662,6 +672,7 @@ void msg_destroy(msg_ctx* ctx) {
     hipFree(ctx->d_ki); hipFree(ctx->d_wi); hipFree(ctx->d_fi);
     hipFree(ctx->d_ke); hipFree(ctx->d_we); hipFree(ctx->d_fe); hipFree(ctx->d_jump);
     for (float2* t : ctx->d_fir2tab) hipFree(t);
+    hipFree(ctx->d_fir4tab);
     for (float2* t : ctx->d_spec_ct_tab) hipFree(t);
     hipFree(ctx->d_spec3_tab);
     ctx->sf_prt.release(); ctx->sf_jobs.release(); ctx->sf_irjobs.release(); ctx->sf_h.release();
@@ -875,6 +886,9 @@ int msg_fir(msg_ctx* ctx, const float* x_dev, float* y_dev, int64_t n, int32_t n
     if (fdl)
         HIPCHK(ctx, launch_fdl(N / 2, (unsigned)fj.size(), s, ctx->sf_prt.p, ctx->sf_jobs.p, ctx->d_fir2tab[ti],
                                ctx->sf_hspec.p, ctx->sf_xspec.p, x_dev, y_dev));
+    else if (N / 2 == 16384 && ctx->fir4)
+        HIPCHK(ctx, launch_fir4(N / 2, (unsigned)fj.size(), s, ctx->sf_prt.p, ctx->sf_jobs.p, ctx->d_fir4tab,
+                                ctx->sf_hspec.p, x_dev, y_dev));
     else
         HIPCHK(ctx, launch_fir2(N / 2, (unsigned)fj.size(), s, ctx->sf_prt.p, ctx->sf_jobs.p, ctx->d_fir2tab[ti],
                                 ctx->sf_hspec.p, x_dev, y_dev));
@@ -1575,11 +1589,16 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
                                  ctx->fir_plans.dev.p, ctx->fir_plan_of.p, ctx->er_off.p, ctx->er_gain.p,
                                  ctx->irbank.p, ctx->hscratch.p, ctx->hspec.p));
         stage_mark(ctx, 8, s);
-        for (int i = 0; i < 5; ++i)
-            if (fjob_off[i + 1] > fjob_off[i])
-                HIPCHK(ctx, launch_fir2(1024 << i, (unsigned)(fjob_off[i + 1] - fjob_off[i]), s, ctx->prt.p,
-                                        ctx->fir_jobs.p + fjob_off[i], ctx->d_fir2tab[i], ctx->hspec.p,
-                                        ctx->mono_a.p, ctx->mono_y.p));
+        for (int i = 0; i < 5; ++i) {
+            if (fjob_off[i + 1] <= fjob_off[i]) continue;
+            const unsigned nj = (unsigned)(fjob_off[i + 1] - fjob_off[i]);
+            if (i == 4 && ctx->fir4)
+                HIPCHK(ctx, launch_fir4(16384, nj, s, ctx->prt.p, ctx->fir_jobs.p + fjob_off[i], ctx->d_fir4tab,
+                                        ctx->hspec.p, ctx->mono_a.p, ctx->mono_y.p));
+            else
+                HIPCHK(ctx, launch_fir2(1024 << i, nj, s, ctx->prt.p, ctx->fir_jobs.p + fjob_off[i],
+                                        ctx->d_fir2tab[i], ctx->hspec.p, ctx->mono_a.p, ctx->mono_y.p));
+        }
         stage_mark(ctx, 9, s);
         // presets with fir_on == 0 in a mixed batch: copy a -> y
         for (int p = 0; p < P; ++p)

@@ -46,7 +46,7 @@ HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: 8.0 TB/s spec
 PROFILES = os.path.join(REPO, "profiles")
 # bench stage -> the kernels it times (rocprofv3 kernel-name prefixes)
 STAGE_KERNEL = {"generate": ("k_gen_normal",), "spectral": ("k_spec3", "k_spectral"), "overlap_add": ("k_ola_env",),
-                "fir_kernel": ("k_fir2<",), "stereo": ("k_stereo_max", "k_stereo_out")}
+                "fir_kernel": ("k_fir4<", "k_fir2<"), "stereo": ("k_stereo_max", "k_stereo_out")}
 STAGE_NAMES = ["plan", "host_prep", "generate", "spectral", "overlap_add", "fir", "stereo", "total",
                "fir_kernel", "fir_h", "host_plan_wall", "host_records_wall", "host_upload_wall"]
 KERNEL_STAGES = ["generate", "spectral", "overlap_add", "fir_kernel", "stereo"]

@@ -167,6 +167,45 @@ def test_fir_transform_sizes(msgpu, irs):
     assert all(e <= RMS_TOL for e in errs), errs
 
 
+def test_fir_16384_kernels_agree(msgpu, irs, monkeypatch):
+    """Blocks with M = 16384 (N = 32768, the 192 kHz two-partition case and C3)
+    run on k_fir4 (four passes, 1024 threads) by default and on k_fir2 (three
+    passes, 512 threads) with MSGPU_FIR4=0: both match the oracle, and each
+    other to float32 rounding."""
+    import torch
+    from oracle import msound_oracle as O
+    from msgpu.engine import Engine
+    from msgpu.pack import PackedBatch
+    base = dict(base_sr=48000, out_dur_s=0.3, gen_mode="Resonant strike", event_process="Poisson",
+                space_ir_on=True, seed=21, _ir_audio=irs["tiny_room_ir"])
+    params = [msgpu.merged(base, er_cloud_on=False, space_ir_max_samps=8192),       # IR only, one partition
+              msgpu.merged(base, er_cloud_on=True, space_ir_max_samps=8192),        # ER + IR
+              msgpu.merged(base, base_sr=192000, out_dur_s=0.21, er_cloud_on=True,
+                           space_ir_max_samps=8192)]                                  # Q = 2
+    packed = PackedBatch(params)
+    outs = {}
+    for flag in ("0", "1"):
+        monkeypatch.setenv("MSGPU_FIR4", flag)
+        eng = Engine(0)
+        outs[flag] = eng.render_packed(packed)
+        torch.cuda.synchronize(0)
+        outs[flag] = outs[flag].cpu().numpy()
+    errs = []
+    for i, p in enumerate(params):
+        ref, _ = O.render(p)
+        off, n = int(packed.offsets[i]), int(packed.out_n[i])
+        assert ref.shape[0] == n
+        d = np.abs(outs["0"][off:off + n] - outs["1"][off:off + n])
+        print(f"case {i}: k_fir2 vs k_fir4 max {float(d.max()):.3e} at frame {int(d.max(axis=1).argmax())}")
+        for flag in ("0", "1"):
+            errs.append(rms(outs[flag][off:off + n], ref))
+            print(f"case {i} MSGPU_FIR4={flag}: rms err {errs[-1]:.3e}")
+    assert all(e <= RMS_TOL for e in errs), errs
+    # two float32 transforms of different radix orders: their rounding noise
+    # differs pointwise (up to ~7e-5 at a peak frame), not in rms
+    assert rms(outs["0"], outs["1"]) <= RMS_TOL
+
+
 @pytest.mark.parametrize("name", ["C4", "C5"])
 def test_full_size_configs(msgpu, irs, large_renders, golden_info, name):
     """C4 (384 kHz, 30 MHz design rate) and C5 (8.4 M frames, 4000 events) at full
