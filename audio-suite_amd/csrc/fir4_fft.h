@@ -241,6 +241,246 @@ k_fir4(const PresetRt* __restrict__ rt, const int2* __restrict__ jobs, const flo
     }
 }
 
+// ---------------------------------------------------------------------------
+// Streaming variant: uniformly partitioned overlap-save with the one pending
+// partition product held in registers across a workgroup's consecutive blocks.
+//
+// With the block hop equal to the partition size (B = P = M, N = 2M), the
+// segment of partition q of block b is the segment of partition 0 of block
+// b - q, so X_{b,q} = X_{b-q}.  For Q <= 2 a workgroup walking blocks b0 ..
+// b0+K-1 of one preset keeps A = X_{b-1} . H_1 in the accumulator registers:
+//     Y_b = X_b . H_0 + A,   then A <- X_b . H_1 once Y_b has left for LDS,
+// so a block costs one forward and one inverse transform (plus one forward
+// for X_{b0-1} per workgroup) instead of Q + 1 = 3.  The transforms, the real
+// split and the MAC are k_fir4's, so the result equals k_fir4 run with B = P.
+// Register pressure: A is live through the inverse passes 2'..4' exactly as
+// the accumulator is live through the forward passes of k_fir4's segment loop.
+// Jobs: (preset, first block); the workgroup runs min(K, blocks - b0) blocks.
+//
+// Measured on MI355X (C3, 512 presets per launch, profiles/r02t_*): 17 % fewer
+// transforms and VALU instructions than k_fir4, but every block re-reads H_0
+// and H_1 (256 KB), and with a C3 preset's 24 blocks cut into runs of K the 32
+// workgroups of an XCD touch 32/(24/K) presets at once: their spectra do not
+// stay in the 4 MB L2 beside the x/y streams.  HBM traffic 1.82 -> 3.40 GB
+// (K = 6) / 4.20 GB (K = 12) per launch; isolated kernel time 2.59 ms (k_fir4)
+// vs 2.55-2.67 ms, whole step unchanged.  Hence opt-in (MSGPU_FIR4S=1).
+// ---------------------------------------------------------------------------
+// The x segments and y blocks stream through L2 once (x twice, one block apart,
+// from the same workgroup) while H_0 and H_1 are re-read by every block.
+// MSG_FIR4S_NT=1 (tuning builds) sends the streams with the nontemporal policy:
+// measured on C3 it cut reads 2.6 -> 2.0 GB per 512 presets but split the
+// interleaved y stores into partial lines (writes 0.81 -> 1.24 GB), net slower.
+#ifndef MSG_FIR4S_NT
+#define MSG_FIR4S_NT 0
+#endif
+MSG_DEV float fir4s_ld(const float* p) {
+#if MSG_FIR4S_NT
+    return __builtin_nontemporal_load(p);
+#else
+    return *p;
+#endif
+}
+MSG_DEV float2 fir4s_ld(const float2* p) {
+#if MSG_FIR4S_NT
+    return ff(__builtin_nontemporal_load(reinterpret_cast<const f2v*>(p)));
+#else
+    return *p;
+#endif
+}
+MSG_DEV void fir4s_st(float* p, float v) {
+#if MSG_FIR4S_NT
+    __builtin_nontemporal_store(v, p);
+#else
+    *p = v;
+#endif
+}
+
+// Forward transform of x[s0, s0 + 2M) (zero outside [0, n)), passes 1-4 and the
+// real split: v holds X at bins (js[0] + r NB4, M - that) in k_fir4's slot pairing
+// (thread 0: the slot layout of fir_slots, a[R4-1] = (X[0], X[M]), b[0] = X[M/2]).
+template <int M>
+MSG_DEV void fir4s_forward(float2* buf, const float2* tab, const float* x, int64_t n, int64_t s0,
+                           float2 (&v)[2][Fir4Geo<M>::R4]) {
+    using G = Fir4Geo<M>;
+    constexpr int R1 = G::R1, R2 = G::R2, R3 = G::R3, R4 = G::R4, NB1 = G::NB1, NB4 = G::NB4;
+    const int t = otid();
+    const bool t0z = (t == 0);
+    const int js[2] = {t, t0z ? NB4 / 2 : NB4 - t};
+    const bool fast = s0 >= 0 && s0 + 2 * M <= n && (((uintptr_t)(x + s0)) & 7) == 0;
+    {
+        float2 u[R1];
+        if (fast) {
+            const float2* z = reinterpret_cast<const float2*>(x + s0);
+#pragma unroll
+            for (int r = 0; r < R1; ++r) u[r] = fir4s_ld(z + (uint32_t)(t + r * NB1));
+        } else {
+#pragma unroll
+            for (int r = 0; r < R1; ++r) {
+                const int64_t a = s0 + 2 * (int64_t)(t + r * NB1);
+                const bool in0 = a >= 0 && a < n, in1 = a + 1 >= 0 && a + 1 < n;
+                const float x0 = fir4s_ld(x + (uint32_t)(in0 ? a : 0)), x1 = fir4s_ld(x + (uint32_t)(in1 ? a + 1 : 0));
+                u[r] = make_float2(in0 ? x0 : 0.f, in1 ? x1 : 0.f);
+            }
+        }
+        Dft<R1, false>::run(u);
+        const int base = pads<G::S1>(t * R1);
+#pragma unroll
+        for (int r = 0; r < R1; ++r) buf[base + r] = u[r];
+    }
+    __syncthreads();
+    fir4_pass_lds<M, R2, R1, G::BP2, G::S1, G::S2, true, G::OFF_TA>(buf, tab, t);
+    __syncthreads();
+    fir4_pass_lds<M, R3, R1 * R2, G::BP3, G::S2, G::S3, false, 0>(buf, tab, t);
+    __syncthreads();
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+#pragma unroll
+        for (int r = 0; r < R4; ++r) v[h][r] = buf[pads<G::S3>(js[h] + r * NB4)];
+    }
+    __syncthreads();   // LDS free for the inverse
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        twiddle_pow_ab<R4, tw_base<R4>()>(v[h], fir_wM(tab, G::OFF_MLO, G::OFF_MHI, js[h]),
+                                          fir_wM(tab, G::OFF_MLO, G::OFF_MHI, (js[h] * tw_base<R4>()) & (M - 1)));
+        Dft<R4, false>::run(v[h]);
+    }
+    if (!t0z) {
+        const float2 wA = fir_wM(tab, G::OFF_PLO, G::OFF_PHI, js[0]);
+#pragma unroll
+        for (int r = 0; r < R4; ++r) {
+            float2 xk, xm;
+            fir_split(v[0][r], v[1][R4 - 1 - r], cmul_k(wA, fir_cr<R4>(r)), xk, xm);
+            v[0][r] = xk;
+            v[1][R4 - 1 - r] = xm;
+        }
+    } else {
+        float2 a[R4], bb[R4];
+        fir_slots<R4>(v, a, bb, true);
+#pragma unroll
+        for (int r = 0; r < R4 - 1; ++r) fir_split(a[r], bb[R4 - 1 - r], fir_w0<M, R4>(r), a[r], bb[R4 - 1 - r]);
+        const float2 z0 = a[R4 - 1];
+        a[R4 - 1] = make_float2(z0.x + z0.y, z0.x - z0.y);   // (X[0], X[M]), both real
+        bb[0] = cconj(bb[0]);                                 // X[M/2]
+#pragma unroll
+        for (int r = 0; r < R4; ++r) { v[0][r] = a[r]; v[1][r] = bb[r]; }
+    }
+}
+
+// acc += X . H (bins as fir4s_forward leaves them)
+template <int M>
+MSG_DEV void fir4s_mac(float2 (&acc)[2][Fir4Geo<M>::R4], const float2 (&v)[2][Fir4Geo<M>::R4],
+                       const float2* __restrict__ H) {
+    constexpr int R4 = Fir4Geo<M>::R4, NB4 = Fir4Geo<M>::NB4;
+    const int t = otid();
+    if (t != 0) {
+#pragma unroll
+        for (int r = 0; r < R4; ++r) {
+            const int kA = t + r * NB4;
+            acc[0][r] = cfma(acc[0][r], v[0][r], H[(uint32_t)kA]);
+            acc[1][R4 - 1 - r] = cfma(acc[1][R4 - 1 - r], v[1][R4 - 1 - r], H[(uint32_t)(M - kA)]);
+        }
+    } else {
+#pragma unroll
+        for (int r = 0; r < R4 - 1; ++r) {
+            const int kA = fir_k0<M, R4>(r);
+            acc[0][r] = cfma(acc[0][r], v[0][r], H[kA]);
+            acc[1][R4 - 1 - r] = cfma(acc[1][R4 - 1 - r], v[1][R4 - 1 - r], H[M - kA]);
+        }
+        const float2 x0 = v[0][R4 - 1];
+        acc[0][R4 - 1] = cadd(acc[0][R4 - 1], make_float2(x0.x * H[0].x, x0.y * H[M].x));
+        acc[1][0] = cfma(acc[1][0], v[1][0], H[M / 2]);
+    }
+}
+
+template <int M>
+__global__ void __launch_bounds__(Fir4Geo<M>::T)
+k_fir4s(const PresetRt* __restrict__ rt, const int2* __restrict__ jobs, const float2* __restrict__ tables,
+        const float2* __restrict__ hspec, const float* __restrict__ x_in, float* __restrict__ y_out, int kblk) {
+    using G = Fir4Geo<M>;
+    constexpr int T = G::T, R1 = G::R1, R4 = G::R4, NB1 = G::NB1, NB4 = G::NB4;
+    extern __shared__ __attribute__((aligned(16))) float2 lds[];
+    float2* tab = lds;
+    float2* buf = lds + G::TAB;
+    const int2 job = jobs[xcd_block(blockIdx.x, gridDim.x)];
+    const PresetRt& pr = rt[job.x];
+    const int P = pr.fir_P, Q = pr.fir_Q;   // P == M (B == P), Q <= 2
+    const int64_t n = pr.out_n;
+    const int nblk = (int)((n + P - 1) / P);
+    const int b0 = job.y, b1 = b0 + kblk < nblk ? b0 + kblk : nblk;
+    const float* x = x_in + pr.y_off;
+    float* y = y_out + pr.y_off;
+    const float2* H0 = hspec + pr.h_off;
+    const float2* H1 = H0 + (M + 1);
+    for (int i = threadIdx.x; i < G::TAB_USED; i += T) tab[i] = tables[i];   // visible after the first exchange
+
+    float2 acc[2][R4];
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int r = 0; r < R4; ++r) acc[h][r] = make_float2(0.f, 0.f);
+    // Q == 2: the walk starts one block early, where it only forms A = X_{b0-1} . H_1
+    for (int b = Q == 2 ? b0 - 1 : b0; b < b1; ++b) {
+        const int64_t t0 = (int64_t)b * P;
+        float2 v[2][R4];
+        fir4s_forward<M>(buf, tab, x, n, t0 - (P - 1), v);
+        fir4s_mac<M>(acc, v, b < b0 ? H1 : H0);
+        if (b < b0) continue;
+        // ---- inverse pre-step and pass 1' (registers -> LDS E1'), as k_fir4
+        {
+            const int t = otid();
+            if (t != 0) {
+                const float2 wA = fir_wM(tab, G::OFF_PLO, G::OFF_PHI, t);
+#pragma unroll
+                for (int r = 0; r < R4; ++r) fir_pair_pre(acc[0][r], acc[1][R4 - 1 - r], cmul_k(wA, fir_cr<R4>(r)));
+            } else {
+#pragma unroll
+                for (int r = 0; r < R4 - 1; ++r) fir_pair_pre(acc[0][r], acc[1][R4 - 1 - r], fir_w0<M, R4>(r));
+                const float y0 = acc[0][R4 - 1].x, yN = acc[0][R4 - 1].y;
+                acc[0][R4 - 1] = make_float2(0.5f * (y0 + yN), -0.5f * (y0 - yN));
+                fir_unslots<R4>(acc, true);
+            }
+            const int js[2] = {t, t == 0 ? NB4 / 2 : NB4 - t};
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                Dft<R4, false>::run(acc[h]);
+                const int base = pads<G::S1I>(js[h] * R4);
+#pragma unroll
+                for (int r = 0; r < R4; ++r) buf[base + r] = acc[h][r];
+            }
+        }
+        // ---- A <- X_b . H_1 (Y_b is in LDS; X_b dies here)
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+            for (int r = 0; r < R4; ++r) acc[h][r] = make_float2(0.f, 0.f);
+        if (Q == 2) fir4s_mac<M>(acc, v, H1);
+        __syncthreads();
+        const int t = otid();
+        fir4_pass_lds<M, G::R3, R4, G::BP3, G::S1I, G::S2I, true, G::OFF_TB>(buf, tab, t);
+        __syncthreads();
+        fir4_pass_lds<M, G::R2, R4 * G::R3, G::BP2, G::S2I, G::S3I, false, 0>(buf, tab, t);
+        __syncthreads();
+        // ---- pass 4': LDS (E3') -> DFT_R1 -> outputs [t0, t0 + P) (segment samples u >= P-1)
+        {
+            const float s = 1.0f / (float)M;
+            float2 u[R1];
+#pragma unroll
+            for (int r = 0; r < R1; ++r) u[r] = buf[pads<G::S3I>(t + r * NB1)];
+            twiddle_pow_ab<R1, tw_base<R1>()>(u, fir_wM(tab, G::OFF_MLO, G::OFF_MHI, t),
+                                              fir_wM(tab, G::OFF_MLO, G::OFF_MHI, (t * tw_base<R1>()) & (M - 1)));
+            Dft<R1, false>::run(u);
+#pragma unroll
+            for (int r = 0; r < R1; ++r) {
+                const int w = 2 * (t + r * NB1) - (P - 1);   // output offset in the block
+                const int64_t o = t0 + w;
+                if (w >= 0 && w < P && o < n) fir4s_st(y + (uint32_t)o, u[r].x * s);
+                if (w + 1 >= 0 && w + 1 < P && o + 1 < n) fir4s_st(y + (uint32_t)(o + 1), -u[r].y * s);
+            }
+        }
+        __syncthreads();   // pass 4' reads done before the next forward's pass 1 writes
+    }
+}
+
 // Host: the twiddle tables of Fir4Geo<M> (float64-built, rounded once).
 template <int M>
 inline void fir4_tables(std::vector<float>& out) {

@@ -16,6 +16,8 @@ template <int M> static void fir2_attr() {
 void fir_init_attrs() {
     (void)hipFuncSetAttribute((const void*)k_fir4<16384>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               Fir4Geo<16384>::LDS_BYTES);
+    (void)hipFuncSetAttribute((const void*)k_fir4s<16384>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              Fir4Geo<16384>::LDS_BYTES);
     fir2_attr<1024>(); fir2_attr<2048>(); fir2_attr<4096>(); fir2_attr<8192>(); fir2_attr<16384>();
     (void)hipFuncSetAttribute((const void*)k_fir_h<FIR_T, FIR_M>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
     (void)hipFuncSetAttribute((const void*)k_fir_hconv<FIR_T, FIR_M>, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -90,6 +92,15 @@ hipError_t launch_fir4(int M, unsigned grid, hipStream_t s, const PresetRt* rt, 
     if (M != 16384) return hipErrorInvalidValue;
     hipLaunchKernelGGL((k_fir4<16384>), dim3(grid), dim3(Fir4Geo<16384>::T), Fir4Geo<16384>::LDS_BYTES, s, rt, jobs,
                        tables, hspec, x_in, y_out);
+    return hipGetLastError();
+}
+
+hipError_t launch_fir4s(int M, unsigned grid, hipStream_t s, const PresetRt* rt, const int2* jobs,
+                        const float2* tables, const float2* hspec, const float* x_in, float* y_out, int kblk) {
+    static_assert(FIR4S_P == 16384, "k_fir4s<16384>: P = M");
+    if (M != 16384 || kblk < 1) return hipErrorInvalidValue;
+    hipLaunchKernelGGL((k_fir4s<16384>), dim3(grid), dim3(Fir4Geo<16384>::T), Fir4Geo<16384>::LDS_BYTES, s, rt, jobs,
+                       tables, hspec, x_in, y_out, kblk);
     return hipGetLastError();
 }
 

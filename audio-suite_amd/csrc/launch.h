@@ -59,6 +59,10 @@ hipError_t launch_fir2(int M, unsigned grid, hipStream_t s, const PresetRt* rt, 
 bool fir4_tables_host(int M, std::vector<float>& out);
 hipError_t launch_fir4(int M, unsigned grid, hipStream_t s, const PresetRt* rt, const int2* jobs,
                        const float2* tables, const float2* hspec, const float* x_in, float* y_out);
+// streaming variant (B = P = 16384, Q <= 2): jobs (preset, first block), kblk blocks per workgroup
+constexpr int FIR4S_P = 16384;
+hipError_t launch_fir4s(int M, unsigned grid, hipStream_t s, const PresetRt* rt, const int2* jobs,
+                        const float2* tables, const float2* hspec, const float* x_in, float* y_out, int kblk);
 
 void fft_bench_init_attrs();
 hipError_t launch_fft_bench(bool po2, unsigned grid, int lds_bytes, hipStream_t s, const RealPlan* plans, int plan,

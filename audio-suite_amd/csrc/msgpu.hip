@@ -254,6 +254,14 @@ struct msg_ctx {
     float2* d_fir2tab[5] = {};   // k_fir2 twiddle tables, M = 1024 << i
     float2* d_fir4tab = nullptr; // k_fir4 twiddle tables (M = 16384)
     bool fir4 = true;            // M = 16384 blocks on k_fir4 (MSGPU_FIR4=0: k_fir2, A/B and tests)
+    // Q <= 2 presets on the streaming k_fir4s (MSGPU_FIR4S=1; off by default: at
+    // C3's 24 blocks per preset its H re-reads miss L2 and cancel the saved transforms)
+    bool fir4s = false;
+    int fir4s_wgs = 1024;        // k_fir4s workgroups a batch aims for (MSGPU_FIR4S_WGS)
+    // at most this many blocks per k_fir4s workgroup (MSGPU_FIR4S_K): every block
+    // re-reads H_0 and H_1 (2 x 128 KB), so the workgroups running at once on an
+    // XCD must share presets for those reads to hit its 4 MB L2
+    int fir4s_kmax = 6;
     float2* d_spec_ct_tab[SPEC_CT_PLANS] = {};   // compile-time spectral plans (spec_ct.h)
     float2* d_spec3_tab = nullptr;               // band-pruned spectral kernel (spec3.h)
     Slice<int32_t> spec3_list;
@@ -491,7 +499,11 @@ static double bessel_j(int m, double x) {
 // Choose (N, P, Q) minimising FFT work for an M-tap FIR over n outputs.
 // need: with early reflections the whole kernel h is built in one transform
 // (k_fir_h), so only N >= need qualify (M - 1 with an IR, M without).
-static void choose_fir(int64_t M, int64_t n, int64_t need, int& N, int& P, int& Q) {
+// stream: when non-null, also consider k_fir4s (N = 32768, P = B = 16384, Q <= 2:
+// one forward and one inverse transform per block plus, for Q = 2, one forward
+// per workgroup of kblk blocks) and report whether it won.
+static void choose_fir(int64_t M, int64_t n, int64_t need, int& N, int& P, int& Q, bool* stream = nullptr,
+                       int kblk = 1) {
     double best = 1e300;
     N = FIR_NMAX; P = (int)std::min<int64_t>(M, FIR_NMAX / 2); Q = (int)((M + P - 1) / P);
     for (int lg = 11; lg <= 15; ++lg) {   // k_fir2 sizes: M = N/2 in 1024..16384
@@ -504,6 +516,16 @@ static void choose_fir(int64_t M, int64_t n, int64_t need, int& N, int& P, int& 
             const int64_t blocks = (n + B - 1) / B;
             const double cost = (double)blocks * (q + 1) * NN * lg + (double)blocks * NN * 4.0;
             if (cost < best) { best = cost; N = NN; P = (int)pp; Q = q; }
+        }
+    }
+    if (stream) {
+        *stream = false;
+        const int NN = 2 * FIR4S_P, lg = 15;
+        const int64_t q = (M + FIR4S_P - 1) / FIR4S_P;
+        if (NN >= need && q <= 2) {
+            const int64_t blocks = (n + FIR4S_P - 1) / FIR4S_P;
+            const double cost = (double)blocks * (2.0 + (q - 1) / (double)kblk) * NN * lg + (double)blocks * NN * 4.0;
+            if (cost < best) { best = cost; N = NN; P = FIR4S_P; Q = (int)q; *stream = true; }
         }
     }
 }
@@ -633,6 +655,9 @@ msg_ctx* msg_create(int device_ordinal) {
         }
     }
     if (const char* e = getenv("MSGPU_FIR4")) ctx->fir4 = e[0] != '0';
+    if (const char* e = getenv("MSGPU_FIR4S")) ctx->fir4s = e[0] == '1';
+    if (const char* e = getenv("MSGPU_FIR4S_WGS")) ctx->fir4s_wgs = std::max(1, atoi(e));
+    if (const char* e = getenv("MSGPU_FIR4S_K")) ctx->fir4s_kmax = std::max(2, std::min(64, atoi(e)));
     for (int i = 0; i < SPEC_CT_PLANS; ++i) {
         std::vector<float> tab;
         if (!spectral_ct_tables(i, tab) || !up(ctx->d_spec_ct_tab[i], reinterpret_cast<float2*>(tab.data()),
@@ -1116,7 +1141,8 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
     std::vector<int32_t> spec3;                           // events of the band-pruned kernel
     std::vector<int32_t> f32_presets;                     // presets on the float32 chain
     std::map<std::pair<int, int>, int64_t> ir_spec_of;   // (IR index, N) -> offset
-    std::vector<int2> fjobs_by[5];                        // FIR output blocks per transform size
+    std::vector<int2> fjobs_by[6];                        // FIR output blocks per transform size; [5]: k_fir4s
+    std::vector<int2> fir4s_presets;                      // (preset, blocks) on the streaming FIR
     std::vector<int64_t> ir_jobs;                         // [ir_off, ir_len, plan, out_off] per job
     // float64 grain chain records
     std::vector<Ev64> ev64;
@@ -1137,6 +1163,35 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
     int64_t g64_big_cap = 0;                              // slot size of the global-class grains
     std::vector<int32_t> g64_lds, g64_glb;                // Ev64 indices by class
     std::vector<Chain64> chains_glb;
+    // Space-FIR taps of preset p ((delta + ER) * IR, MS:409-445), 0 without a FIR;
+    // need: the smallest transform that builds h in one piece
+    auto fir_taps = [&](int p, int64_t& need) -> int64_t {
+        const msg_preset& pr = presets[p];
+        const bool er = (pr.flags & MSG_F_ER_CLOUD) != 0;
+        const int ic = pr.ir_conv;
+        const bool ir = (pr.flags & MSG_F_SPACE_IR) && ic >= 0 && ir_lens[ic] > 0;
+        need = 0;
+        if (!er && !ir) return 0;
+        const int64_t er_span = er ? (int64_t)std::nearbyint(pr.er_max_ms / 1000.0 * (double)pr.base_sr) + 1 : 0;
+        const int64_t M = (ir ? std::min<int64_t>(ir_lens[ic], 8192) : 1) + er_span;
+        need = er ? (ir ? M - 1 : M) : 0;
+        return M;
+    };
+    // k_fir4s pays one extra forward transform per workgroup: it is offered only
+    // when the batch's streaming-eligible blocks give >= 2 blocks per workgroup
+    bool fir4s_ok = false;
+    int fir4s_k = 1;                                      // blocks per k_fir4s workgroup
+    if (ctx->fir4 && ctx->fir4s) {
+        int64_t total = 0;
+        for (int p = 0; p < P; ++p) {
+            int64_t need;
+            const int64_t M = fir_taps(p, need);
+            if (M > 0 && M <= 2 * FIR4S_P && need <= 2 * FIR4S_P)
+                total += (info[p].out_n + FIR4S_P - 1) / FIR4S_P;
+        }
+        fir4s_k = (int)std::min<int64_t>(ctx->fir4s_kmax, total / std::max(1, ctx->fir4s_wgs));
+        fir4s_ok = fir4s_k >= 2;
+    }
     for (int p = 0; p < P; ++p) {
         const msg_preset& pr = presets[p];
         const msg_plan_info& inf = info[p];
@@ -1194,16 +1249,17 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
         r.fir_block_begin = fblocks;   // prefix arrays must stay monotone for find_preset
         r.h_block_begin = hblocks;
         if (r.fir_on) {
-            const int64_t er_span = er ? (int64_t)std::nearbyint(pr.er_max_ms / 1000.0 * sr) + 1 : 0;
-            const int64_t M = (ir ? r.ir_len : 1) + er_span;
+            int64_t need;
+            const int64_t M = fir_taps(p, need);
             int N, Pp, Q;
-            choose_fir(M, inf.out_n, er ? (ir ? M - 1 : M) : 0, N, Pp, Q);
+            bool stream = false;
+            choose_fir(M, inf.out_n, need, N, Pp, Q, fir4s_ok ? &stream : nullptr, fir4s_k);
             std::string why;
             const int fp = real_plan(ctx->fir_plans, N, why);
             if (fp < 0) return fail(ctx, MSG_E_DEVICE, "FIR plan: " + why);
             fir_plan_of[p] = fp;
             fir_lds = std::max(fir_lds, ctx->fir_plans.host[fp].lds_bytes);
-            r.fir_N = N; r.fir_P = Pp; r.fir_Q = Q; r.fir_B = N - Pp + 1;
+            r.fir_N = N; r.fir_P = Pp; r.fir_Q = Q; r.fir_B = stream ? Pp : N - Pp + 1;
             r.h_off = hsum;
             if (er && ir) {
                 if (M - 1 > N)
@@ -1224,8 +1280,12 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
                 return fail(ctx, MSG_E_UNSUPPORTED, "early-reflection span exceeds the FIR transform");
             }
             const int32_t nblk = (int32_t)((inf.out_n + r.fir_B - 1) / r.fir_B);
-            std::vector<int2>& fj = fjobs_by[__builtin_ctz(N) - 11];
-            for (int32_t b = 0; b < nblk; ++b) fj.push_back(make_int2(p, b));
+            if (stream) {
+                fir4s_presets.push_back(make_int2(p, nblk));   // jobs cut once the batch's total is known
+            } else {
+                std::vector<int2>& fj = fjobs_by[__builtin_ctz(N) - 11];
+                for (int32_t b = 0; b < nblk; ++b) fj.push_back(make_int2(p, b));
+            }
             fblocks += nblk;
             hblocks += Q;
             hsum += (int64_t)Q * (N / 2 + 1);
@@ -1460,13 +1520,16 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
     HIPCHK(ctx, ctx->state64.ensure(state_sum));
     HIPCHK(ctx, ctx->so_r2.ensure(r2_sum));
     HIPCHK(ctx, ctx->so_A.ensure(so_M));
+    // k_fir4s: each workgroup walks fir4s_k consecutive blocks of one preset
+    for (const int2& pb : fir4s_presets)
+        for (int32_t b = 0; b < pb.y; b += fir4s_k) fjobs_by[5].push_back(make_int2(pb.x, b));
     std::vector<int2> fir_jobs;
-    int32_t fjob_off[6] = {0};
-    for (int i = 0; i < 5; ++i) {
+    int32_t fjob_off[7] = {0};
+    for (int i = 0; i < 6; ++i) {
         fjob_off[i] = (int32_t)fir_jobs.size();
         fir_jobs.insert(fir_jobs.end(), fjobs_by[i].begin(), fjobs_by[i].end());
     }
-    fjob_off[5] = (int32_t)fir_jobs.size();
+    fjob_off[6] = (int32_t)fir_jobs.size();
     HIPCHK(ctx, ctx->micro.ensure(pool));
     HIPCHK(ctx, ctx->grain.ensure(pool));
     HIPCHK(ctx, ctx->mono_a.ensure(ysum));
@@ -1589,10 +1652,13 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
                                  ctx->fir_plans.dev.p, ctx->fir_plan_of.p, ctx->er_off.p, ctx->er_gain.p,
                                  ctx->irbank.p, ctx->hscratch.p, ctx->hspec.p));
         stage_mark(ctx, 8, s);
-        for (int i = 0; i < 5; ++i) {
+        for (int i = 0; i < 6; ++i) {
             if (fjob_off[i + 1] <= fjob_off[i]) continue;
             const unsigned nj = (unsigned)(fjob_off[i + 1] - fjob_off[i]);
-            if (i == 4 && ctx->fir4)
+            if (i == 5)
+                HIPCHK(ctx, launch_fir4s(16384, nj, s, ctx->prt.p, ctx->fir_jobs.p + fjob_off[i], ctx->d_fir4tab,
+                                         ctx->hspec.p, ctx->mono_a.p, ctx->mono_y.p, fir4s_k));
+            else if (i == 4 && ctx->fir4)
                 HIPCHK(ctx, launch_fir4(16384, nj, s, ctx->prt.p, ctx->fir_jobs.p + fjob_off[i], ctx->d_fir4tab,
                                         ctx->hspec.p, ctx->mono_a.p, ctx->mono_y.p));
             else

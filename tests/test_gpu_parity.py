@@ -206,6 +206,56 @@ def test_fir_16384_kernels_agree(msgpu, irs, monkeypatch):
     assert rms(outs["0"], outs["1"]) <= RMS_TOL
 
 
+def test_fir_streaming_kernel(msgpu, irs, full_renders, monkeypatch):
+    """Two-partition presets at N = 32768 (C3's ER + IR filter) run on the
+    streaming k_fir4s (opt-in, MSGPU_FIR4S=1) when the batch gives >= 2 blocks
+    per workgroup: B = P =
+    16384, the pending X_{b-1} . H_1 kept in registers across a workgroup's
+    blocks.  MSGPU_FIR4S_WGS=1 puts whole presets (6, 12 and 8 blocks) on one
+    workgroup, =8 cuts them into runs of 3 blocks (workgroup boundaries inside
+    every preset);
+    both match the reference renders, the oracle and the recomputing kernel
+    (MSGPU_FIR4S=0) to float32 rounding."""
+    import torch
+    from oracle import msound_oracle as O
+    from msgpu.engine import Engine
+    from msgpu.pack import PackedBatch
+    params = [msgpu.config_params("C3", seed=1001, irs=irs, out_dur_s=0.25),
+              msgpu.config_params("C3", seed=1002, irs=irs, out_dur_s=0.5),
+              msgpu.merged(base_sr=192000, out_dur_s=0.6826, gen_mode="Resonant strike", event_process="Poisson",
+                           space_ir_on=True, seed=21, er_cloud_on=True, space_ir_max_samps=8192,
+                           _ir_audio=irs["tiny_room_ir"])]
+    packed = PackedBatch(params)
+    outs = {}
+    for key, env in (("off", {"MSGPU_FIR4S": "0"}), ("w1", {"MSGPU_FIR4S": "1", "MSGPU_FIR4S_WGS": "1"}),
+                     ("w8", {"MSGPU_FIR4S": "1", "MSGPU_FIR4S_WGS": "8"})):
+        monkeypatch.delenv("MSGPU_FIR4S", raising=False)
+        monkeypatch.delenv("MSGPU_FIR4S_WGS", raising=False)
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        eng = Engine(0)
+        outs[key] = eng.render_packed(packed)
+        torch.cuda.synchronize(0)
+        outs[key] = outs[key].cpu().numpy()
+    off0, n0 = int(packed.offsets[0]), int(packed.out_n[0])
+    for key in outs:
+        e = rms(outs[key][off0:off0 + n0], full_renders["C3s1001_audio"])
+        print(f"C3 seed 1001 0.25 s [{key}]: rms err vs reference {e:.3e}")
+        assert e <= RMS_TOL, key
+    for i, p in enumerate(params):
+        ref, _ = O.render(p)
+        off, n = int(packed.offsets[i]), int(packed.out_n[i])
+        for key in outs:
+            e = rms(outs[key][off:off + n], ref)
+            print(f"case {i} [{key}]: rms err vs oracle {e:.3e}")
+            assert e <= RMS_TOL, (i, key)
+    # the streaming runs agree with each other exactly (same transforms, same
+    # order of the two partition products), and with the recomputing kernel at
+    # float32 rounding (different block length B)
+    assert np.array_equal(outs["w1"], outs["w8"])
+    assert rms(outs["off"], outs["w1"]) <= RMS_TOL
+
+
 @pytest.mark.parametrize("name", ["C4", "C5"])
 def test_full_size_configs(msgpu, irs, large_renders, golden_info, name):
     """C4 (384 kHz, 30 MHz design rate) and C5 (8.4 M frames, 4000 events) at full
