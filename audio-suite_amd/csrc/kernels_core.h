@@ -45,7 +45,15 @@ __global__ void k_plan_events(const msg_preset* __restrict__ presets, int n_pres
 #define MSG_GEN_G 8
 #endif
 constexpr int GEN_G = MSG_GEN_G;   // chunks of 64 draws classified per pass
-struct JumpTab { nprng::u128 a[GEN_T]; nprng::u128 s[GEN_T]; nprng::u128 a64, s64, aG, sG; };
+// MSG_GEN_LDS=0 (tuning builds): the ziggurat tables are read through L1 and the
+// resonant rotation by cross-lane reads, so k_gen_normal allocates no LDS and its
+// waves can sit beside k_spec3's 162 KB workgroups.
+#ifndef MSG_GEN_LDS
+#define MSG_GEN_LDS 1
+#endif
+// Jump-ahead constants and the ziggurat fast-path table (ki >> 20, wi * 2^20 as
+// float32 bits).
+struct JumpTab { nprng::u128 a[GEN_T]; nprng::u128 s[GEN_T]; nprng::u128 a64, s64, aG, sG; uint2 kw[256]; };
 
 MSG_DEV double slow_normal(nprng::u128 st, nprng::u128 inc, uint64_t rabs, int idx, double x,
                            const nprng::Zig& z, int& consumed) {
@@ -143,18 +151,26 @@ k_gen_normal(const msg_preset* __restrict__ presets, const msg_event* __restrict
              const PresetRt* __restrict__ rt, const int32_t* __restrict__ ev_list, int n_list,
              nprng::Zig z, const JumpTab* __restrict__ jt, float* __restrict__ pool,
              double* __restrict__ pool64, const int64_t* __restrict__ off64) {
+#if MSG_GEN_LDS
     __shared__ uint64_t s_ki[256];
     __shared__ double s_wi[256];
     __shared__ uint2 s_kw[256];          // (ki >> 20, wi * 2^20 as float32 bits): the fast path's one read
     __shared__ float4 s_rot[64];         // resonant: (cos, sin)(2 pi r f/sr), 2^(r k_ring), 2^(r k_exc), r < 64
+#else
+    const uint64_t* __restrict__ s_ki = z.ki;
+    const double* __restrict__ s_wi = z.wi;
+    const uint2* __restrict__ s_kw = jt->kw;
+#endif
     const int li = blockIdx.x;
     if (li >= n_list) return;
     const int lane = threadIdx.x;
+#if MSG_GEN_LDS
     for (int i = lane; i < 256; i += GEN_T) {
         s_ki[i] = z.ki[i];
         s_wi[i] = z.wi[i];
-        s_kw[i] = make_uint2((uint32_t)(z.ki[i] >> 20), __float_as_uint((float)(z.wi[i] * 1048576.0)));
+        s_kw[i] = jt->kw[i];
     }
+#endif
     const msg_event& e = events[ev_list[li]];
     const msg_preset& pr = presets[e.preset];
     const PresetRt& r = rt[e.preset];
@@ -181,11 +197,15 @@ k_gen_normal(const msg_preset* __restrict__ presets, const msg_event* __restrict
     // emitted, r = the lane's rank) from the chunk's uniform sin/cos and decay
     // at j0 and the per-rank rotation/decay table (angle addition, one ds_read
     // per sample instead of the phase reduction, a sine and two exponentials).
+    float4 rot = make_float4(0.f, 0.f, 0.f, 0.f);
     if (!RAW64 && c.mode == MSG_GEN_RESONANT) {
         const float rf = (float)lane;
         const float ph = ring_phase(rf, c.fa, c.fb);
-        s_rot[lane] = make_float4(__builtin_amdgcn_cosf(ph), __builtin_amdgcn_sinf(ph),
-                                  __builtin_amdgcn_exp2f(rf * c.k_ring), __builtin_amdgcn_exp2f(rf * c.k_exc));
+        rot = make_float4(__builtin_amdgcn_cosf(ph), __builtin_amdgcn_sinf(ph),
+                          __builtin_amdgcn_exp2f(rf * c.k_ring), __builtin_amdgcn_exp2f(rf * c.k_exc));
+#if MSG_GEN_LDS
+        s_rot[lane] = rot;
+#endif
     }
 
     // default_rng(seed + i): every lane computes the (uniform) seed state.
@@ -207,7 +227,9 @@ k_gen_normal(const msg_preset* __restrict__ presets, const msg_event* __restrict
     for (int g = 1; g < G; ++g) st[g] = a64 * st[g - 1] + c64;
     const nprng::u128 aG = jt->aG;
     const nprng::u128 cG = inc * jt->sG;
+#if MSG_GEN_LDS
     __syncthreads();
+#endif
 
     int produced = 0;
     int local = 0;   // first lane of the current chunk not consumed by an earlier slow normal
@@ -300,11 +322,16 @@ k_gen_normal(const msg_preset* __restrict__ presets, const msg_event* __restrict
                 const float dA = __builtin_amdgcn_exp2f(fmaxf(j0 * c.k_ring, -126.f));
                 const float dE = __builtin_amdgcn_exp2f(fmaxf(j0 * c.k_exc, -126.f));
                 const bool edge = produced < c.fade || produced + 64 > c.n - c.fade;
+                const int rk = __popcll(valid & ((1ULL << lane) - 1));
+#if MSG_GEN_LDS
+                const float4 tb = s_rot[rk];
+#else
+                const float4 tb = make_float4(__shfl(rot.x, rk), __shfl(rot.y, rk), __shfl(rot.z, rk),
+                                              __shfl(rot.w, rk));   // every lane: lane rk holds rank rk's rotation
+#endif
                 if ((valid >> lane) & 1) {
-                    const int rk = __popcll(valid & ((1ULL << lane) - 1));
                     const int j = produced + rk;
                     if (j < n) {
-                        const float4 tb = s_rot[rk];
                         float v = 0.9f * fmaf(s0, tb.x, c0 * tb.y) * (dA * tb.z) + 0.25f * x[g] * (dE * tb.w);
                         if (edge) v = gen_fade(c, j, v);
                         out[j] = v;

@@ -638,6 +638,12 @@ msg_ctx* msg_create(int device_ordinal) {
     jt.a64 = j64.a; jt.s64 = j64.s;
     const nprng::Jump jG = nprng::jump_of((uint64_t)GEN_T * GEN_G);
     jt.aG = jG.a; jt.sG = jG.s;
+    for (int i = 0; i < 256; ++i) {
+        const float w = (float)(zig_wi_double[i] * 1048576.0);
+        uint32_t wb;
+        memcpy(&wb, &w, 4);
+        jt.kw[i] = make_uint2((uint32_t)(zig_ki_double[i] >> 20), wb);
+    }
     if (!up(ctx->d_jump, &jt, 1)) { g_err = "uploading jump table failed"; return nullptr; }
     for (int i = 0; i < 5; ++i) {
         std::vector<float> tab;
