@@ -18,6 +18,10 @@ void fir_init_attrs() {
                               Fir4Geo<16384>::LDS_BYTES);
     (void)hipFuncSetAttribute((const void*)k_fir4s<16384>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               Fir4Geo<16384>::LDS_BYTES);
+    (void)hipFuncSetAttribute((const void*)k_fir4_hconv<16384>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              Fir4Geo<16384>::LDS_BYTES);
+    (void)hipFuncSetAttribute((const void*)k_fir4_hpart<16384>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              Fir4Geo<16384>::LDS_BYTES);
     fir2_attr<1024>(); fir2_attr<2048>(); fir2_attr<4096>(); fir2_attr<8192>(); fir2_attr<16384>();
     (void)hipFuncSetAttribute((const void*)k_fir_h<FIR_T, FIR_M>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
     (void)hipFuncSetAttribute((const void*)k_fir_hconv<FIR_T, FIR_M>, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -101,6 +105,19 @@ hipError_t launch_fir4s(int M, unsigned grid, hipStream_t s, const PresetRt* rt,
     if (M != 16384 || kblk < 1) return hipErrorInvalidValue;
     hipLaunchKernelGGL((k_fir4s<16384>), dim3(grid), dim3(Fir4Geo<16384>::T), Fir4Geo<16384>::LDS_BYTES, s, rt, jobs,
                        tables, hspec, x_in, y_out, kblk);
+    return hipGetLastError();
+}
+
+hipError_t launch_fir4_h(int M, unsigned n_conv, unsigned n_parts, hipStream_t s, const PresetRt* rt,
+                         const int32_t* conv_list, const int2* part_jobs, const float2* tables, const int32_t* er_off,
+                         const double* er_gain, const float2* ir_spec, float* hs, float2* hspec) {
+    if (M != 16384) return hipErrorInvalidValue;
+    hipLaunchKernelGGL((k_fir4_hconv<16384>), dim3(n_conv), dim3(Fir4Geo<16384>::T), Fir4Geo<16384>::LDS_BYTES, s, rt,
+                       conv_list, tables, er_off, er_gain, ir_spec, hs);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL((k_fir4_hpart<16384>), dim3(n_parts), dim3(Fir4Geo<16384>::T), Fir4Geo<16384>::LDS_BYTES, s,
+                       rt, part_jobs, tables, (const float*)hs, hspec);
     return hipGetLastError();
 }
 

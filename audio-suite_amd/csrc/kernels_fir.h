@@ -80,6 +80,7 @@ k_fir_h(const PresetRt* __restrict__ rt, const int32_t* __restrict__ hblk_begin,
     const int b = blockIdx.x;
     const int p = find_preset(hblk_begin, n_presets, b);
     const PresetRt& r = rt[p];
+    if (r.h_fir4) return;   // built by k_fir4_hconv / k_fir4_hpart (fir4_fft.h)
     const int q = b - r.h_block_begin;
     const RealPlan& rp = fir_plans[fir_plan_of[p]];
     const bool evn = rp.even != 0;

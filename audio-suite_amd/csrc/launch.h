@@ -61,6 +61,11 @@ hipError_t launch_fir4(int M, unsigned grid, hipStream_t s, const PresetRt* rt, 
                        const float2* tables, const float2* hspec, const float* x_in, float* y_out);
 // streaming variant (B = P = 16384, Q <= 2): jobs (preset, first block), kblk blocks per workgroup
 constexpr int FIR4S_P = 16384;
+// ER + IR partition spectra on the k_fir4 engine (fir4_fft.h): k_fir4_hconv over
+// conv_list, then k_fir4_hpart over the (preset, q) jobs.
+hipError_t launch_fir4_h(int M, unsigned n_conv, unsigned n_parts, hipStream_t s, const PresetRt* rt,
+                         const int32_t* conv_list, const int2* part_jobs, const float2* tables, const int32_t* er_off,
+                         const double* er_gain, const float2* ir_spec, float* hs, float2* hspec);
 hipError_t launch_fir4s(int M, unsigned grid, hipStream_t s, const PresetRt* rt, const int2* jobs,
                         const float2* tables, const float2* hspec, const float* x_in, float* y_out, int kblk);
 

@@ -287,7 +287,8 @@ struct msg_ctx {
     DevBuf<float> micro, grain, mono_a, mono_y;
     DevBuf<float2> hspec, irspec;
     DevBuf<float> hscratch;                     // h of ER + IR presets (k_fir_hconv -> k_fir_h)
-    Slice<int32_t> conv_list;
+    Slice<int32_t> conv_list, conv4_list;
+    Slice<int2> hpart_jobs;
     Slice<int2> fir_jobs;
     Slice<int32_t> spec_ct_list;
     Slice<int64_t> irjobs;
@@ -1132,7 +1133,9 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
     }
     int64_t pool = 0, ysum = 0, hsum = 0, irs_sum = 0;
     int32_t tiles = 0, fblocks = 0, hblocks = 0, stiles = 0;
-    std::vector<int32_t> conv_list;
+    std::vector<int32_t> conv_list, conv4_list;   // ER + IR presets: runtime-plan engine / k_fir4 engine
+    std::vector<int2> hpart_jobs;                  // (preset, q) of the conv4_list presets
+    int32_t hblocks_gen = 0;                       // k_fir_h blocks of presets not on the k_fir4 engine
     int64_t hs_sum = 0;
     int spec_small_lds = 0, spec_big_lds = 0, fir_lds = 0;
     std::vector<int32_t> spec_ct[SPEC_CT_PLANS];           // events of the compile-time spectral plans
@@ -1254,6 +1257,7 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
         r.fir_on = (er || ir) ? 1 : 0;
         r.fir_block_begin = fblocks;   // prefix arrays must stay monotone for find_preset
         r.h_block_begin = hblocks;
+        r.h_fir4 = 0;
         if (r.fir_on) {
             int64_t need;
             const int64_t M = fir_taps(p, need);
@@ -1281,7 +1285,13 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
                 r.irs_off = it->second;
                 r.hs_off = hs_sum;
                 hs_sum += N;
-                conv_list.push_back(p);
+                if (N == 2 * 16384 && ctx->fir4) {   // the C3/C4 size: k_fir4_hconv + k_fir4_hpart
+                    r.h_fir4 = 1;
+                    conv4_list.push_back(p);
+                    for (int q = 0; q < Q; ++q) hpart_jobs.push_back(make_int2(p, q));
+                } else {
+                    conv_list.push_back(p);
+                }
             } else if (er && M > N) {
                 return fail(ctx, MSG_E_UNSUPPORTED, "early-reflection span exceeds the FIR transform");
             }
@@ -1294,6 +1304,7 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
             }
             fblocks += nblk;
             hblocks += Q;
+            if (!r.h_fir4) hblocks_gen += Q;
             hsum += (int64_t)Q * (N / 2 + 1);
         }
         fir_begin[p] = r.fir_block_begin;
@@ -1572,6 +1583,8 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
     HIPCHK(ctx, h2d(&ctx->irbank.p, irbank.data(), sizeof(double) * irbank.size()));
     HIPCHK(ctx, h2d(&ctx->irjobs.p, ir_jobs.data(), sizeof(int64_t) * ir_jobs.size()));
     HIPCHK(ctx, h2d(&ctx->conv_list.p, conv_list.data(), sizeof(int32_t) * conv_list.size()));
+    HIPCHK(ctx, h2d(&ctx->conv4_list.p, conv4_list.data(), sizeof(int32_t) * conv4_list.size()));
+    HIPCHK(ctx, h2d(&ctx->hpart_jobs.p, hpart_jobs.data(), sizeof(int2) * hpart_jobs.size()));
     HIPCHK(ctx, hipMemsetAsync(ctx->maxbits.p, 0, sizeof(unsigned) * P, s));
     HIPCHK(ctx, h2d(&ctx->ev64.p, ev64.data(), sizeof(Ev64) * ev64.size()));
     HIPCHK(ctx, h2d(&ctx->g64_list.p, g64_list.data(), sizeof(int32_t) * g64_list.size()));
@@ -1654,9 +1667,14 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
             HIPCHK(ctx, launch_fir_hconv((unsigned)conv_list.size(), fir_lds, s, ctx->prt.p, ctx->conv_list.p,
                                          ctx->fir_plans.dev.p, ctx->fir_plan_of.p, ctx->er_off.p, ctx->er_gain.p,
                                          ctx->irspec.p, ctx->hscratch.p));
-        HIPCHK(ctx, launch_fir_h((unsigned)hblocks, fir_lds, s, ctx->prt.p, ctx->h_begin.p, P,
-                                 ctx->fir_plans.dev.p, ctx->fir_plan_of.p, ctx->er_off.p, ctx->er_gain.p,
-                                 ctx->irbank.p, ctx->hscratch.p, ctx->hspec.p));
+        if (!conv4_list.empty())
+            HIPCHK(ctx, launch_fir4_h(16384, (unsigned)conv4_list.size(), (unsigned)hpart_jobs.size(), s, ctx->prt.p,
+                                      ctx->conv4_list.p, ctx->hpart_jobs.p, ctx->d_fir4tab, ctx->er_off.p,
+                                      ctx->er_gain.p, ctx->irspec.p, ctx->hscratch.p, ctx->hspec.p));
+        if (hblocks_gen > 0)   // blocks of k_fir4-engine presets return at once
+            HIPCHK(ctx, launch_fir_h((unsigned)hblocks, fir_lds, s, ctx->prt.p, ctx->h_begin.p, P,
+                                     ctx->fir_plans.dev.p, ctx->fir_plan_of.p, ctx->er_off.p, ctx->er_gain.p,
+                                     ctx->irbank.p, ctx->hscratch.p, ctx->hspec.p));
         stage_mark(ctx, 8, s);
         for (int i = 0; i < 6; ++i) {
             if (fjob_off[i + 1] <= fjob_off[i]) continue;

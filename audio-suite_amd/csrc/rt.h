@@ -43,7 +43,7 @@ struct PresetRt {
     int32_t dl, dr;
     float bess[25];        // J_m(0.9 w), m = -12..12
     float drive, peak;
-    int32_t pad2;
+    int32_t h_fir4;        // 1: partition spectra built on the k_fir4 engine (k_fir4_hconv/hpart)
     // generator sources: IR fragment (float64 IR bank) and image (uint8 bank)
     int64_t frag_off, frag_len;
     int64_t img_off;
