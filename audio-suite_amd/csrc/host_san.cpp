@@ -50,6 +50,7 @@ int msg_last_events(msg_ctx*, int32_t, msg_event*, int32_t, int32_t*) { return n
 int msg_last_meta(msg_ctx*, int32_t, double*, double*, int64_t, int64_t*) { return no_device(); }
 int msg_set_profiling(msg_ctx*, int32_t) { return no_device(); }
 int msg_stage_times(msg_ctx*, float*, int32_t) { return no_device(); }
+int msg_gate(msg_ctx*, msg_ctx*, int32_t, int32_t) { return no_device(); }
 int msg_bench_fft(msg_ctx*, int32_t, int32_t, int32_t, float*) { return no_device(); }
 int msg_fft64(msg_ctx*, int32_t, int32_t, const double*, double*) { return no_device(); }
 int msg_fir(msg_ctx*, const float*, float*, int64_t, int32_t, const double*, int64_t, int32_t*, void*) {

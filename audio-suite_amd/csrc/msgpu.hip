@@ -234,6 +234,12 @@ struct msg_ctx {
     int device = 0;
     std::string err;
     bool profiling = false;
+    // msg_gate: this context's stream waits, before stage gate_wait, for the
+    // peer's gate event, and records its own after stage gate_rec begins
+    msg_ctx* gate_peer = nullptr;
+    int gate_wait = -1, gate_rec = -1;
+    hipEvent_t gate_ev = nullptr;
+    bool gate_armed = false;          // gate_ev recorded at least once
     // stage events: two sets alternate between batches; a set is read (folded
     // into the sums) when it comes round again, two batches later, or at
     // msg_stage_times -- profiling never makes the host wait for the last batch
@@ -590,6 +596,13 @@ static int g64_ops(const msg_preset& p, const msg_event& e) {
 
 static void stage_mark(msg_ctx* ctx, int i, hipStream_t s) {
     if (ctx->profiling) hipEventRecord(ctx->ev[ctx->ev_cur][i], s);
+    if (ctx->gate_peer) {
+        if (i == ctx->gate_wait && ctx->gate_peer->gate_armed) hipStreamWaitEvent(s, ctx->gate_peer->gate_ev, 0);
+        if (i == ctx->gate_rec) {
+            hipEventRecord(ctx->gate_ev, s);
+            ctx->gate_armed = true;
+        }
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -711,6 +724,7 @@ void msg_destroy(msg_ctx* ctx) {
     ctx->sf_hspec.release(); ctx->sf_xspec.release();
     for (auto& set : ctx->ev)
         for (auto& ev : set) hipEventDestroy(ev);
+    if (ctx->gate_ev) hipEventDestroy(ctx->gate_ev);
     ctx->staging.release();
     ctx->dp_presets.release(); ctx->frag_len.release(); ctx->info.release(); ctx->slot_base.release();
     ctx->tap_base.release(); ctx->dp_events.release(); ctx->dp_er_off.release(); ctx->dp_er_gain.release();
@@ -760,6 +774,19 @@ int msg_set_profiling(msg_ctx* ctx, int32_t on) {
         ctx->stage_cnt = 0;
         ctx->host_cnt = 0;
     }
+    return MSG_OK;
+}
+
+int msg_gate(msg_ctx* ctx, msg_ctx* peer, int32_t wait_stage, int32_t record_stage) {
+    if (!ctx || peer == ctx || wait_stage < -1 || wait_stage > 9 || record_stage < -1 || record_stage > 9)
+        return MSG_E_ARG;
+    if (peer && peer->device != ctx->device) return MSG_E_ARG;
+    if (peer && !ctx->gate_ev && hipEventCreateWithFlags(&ctx->gate_ev, hipEventDisableTiming) != hipSuccess)
+        return fail(ctx, MSG_E_DEVICE, "hipEventCreate failed");
+    ctx->gate_peer = peer;
+    ctx->gate_wait = peer ? wait_stage : -1;
+    ctx->gate_rec = peer ? record_stage : -1;
+    ctx->gate_armed = false;
     return MSG_OK;
 }
 

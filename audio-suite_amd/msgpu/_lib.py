@@ -100,6 +100,7 @@ _PROTOS = {
     "msg_last_meta": (C.c_int, [C.c_void_p, C.c_int32, C.POINTER(C.c_double), C.POINTER(C.c_double),
                                 C.c_int64, C.POINTER(C.c_int64)]),
     "msg_set_profiling": (C.c_int, [C.c_void_p, C.c_int32]),
+    "msg_gate": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.c_int32]),
     "msg_stage_times": (C.c_int, [C.c_void_p, C.POINTER(C.c_float), C.c_int32]),
     "msg_bench_fft": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32, C.c_int32, C.POINTER(C.c_float)]),
     "msg_fft64": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32, C.POINTER(C.c_double), C.POINTER(C.c_double)]),

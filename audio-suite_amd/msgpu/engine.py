@@ -49,6 +49,13 @@ class Engine:
     def set_profiling(self, on: bool):
         L.check(L.lib().msg_set_profiling(self._ctx, 1 if on else 0), self._ctx)
 
+    def gate(self, peer, wait_stage: int = 2, record_stage: int = 6):
+        """Order this context's batches against ``peer``'s (msg_gate): stage
+        ``wait_stage`` of each batch waits for the stage ``record_stage`` of the
+        peer's latest batch to begin.  ``peer=None`` clears the gate."""
+        L.check(L.lib().msg_gate(self._ctx, peer._ctx if peer is not None else None, int(wait_stage),
+                                 int(record_stage)), self._ctx)
+
     def stage_times(self):
         arr = (C.c_float * 13)()
         L.check(L.lib().msg_stage_times(self._ctx, arr, 13), self._ctx)

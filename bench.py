@@ -330,7 +330,7 @@ class GpuRunner:
     plans one sub-batch while the device runs another and their kernels share
     the CUs."""
 
-    def __init__(self, dev, streams):
+    def __init__(self, dev, streams, gate=None):
         import torch
         from msgpu.engine import Engine
         self.torch = torch
@@ -338,6 +338,9 @@ class GpuRunner:
         torch.cuda.set_device(dev)
         self.engs = [Engine(dev) for _ in range(streams)]
         self.streams = [torch.cuda.Stream(device=dev) for _ in range(streams)]
+        if gate and streams > 1:   # each context waits for the previous one's stage (msg_gate)
+            for i, e in enumerate(self.engs):
+                e.gate(self.engs[i - 1], gate[0], gate[1])
 
     def prepare(self, w: Workload):
         S = len(self.engs)
@@ -517,6 +520,9 @@ def parse():
     ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of CPU-baseline work")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--streams", type=int, default=2, help="in-flight sub-batches (contexts/streams) per GPU")
+    ap.add_argument("--gate", default="none",
+                    help="WAIT,RECORD stages of msg_gate between the streams' contexts (e.g. 2,6: a sub-batch's "
+                         "generator waits until the previous one's stereo pass begins), or none")
     ap.add_argument("--iso-steps", type=int, default=3, help="single-stream renders for roofline_isolated")
     ap.add_argument("--points", default="H48,C4,C5",
                     help="secondary configs timed after the headline (comma list, '' = none)")
@@ -592,7 +598,8 @@ def main():
         irs = load_irs()
         with open(os.path.join(REPO, "tests", "golden", "golden_info.json")) as f:
             golden = json.load(f)["summaries"]
-        runner = GpuRunner(local, max(1, args.streams))
+        gate = None if args.gate in ("", "none") else tuple(int(v) for v in args.gate.split(","))
+        runner = GpuRunner(local, max(1, args.streams), gate)
         head = measure(runner, cfg, seeds, default_sub(cfg, args, batch), args.steps, args.warmup, comm, irs,
                        golden, iso_steps=args.iso_steps)
         points = {}
@@ -618,7 +625,8 @@ def main():
                            "events_per_gpu_step": head["events_per_gpu_step"],
                            "design_samples_per_gpu_step": head["design_samples_per_gpu_step"],
                            "sub_batches_per_gpu": head["sub_batches"],
-                           "parallelism": f"preset-sharded x{world}", "streams_per_gpu": len(runner.engs)},
+                           "parallelism": f"preset-sharded x{world}", "streams_per_gpu": len(runner.engs),
+                           "stream_gate": args.gate},
                 "roofline": head["roofline"], "roofline_isolated": head.get("roofline_isolated"),
                 "stage_ms": head["stage_ms"], "stage_algorithmic_GBs": head["stage_algorithmic_GBs"],
                 "design_msamples_per_s": head["design_msamples_per_s"],

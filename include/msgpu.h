@@ -157,6 +157,16 @@ int msg_last_meta(msg_ctx* ctx, int32_t preset, double* micro, double* grain,
 int msg_set_profiling(msg_ctx* ctx, int32_t on);
 int msg_stage_times(msg_ctx* ctx, float* ms, int32_t n);
 
+/* Stream gate between two contexts of one device rendering alternate batches
+ * on their own streams: before stage `wait_stage` of each later batch the
+ * context's stream waits for the peer's most recent gate event, and it records
+ * its own gate event when stage `record_stage` begins (stage numbers as in
+ * msg_stage_times: 2 generate, 3 spectral, 4 overlap-add, 5 FIR, 6 stereo).
+ * With msg_gate(a, b, 2, 6) and msg_gate(b, a, 2, 6), one batch's generator
+ * (VALU-bound) runs beside the other's stereo pass (HBM-bound) instead of
+ * whichever kernels the two queues happen to interleave.  peer = NULL clears. */
+int msg_gate(msg_ctx* ctx, msg_ctx* peer, int32_t wait_stage, int32_t record_stage);
+
 /* Micro-benchmark of the LDS FFT engine: `blocks` workgroups each run `reps`
  * forward+inverse real transforms of length n; *ms receives the device time. */
 int msg_bench_fft(msg_ctx* ctx, int32_t n, int32_t reps, int32_t blocks, float* ms);
