@@ -98,6 +98,28 @@ def test_launcher_two_ranks_dry_run():
     assert d["value"] == pytest.approx(2 * 4 * 3 * 192000 / d["elapsed_max_s"] / 1e6)
 
 
+def test_torchrun_two_ranks_dry_run():
+    """The driver's N > 1 launch: ``python -m torch.distributed.run --nproc-per-node 2
+    ... bench.py --gpus 2``.  Each process is one rank (RANK / LOCAL_RANK from the
+    launcher, no second spawn), rank 0 prints the one line: two ranks on devices 0
+    and 1 with disjoint contiguous seeds and the slow rank's time."""
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(REPO, "bench.py"),
+           "--gpus", "2", "--steps", "3", "--warmup", "1", "--batch", "2", "--config", "C2", "--dry-run", "40"]
+    r = subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1, r.stdout                       # rank 0 only
+    d = lines[0]
+    assert d["dry_run"] is True and d["n_gpus"] == 2
+    ranks = sorted(d["ranks"], key=lambda q: q["rank"])
+    assert [q["device"] for q in ranks] == [0, 1]
+    assert len({q["pid"] for q in ranks}) == 2
+    assert [s for q in ranks for s in q["seeds"]] == list(range(1000, 1004))
+    assert d["elapsed_max_s"] == pytest.approx(max(q["elapsed_s"] for q in ranks), rel=0.05)
+
+
 def test_launcher_one_rank_dry_run():
     """--gpus 1 stays in-process (no child)."""
     d = _run_bench("--gpus", "1", "--steps", "2", "--warmup", "0", "--batch", "2", "--config", "C2",
