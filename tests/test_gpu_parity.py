@@ -313,6 +313,38 @@ def test_odd_length_stereo(msgpu, irs, frames):
         assert np.max(np.abs(a)) > 0.5                 # a real signal, normalised to the peak
 
 
+def test_gated_engines_equal_single(msgpu, irs):
+    """msg_gate between the two contexts (bench.py --gate 2,6: a batch's
+    generator waits for the other batch's stereo pass) reorders work only:
+    three rounds of gated renders equal single-engine renders exactly, and
+    clearing the gate restores ungated rendering."""
+    import torch
+    from msgpu.engine import Engine
+    from msgpu.pack import PackedBatch
+    params = [msgpu.config_params("C2", seed=s, irs=irs) for s in range(2000, 2006)]
+    halves = [PackedBatch(params[:3]), PackedBatch(params[3:])]
+    engs = [Engine(0), Engine(0)]
+    engs[0].gate(engs[1], 2, 6)
+    engs[1].gate(engs[0], 2, 6)
+    streams = [torch.cuda.Stream(device=0) for _ in range(2)]
+    outs = [e.alloc_output(p) for e, p in zip(engs, halves)]
+    for _ in range(3):
+        for e, p, o, st in zip(engs, halves, outs, streams):
+            e.render_packed(p, o, st)
+    torch.cuda.synchronize(0)
+    gated = [o.cpu().numpy() for o in outs]
+    single = Engine(0)
+    for h, p in enumerate(halves):
+        ref = single.render_packed(p)
+        torch.cuda.synchronize(0)
+        assert np.array_equal(gated[h], ref.cpu().numpy()), h
+    for e in engs:
+        e.gate(None)
+    engs[0].render_packed(halves[0], outs[0], streams[0])
+    torch.cuda.synchronize(0)
+    assert np.array_equal(outs[0].cpu().numpy(), gated[0])
+
+
 def test_two_engines_two_streams_concurrent(msgpu, irs, golden_info):
     """The bench's in-flight mode: two contexts rendering on two HIP streams at
     once (sub-batches enqueued back to back, one sync at the end) give exactly
