@@ -512,7 +512,8 @@ def isolated(runner, w, iso_steps, sb, cfg):
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=100,
+                    help="timed steps (100 C3 steps keep the GPU busy for ~1 s, long enough for an outside sampler)")
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="C3")
     ap.add_argument("--batch", type=int, default=0, help="presets per GPU (0: the config's default)")
