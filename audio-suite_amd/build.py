@@ -121,8 +121,14 @@ def build(force: bool = False, variant: str = "") -> str:
 
 
 def build_exp_tu(tus, out_name="libmsgpu_exp.so") -> str:
-    """Experiment library: `tus` compiled with MSGPU_EXP_DEFS, the rest from the product build."""
-    build()                                   # product objects up to date
+    """Experiment library: `tus` compiled with MSGPU_EXP_DEFS, the rest from the product build.
+
+    The product objects are used as they are (built only when one is missing):
+    rebuilding them here would compile an experiment's modified sources into the
+    product library too, and an A/B against it would compare a variant with
+    itself."""
+    if not all(os.path.exists(os.path.join(OBJ, tu.replace(".hip", ".o"))) for tu in TUS):
+        build()
     defs = os.environ.get("MSGPU_EXP_DEFS", "").split()
     objdir = os.path.join(HERE, "build_exp_tu")
     os.makedirs(objdir, exist_ok=True)
