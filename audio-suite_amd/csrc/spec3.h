@@ -60,7 +60,11 @@ struct Spec3Plan {
     static MSG_HD constexpr int phB(int x) { return x + (x / NB3) * PADB; }
 };
 
-using Spec3P18750 = Spec3Plan<18750, 768, 25, 30, 25, 11>;
+// MSG_S3_PLAN (tuning builds): radices R1, R2, R3 and the exchange-B pad
+#ifndef MSG_S3_PLAN
+#define MSG_S3_PLAN 25, 30, 25, 11
+#endif
+using Spec3P18750 = Spec3Plan<18750, 768, MSG_S3_PLAN>;
 
 template <class P> MSG_DEV float2 s3_wM(const float2* tab, int x) {    // exp(-2 pi i x / M)
     return cmul(tab[P::OFF_MHI + (x >> 7)], tab[P::OFF_MLO + (x & 127)]);
