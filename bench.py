@@ -521,9 +521,11 @@ def parse():
     ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of CPU-baseline work")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--streams", type=int, default=2, help="in-flight sub-batches (contexts/streams) per GPU")
-    ap.add_argument("--gate", default="none",
-                    help="WAIT,RECORD stages of msg_gate between the streams' contexts (e.g. 2,6: a sub-batch's "
-                         "generator waits until the previous one's stereo pass begins), or none")
+    ap.add_argument("--gate", default="2,4",
+                    help="WAIT,RECORD stages of msg_gate between the streams' contexts, or none.  Default 2,4: a "
+                         "sub-batch's generator waits until the previous sub-batch's overlap-add begins, so it "
+                         "runs beside that sub-batch's FIR and stereo passes rather than its spectral kernel "
+                         "(C3: 9.43-9.45 vs 9.52-9.54 ms per step ungated, profiles/r02ze_gate.txt)")
     ap.add_argument("--iso-steps", type=int, default=3, help="single-stream renders for roofline_isolated")
     ap.add_argument("--points", default="H48,C4,C5",
                     help="secondary configs timed after the headline (comma list, '' = none)")
