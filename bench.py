@@ -42,7 +42,8 @@ import numpy as np  # noqa: E402
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: 8.0 TB/s spec
 # Per-launch HBM bytes of each kernel from rocprofv3 PMC passes (FETCH_SIZE x2
 # per the gfx950 correction + WRITE_SIZE), written by tools/pmc_traffic.py:
-# profiles/traffic_<config>.json, or profiles/traffic.json (C3, round 1).
+# profiles/traffic_<config>.json, else the newest profiles/r*_traffic_<config>.json
+# of the same launch size, else profiles/traffic.json (C3, round 1).
 PROFILES = os.path.join(REPO, "profiles")
 # bench stage -> the kernels it times (rocprofv3 kernel-name prefixes)
 STAGE_KERNEL = {"generate": ("k_gen_normal",), "spectral": ("k_spec3", "k_spectral"), "overlap_add": ("k_ola_env",),
@@ -99,7 +100,9 @@ def measured_traffic(prefixes, cfg, batch):
     """HBM bytes per launch of the stage's kernels (name prefixes) from the
     committed PMC summary of this workload, or None when there is none (bench
     cannot read PMC itself)."""
-    for path in (os.path.join(PROFILES, f"traffic_{cfg}.json"), os.path.join(PROFILES, "traffic.json")):
+    import glob
+    newest = sorted(glob.glob(os.path.join(PROFILES, f"r*_traffic_{cfg}.json")), reverse=True)
+    for path in (os.path.join(PROFILES, f"traffic_{cfg}.json"), *newest, os.path.join(PROFILES, "traffic.json")):
         try:
             with open(path) as f:
                 t = json.load(f)
@@ -530,7 +533,9 @@ def parse():
     ap.add_argument("--sub", type=int, default=0, help="presets per in-flight sub-batch (0: config default)")
     ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of CPU-baseline work")
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--streams", type=int, default=2, help="in-flight sub-batches (contexts/streams) per GPU")
+    ap.add_argument("--streams", type=int, default=3,
+                    help="in-flight sub-batches (contexts/streams) per GPU (C3 with the 2,4 gate: 3 streams "
+                         "9.35-9.38 ms vs 2 streams 9.45 ms per step, profiles/r02zh_streams.txt)")
     ap.add_argument("--gate", default="2,4",
                     help="WAIT,RECORD stages of msg_gate between the streams' contexts, or none.  Default 2,4: a "
                          "sub-batch's generator waits until the previous sub-batch's overlap-add begins, so it "
