@@ -57,9 +57,10 @@ BOX_CORES = 16
 # Per-GPU batch of each config (BASELINE.json configs: C2 batch 1; C3 1024 on one
 # GPU; C4 4096 and C5 8192 across 8 GPUs = 512 and 1024 per GPU) and the presets
 # per in-flight sub-batch.  A C5 preset (8.4 M frames, 4000 events) needs ~0.2 GB
-# of working buffers besides its 67 MB output, so C5 renders in sub-batches of 128.
+# of working buffers besides its 67 MB output, so C5 renders in sub-batches of 171
+# (~35 GB of working buffers per context, three contexts, all outputs resident).
 CONFIG_BATCH = {"C1": 1, "C2": 1, "C3": 1024, "C4": 512, "C5": 1024, "H48": 1024}
-CONFIG_SUB = {"C5": 128}
+CONFIG_SUB = {"C5": 171}   # six sub-batches, two per stream (C5 ungated: 126.8 ms vs 130.6-132.2 at 128)
 GATE_OFF = {"C5"}   # configs whose points run ungated (measured slower with --gate 2,4)
 WORKLOAD = {
     "C1": "C1: 48 kHz out, no band limit, unfold x1, stretch x1, Single event, 1 s, ER 320 taps, stereo",
