@@ -37,7 +37,11 @@ template <int M> struct Fir4Geo {
     static constexpr int BP1 = NB1 / T, BP2 = NB2 / T, BP3 = NB3 / T;
     static_assert(NB1 % T == 0 && NB2 % T == 0 && NB3 % T == 0 && NB4 == 2 * T, "FIR4 plan");
     // exchange pads: forward E1..E3, inverse E1'..E3'
-    static constexpr int S1 = 16, S2 = 0, S3 = 0, S1I = 8, S2I = 8, S3I = 0;
+#ifndef MSG_FIR4_PADS   // tuning builds: exchange pads S2, S3, S2I, S3I (S1 = R1, S1I = R4 fixed)
+#define MSG_FIR4_PADS 0, 0, 8, 0
+#endif
+    static constexpr int PADS_[4] = {MSG_FIR4_PADS};
+    static constexpr int S1 = 16, S2 = PADS_[0], S3 = PADS_[1], S1I = 8, S2I = PADS_[2], S3I = PADS_[3];
     static_assert(S1 == R1 && S1I == R4, "pass-1 writes of R consecutive elements: pad S = R");
     // twiddle tables at LDS offset 0 (float2 entries): exact [r][k] tables for the
     // two passes with small NS, two-level w_M and w_2M tables for the rest
