@@ -492,101 +492,12 @@ k_fir4s(const PresetRt* __restrict__ rt, const int2* __restrict__ jobs, const fl
 }
 
 // ---------------------------------------------------------------------------
-// FIR partition spectra of the ER + IR presets on the k_fir4 engine (N = 2M =
-// 32768), the C3/C4 path (MS:409-445: h = (delta + ER taps) * IR).  The
-// general-size kernels of kernels_fir.h (k_fir_hconv, k_fir_h) run these four
-// transforms per preset on the 512-thread runtime-plan engine at ~3x k_fir4's
-// time per transform.
-//   k_fir4_hconv  one workgroup per preset: e = delta + ER taps built in LDS,
-//                 h = irfft(rfft(e) . S_IR) (S_IR: k_ir_spec, natural bins) to
-//                 the float scratch hs (N samples; the linear convolution fits:
-//                 ER span + IR <= N, checked on the host)
-//   k_fir4_hpart  one workgroup per (preset, q): H_q = rfft(h[qP, qP + P)),
-//                 written in natural bin order (k_fir4 / k_fir2's hspec layout)
+// FIR partition spectra on the k_fir4 engine (N = 2M = 32768), the C3/C4 path:
+// one workgroup per (preset, q), H_q = rfft(h[qP, qP + P)) zero-padded to N,
+// from k_h_build's time-domain h (kernels_fir.h), written in natural bin order
+// (k_fir4 / k_fir2's hspec layout).  The general-size k_fir_h runs the same
+// transform on the 512-thread runtime-plan engine at ~3x k_fir4's time.
 // ---------------------------------------------------------------------------
-
-// Inverse transform of the spectrum pairs in acc (k_fir4's layout) up to pass
-// 4': u[r] = z'[t + r NB1] (z'[m] = x[2m] - i x[2m+1], times M).  The same
-// steps as k_fir4's inverse, which keeps its own inline copy (its register
-// allocation was tuned with it).
-template <int M>
-MSG_DEV void fir4_inverse(float2* buf, const float2* tab, float2 (&acc)[2][Fir4Geo<M>::R4],
-                          float2 (&u)[Fir4Geo<M>::R1]) {
-    using G = Fir4Geo<M>;
-    constexpr int R1 = G::R1, R4 = G::R4, NB1 = G::NB1, NB4 = G::NB4;
-    const int t = otid();
-    if (t != 0) {
-        const float2 wA = fir_wM(tab, G::OFF_PLO, G::OFF_PHI, t);
-#pragma unroll
-        for (int r = 0; r < R4; ++r) fir_pair_pre(acc[0][r], acc[1][R4 - 1 - r], cmul_k(wA, fir_cr<R4>(r)));
-    } else {
-#pragma unroll
-        for (int r = 0; r < R4 - 1; ++r) fir_pair_pre(acc[0][r], acc[1][R4 - 1 - r], fir_w0<M, R4>(r));
-        const float y0 = acc[0][R4 - 1].x, yN = acc[0][R4 - 1].y;
-        acc[0][R4 - 1] = make_float2(0.5f * (y0 + yN), -0.5f * (y0 - yN));   // bin M/2: conj Z' = Y
-        fir_unslots<R4>(acc, true);
-    }
-    const int js[2] = {t, t == 0 ? NB4 / 2 : NB4 - t};
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-        Dft<R4, false>::run(acc[h]);
-        const int base = pads<G::S1I>(js[h] * R4);
-#pragma unroll
-        for (int r = 0; r < R4; ++r) buf[base + r] = acc[h][r];
-    }
-    __syncthreads();
-    fir4_pass_lds<M, G::R3, R4, G::BP3, G::S1I, G::S2I, true, G::OFF_TB>(buf, tab, t);
-    __syncthreads();
-    fir4_pass_lds<M, G::R2, R4 * G::R3, G::BP2, G::S2I, G::S3I, false, 0>(buf, tab, t);
-    __syncthreads();
-#pragma unroll
-    for (int r = 0; r < R1; ++r) u[r] = buf[pads<G::S3I>(t + r * NB1)];
-    twiddle_pow_ab<R1, tw_base<R1>()>(u, fir_wM(tab, G::OFF_MLO, G::OFF_MHI, t),
-                                      fir_wM(tab, G::OFF_MLO, G::OFF_MHI, (t * tw_base<R1>()) & (M - 1)));
-    Dft<R1, false>::run(u);
-}
-
-template <int M>
-__global__ void __launch_bounds__(Fir4Geo<M>::T)
-k_fir4_hconv(const PresetRt* __restrict__ rt, const int32_t* __restrict__ conv_list,
-             const float2* __restrict__ tables, const int32_t* __restrict__ er_off,
-             const double* __restrict__ er_gain, const float2* __restrict__ ir_spec, float* __restrict__ hs) {
-    using G = Fir4Geo<M>;
-    constexpr int T = G::T, R1 = G::R1, R4 = G::R4, NB1 = G::NB1;
-    extern __shared__ __attribute__((aligned(16))) float2 lds[];
-    float2* tab = lds;
-    float2* buf = lds + G::TAB;
-    const PresetRt& r = rt[conv_list[blockIdx.x]];
-    for (int i = threadIdx.x; i < G::TAB_USED; i += T) tab[i] = tables[i];
-    // e = delta + ER taps (MS:409-420), as floats in natural order: buf[m] = (e[2m], e[2m+1])
-    for (int m = threadIdx.x; m < M; m += T) buf[m] = make_float2(m == 0 ? 1.f : 0.f, 0.f);
-    __syncthreads();
-    float* e = reinterpret_cast<float*>(buf);
-    for (int k = threadIdx.x; k < r.n_taps; k += T) {
-        const int64_t o = er_off[r.er_base + k];
-        if (o <= 0 || o >= r.out_n || o >= 2 * M) continue;   // MS:418-420
-        atomicAdd(e + o, (float)er_gain[r.er_base + k]);      // colliding taps are merged on the host
-    }
-    __syncthreads();
-    float2 v[2][R4], acc[2][R4];
-    fir4s_forward<M, true>(buf, tab, nullptr, 0, 0, v);
-#pragma unroll
-    for (int h = 0; h < 2; ++h)
-#pragma unroll
-        for (int q = 0; q < R4; ++q) acc[h][q] = make_float2(0.f, 0.f);
-    fir4s_mac<M>(acc, v, ir_spec + r.irs_off);                // E . S_IR
-    float2 u[R1];
-    fir4_inverse<M>(buf, tab, acc, u);
-    float* h = hs + r.hs_off;
-    const float s = 1.0f / (float)M;
-    const int t = otid();
-#pragma unroll
-    for (int q = 0; q < R1; ++q) {
-        const int w = 2 * (t + q * NB1);
-        *reinterpret_cast<float2*>(h + w) = make_float2(u[q].x * s, -u[q].y * s);
-    }
-}
-
 template <int M>
 __global__ void __launch_bounds__(Fir4Geo<M>::T)
 k_fir4_hpart(const PresetRt* __restrict__ rt, const int2* __restrict__ jobs, const float2* __restrict__ tables,
@@ -601,7 +512,7 @@ k_fir4_hpart(const PresetRt* __restrict__ rt, const int2* __restrict__ jobs, con
     const int q = job.y, P = r.fir_P;
     for (int i = threadIdx.x; i < G::TAB_USED; i += T) tab[i] = tables[i];   // visible after the first exchange
     const int64_t s0 = (int64_t)q * P;
-    const int64_t len = P < 2 * M - s0 ? P : 2 * M - s0;                   // h[qP, qP + P), zero-padded to N
+    const int64_t len = P < r.h_len - s0 ? P : r.h_len - s0;               // h[qP, qP + P), zero-padded to N
     float2 v[2][R4];
     fir4s_forward<M>(buf, tab, hs + r.hs_off + s0, len, 0, v);
     float2* H = hspec + r.h_off + (int64_t)q * (M + 1);

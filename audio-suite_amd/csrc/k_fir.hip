@@ -13,19 +13,17 @@ template <int M> static void fir2_attr() {
                               FirGeo<M>::LDS_BYTES);
 }
 
+static_assert(H_TILE == H_BUILD_TILE, "k_h_build tile");
+
 void fir_init_attrs() {
     (void)hipFuncSetAttribute((const void*)k_fir4<16384>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               Fir4Geo<16384>::LDS_BYTES);
     (void)hipFuncSetAttribute((const void*)k_fir4s<16384>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               Fir4Geo<16384>::LDS_BYTES);
-    (void)hipFuncSetAttribute((const void*)k_fir4_hconv<16384>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              Fir4Geo<16384>::LDS_BYTES);
     (void)hipFuncSetAttribute((const void*)k_fir4_hpart<16384>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               Fir4Geo<16384>::LDS_BYTES);
     fir2_attr<1024>(); fir2_attr<2048>(); fir2_attr<4096>(); fir2_attr<8192>(); fir2_attr<16384>();
     (void)hipFuncSetAttribute((const void*)k_fir_h<FIR_T, FIR_M>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
-    (void)hipFuncSetAttribute((const void*)k_fir_hconv<FIR_T, FIR_M>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              LDS_MAX);
     (void)hipFuncSetAttribute((const void*)k_ir_spec<FIR_T, FIR_M>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               LDS_MAX);
 }
@@ -37,20 +35,17 @@ hipError_t launch_ir_spec(unsigned grid, int lds_bytes, hipStream_t s, const int
     return hipGetLastError();
 }
 
-hipError_t launch_fir_hconv(unsigned grid, int lds_bytes, hipStream_t s, const PresetRt* rt, const int32_t* conv_list,
-                            const RealPlan* fir_plans, const int32_t* fir_plan_of, const int32_t* er_off,
-                            const double* er_gain, const float2* ir_spec, float* hs) {
-    hipLaunchKernelGGL((k_fir_hconv<FIR_T, FIR_M>), dim3(grid), dim3(FIR_T), lds_bytes, s, rt, conv_list, fir_plans,
-                       fir_plan_of, er_off, er_gain, ir_spec, hs);
+hipError_t launch_h_build(unsigned grid, hipStream_t s, const PresetRt* rt, const int32_t* tile_begin, int n_presets,
+                          const int32_t* er_off, const double* er_gain, const double* ir_bank, float* hs) {
+    hipLaunchKernelGGL(k_h_build, dim3(grid), dim3(H_T), 0, s, rt, tile_begin, n_presets, er_off, er_gain, ir_bank, hs);
     return hipGetLastError();
 }
 
 hipError_t launch_fir_h(unsigned grid, int lds_bytes, hipStream_t s, const PresetRt* rt, const int32_t* hblk_begin,
-                        int n_presets, const RealPlan* fir_plans, const int32_t* fir_plan_of,
-                        const int32_t* er_off, const double* er_gain, const double* ir_bank,
-                        const float* hs, float2* hspec) {
+                        int n_presets, const RealPlan* fir_plans, const int32_t* fir_plan_of, const float* hs,
+                        float2* hspec) {
     hipLaunchKernelGGL((k_fir_h<FIR_T, FIR_M>), dim3(grid), dim3(FIR_T), lds_bytes, s, rt, hblk_begin, n_presets,
-                       fir_plans, fir_plan_of, er_off, er_gain, ir_bank, hs, hspec);
+                       fir_plans, fir_plan_of, hs, hspec);
     return hipGetLastError();
 }
 
@@ -108,16 +103,11 @@ hipError_t launch_fir4s(int M, unsigned grid, hipStream_t s, const PresetRt* rt,
     return hipGetLastError();
 }
 
-hipError_t launch_fir4_h(int M, unsigned n_conv, unsigned n_parts, hipStream_t s, const PresetRt* rt,
-                         const int32_t* conv_list, const int2* part_jobs, const float2* tables, const int32_t* er_off,
-                         const double* er_gain, const float2* ir_spec, float* hs, float2* hspec) {
+hipError_t launch_fir4_hpart(int M, unsigned n_parts, hipStream_t s, const PresetRt* rt, const int2* part_jobs,
+                             const float2* tables, const float* hs, float2* hspec) {
     if (M != 16384) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((k_fir4_hconv<16384>), dim3(n_conv), dim3(Fir4Geo<16384>::T), Fir4Geo<16384>::LDS_BYTES, s, rt,
-                       conv_list, tables, er_off, er_gain, ir_spec, hs);
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return e;
     hipLaunchKernelGGL((k_fir4_hpart<16384>), dim3(n_parts), dim3(Fir4Geo<16384>::T), Fir4Geo<16384>::LDS_BYTES, s,
-                       rt, part_jobs, tables, (const float*)hs, hspec);
+                       rt, part_jobs, tables, hs, hspec);
     return hipGetLastError();
 }
 

@@ -10,7 +10,11 @@
 // strided data, M2 <= 4096 row transforms of contiguous data) with the chirp
 // convolution's pointwise product fused between the forward and inverse row
 // transforms, and no transposes (the kernel spectrum is kept in the same
-// permuted order).  float32 data, float64-built twiddles and chirps.
+// permuted order).  Above M = 2^23 (odd outputs longer than 4 194 304 frames,
+// e.g. 95 s at 44.1 kHz) one more column level splits M = M0 x L, L = M1 x M2:
+// column transforms of length M0 over stride L with the W_M twiddle, then the
+// four-step FFT_L inside each of the M0 contiguous chunks (k_so_cols with a
+// chunk index in blockIdx.y).  float32 data, float64-built twiddles and chirps.
 #pragma once
 #include "rt.h"
 
@@ -104,12 +108,15 @@ MSG_DEV void so_stage_tw(float2* tw, int N) {
 // Column step over A (M1 rows x M2 columns, row-major), C columns per block.
 // forward: FFT_M1 down each column, then x W_M^(j2 k1);  inverse: x conj(W_M^(j2 k1)),
 // then inverse FFT_M1.
+// blockIdx.y: chunk of A (stride `chunk` elements) for the inner level of a
+// three-level transform.
 template <bool INV>
 __global__ void __launch_bounds__(SO_T)
-k_so_cols(float2* __restrict__ A, int M1, int M2, int C) {
+k_so_cols(float2* __restrict__ A, int M1, int M2, int C, int64_t chunk) {
     extern __shared__ __attribute__((aligned(16))) float2 so_lds[];
     float2* tw = so_lds;                   // M1 entries
     float2* s = so_lds + M1;               // C x M1
+    A += (int64_t)blockIdx.y * chunk;
     so_stage_tw(tw, M1);
     const int j20 = blockIdx.x * C;
     const int64_t M = (int64_t)M1 * M2;

@@ -41,13 +41,14 @@ hipError_t launch_spec3(unsigned grid, hipStream_t s, const msg_event* events, c
 void fir_init_attrs();
 hipError_t launch_ir_spec(unsigned grid, int lds_bytes, hipStream_t s, const int64_t* jobs, int n_jobs,
                           const RealPlan* fir_plans, const double* ir_bank, float2* ir_spec);
-hipError_t launch_fir_hconv(unsigned grid, int lds_bytes, hipStream_t s, const PresetRt* rt, const int32_t* conv_list,
-                            const RealPlan* fir_plans, const int32_t* fir_plan_of, const int32_t* er_off,
-                            const double* er_gain, const float2* ir_spec, float* hs);
+// h = (delta + ER) * IR in the time domain, one workgroup per H_TILE taps of a preset
+// (tile_begin: first tile per preset, non-decreasing)
+hipError_t launch_h_build(unsigned grid, hipStream_t s, const PresetRt* rt, const int32_t* tile_begin, int n_presets,
+                          const int32_t* er_off, const double* er_gain, const double* ir_bank, float* hs);
+constexpr int H_BUILD_TILE = 1024;   // kernels_fir.h H_TILE
 hipError_t launch_fir_h(unsigned grid, int lds_bytes, hipStream_t s, const PresetRt* rt, const int32_t* hblk_begin,
-                        int n_presets, const RealPlan* fir_plans, const int32_t* fir_plan_of,
-                        const int32_t* er_off, const double* er_gain, const double* ir_bank,
-                        const float* hs, float2* hspec);
+                        int n_presets, const RealPlan* fir_plans, const int32_t* fir_plan_of, const float* hs,
+                        float2* hspec);
 // register-resident FIR with compile-time transform size M = N/2 in {1024..16384}
 bool fir2_tables_host(int M, std::vector<float>& out);
 // frequency-domain delay line (msg_fir with many partitions): segment spectra, then MAC + inverse
@@ -61,11 +62,9 @@ hipError_t launch_fir4(int M, unsigned grid, hipStream_t s, const PresetRt* rt, 
                        const float2* tables, const float2* hspec, const float* x_in, float* y_out);
 // streaming variant (B = P = 16384, Q <= 2): jobs (preset, first block), kblk blocks per workgroup
 constexpr int FIR4S_P = 16384;
-// ER + IR partition spectra on the k_fir4 engine (fir4_fft.h): k_fir4_hconv over
-// conv_list, then k_fir4_hpart over the (preset, q) jobs.
-hipError_t launch_fir4_h(int M, unsigned n_conv, unsigned n_parts, hipStream_t s, const PresetRt* rt,
-                         const int32_t* conv_list, const int2* part_jobs, const float2* tables, const int32_t* er_off,
-                         const double* er_gain, const float2* ir_spec, float* hs, float2* hspec);
+// partition spectra on the k_fir4 engine (fir4_fft.h): k_fir4_hpart over the (preset, q) jobs
+hipError_t launch_fir4_hpart(int M, unsigned n_parts, hipStream_t s, const PresetRt* rt, const int2* part_jobs,
+                             const float2* tables, const float* hs, float2* hspec);
 hipError_t launch_fir4s(int M, unsigned grid, hipStream_t s, const PresetRt* rt, const int2* jobs,
                         const float2* tables, const float2* hspec, const float* x_in, float* y_out, int kblk);
 
@@ -106,10 +105,11 @@ hipError_t launch_fft64_one(int lds_bytes, hipStream_t s, const Real64Plan* plan
 
 // odd-length stereo rotation (kernels_stereo_odd.h): Bluestein through M = pow2 >= 2n-1
 void stereo_odd_init_attrs();
-int64_t stereo_odd_len(int64_t n);                  // M, or -1 when n is too long
-hipError_t launch_stereo_odd_kernel(int64_t n, float2* Bp, float2* A, hipStream_t s);
-hipError_t launch_stereo_odd(int64_t n, int dr, double width, const float* y, const float2* Bp, float2* A,
-                             float* r2, hipStream_t s);
+// row_max / col_max: transform-split limits (0: the defaults 4096 / 2048)
+int64_t stereo_odd_len(int64_t n, int row_max, int col_max);   // M, or -1 when n is too long
+hipError_t launch_stereo_odd_kernel(int64_t n, int row_max, int col_max, float2* Bp, float2* A, hipStream_t s);
+hipError_t launch_stereo_odd(int64_t n, int row_max, int col_max, int dr, double width, const float* y,
+                             const float2* Bp, float2* A, float* r2, hipStream_t s);
 // the app's spectrogram (stft_mag_db, MS:197-212) on the float64 engine
 hipError_t launch_stft64(unsigned frames, int lds_bytes, hipStream_t s, const Real64Plan* plans, int plan,
                          const void* x, int elem_bytes, int64_t n, int channels, int win, int hop, double* S);

@@ -291,13 +291,12 @@ struct msg_ctx {
     Slice<PresetRt> prt;
     Slice<int32_t> gen_list, spec_small, spec_big, tile_begin, fir_begin, h_begin, st_begin, fir_plan_of;
     DevBuf<float> micro, grain, mono_a, mono_y;
-    DevBuf<float2> hspec, irspec;
-    DevBuf<float> hscratch;                     // h of ER + IR presets (k_fir_hconv -> k_fir_h)
-    Slice<int32_t> conv_list, conv4_list;
+    DevBuf<float2> hspec;
+    DevBuf<float> hscratch;                     // h of every FIR preset (k_h_build -> k_fir_h / k_fir4_hpart)
+    Slice<int32_t> h_tile_begin;
     Slice<int2> hpart_jobs;
     Slice<int2> fir_jobs;
     Slice<int32_t> spec_ct_list;
-    Slice<int64_t> irjobs;
     Slice<double> irbank;
     DevBuf<unsigned> maxbits;
     // float64 grain chain (kernels_grain64.h)
@@ -319,6 +318,7 @@ struct msg_ctx {
     DevBuf<float2> sf_hspec, sf_xspec;
     // odd-length stereo rotation (kernels_stereo_odd.h)
     std::map<int64_t, DevBuf<float2>> so_bp;   // chirp kernel spectra by n
+    int so_row = 0, so_col = 0;                // transform-split limits (MSGPU_SO_ROW / _COL, tests; 0 = default)
     DevBuf<float2> so_A;
     DevBuf<float> so_r2;
     // host mirrors of the last batch
@@ -503,19 +503,17 @@ static double bessel_j(int m, double x) {
     return sum;
 }
 
-// Choose (N, P, Q) minimising FFT work for an M-tap FIR over n outputs.
-// need: with early reflections the whole kernel h is built in one transform
-// (k_fir_h), so only N >= need qualify (M - 1 with an IR, M without).
+// Choose (N, P, Q) minimising FFT work for an M-tap FIR over n outputs (h is
+// built in the time domain by k_h_build, so any N with P < N qualifies).
 // stream: when non-null, also consider k_fir4s (N = 32768, P = B = 16384, Q <= 2:
 // one forward and one inverse transform per block plus, for Q = 2, one forward
 // per workgroup of kblk blocks) and report whether it won.
-static void choose_fir(int64_t M, int64_t n, int64_t need, int& N, int& P, int& Q, bool* stream = nullptr,
+static void choose_fir(int64_t M, int64_t n, int& N, int& P, int& Q, bool* stream = nullptr,
                        int kblk = 1) {
     double best = 1e300;
     N = FIR_NMAX; P = (int)std::min<int64_t>(M, FIR_NMAX / 2); Q = (int)((M + P - 1) / P);
     for (int lg = 11; lg <= 15; ++lg) {   // k_fir2 sizes: M = N/2 in 1024..16384
         const int NN = 1 << lg;
-        if (NN < need) continue;
         for (int q = 1; q <= 64; ++q) {
             const int64_t pp = (M + q - 1) / q;
             if (pp >= NN) continue;
@@ -529,7 +527,7 @@ static void choose_fir(int64_t M, int64_t n, int64_t need, int& N, int& P, int& 
         *stream = false;
         const int NN = 2 * FIR4S_P, lg = 15;
         const int64_t q = (M + FIR4S_P - 1) / FIR4S_P;
-        if (NN >= need && q <= 2) {
+        if (q <= 2) {
             const int64_t blocks = (n + FIR4S_P - 1) / FIR4S_P;
             const double cost = (double)blocks * (2.0 + (q - 1) / (double)kblk) * NN * lg + (double)blocks * NN * 4.0;
             if (cost < best) { best = cost; N = NN; P = FIR4S_P; Q = (int)q; *stream = true; }
@@ -696,6 +694,8 @@ msg_ctx* msg_create(int device_ordinal) {
     for (auto& set : ctx->ev)
         for (auto& ev : set) hipEventCreate(&ev);
     if (const char* e = getenv("MSGPU_DEVICE_PLAN")) ctx->device_plan = e[0] == '1';
+    if (const char* e = getenv("MSGPU_SO_ROW")) ctx->so_row = atoi(e);
+    if (const char* e = getenv("MSGPU_SO_COL")) ctx->so_col = atoi(e);
     spectral_ct_init_attrs();
     spec3_init_attrs();
     spectral_init_attrs();
@@ -729,7 +729,7 @@ void msg_destroy(msg_ctx* ctx) {
     ctx->dp_presets.release(); ctx->frag_len.release(); ctx->info.release(); ctx->slot_base.release();
     ctx->tap_base.release(); ctx->dp_events.release(); ctx->dp_er_off.release(); ctx->dp_er_gain.release();
     ctx->micro.release(); ctx->grain.release();
-    ctx->mono_a.release(); ctx->mono_y.release(); ctx->hspec.release(); ctx->irspec.release();
+    ctx->mono_a.release(); ctx->mono_y.release(); ctx->hspec.release();
     ctx->hscratch.release(); ctx->maxbits.release();
     for (void* p : ctx->plans64.allocs) hipFree(p);
     ctx->plans64.dev.release();
@@ -887,7 +887,7 @@ int msg_fir(msg_ctx* ctx, const float* x_dev, float* y_dev, int64_t n, int32_t n
     HIPCHK(ctx, hipSetDevice(ctx->device));
     hipStream_t s = (hipStream_t)stream;
     int N = 0, Pp = 0, Q = 0;
-    choose_fir(M, n, 0, N, Pp, Q);
+    choose_fir(M, n, N, Pp, Q);
     // Many partitions: a frequency-domain delay line (fir_fft.h) computes each
     // input segment's spectrum once and reuses it for Q blocks -- two transforms
     // per block of N/2 outputs instead of Q + 1 per block of N - P + 1, for
@@ -1106,10 +1106,12 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
         HIPCHK(ctx, hipStreamSynchronize(s));
     }
     // Early-reflection taps whose rounded delays coincide are merged here, in tap
-    // order and in float64 (the order MS:416-420 adds them), so the FIR kernels
-    // scatter at most one tap per offset: LDS float atomics on a shared offset
-    // sum in arbitrary order, and a last-ulp change of h re-rounds the whole
-    // float32 convolution (renders of one batch differed by up to 1.2e-5).
+    // order and in float64 (the order MS:416-420 adds them), and the taps that
+    // act on the output (0 < offset < out_n, MS:418-420) are compacted to the
+    // front of the preset's tap range sorted by offset: k_h_build walks only the
+    // taps whose shifted IR overlaps its tile.  n_taps_live[p]: their count,
+    // tap_max[p]: the largest offset (0 without taps).
+    std::vector<int32_t> n_taps_live(P, 0), tap_max(P, 0);
     {
         auto merge = [&](int p) {
             if (!(presets[p].flags & MSG_F_ER_CLOUD)) return;
@@ -1119,16 +1121,23 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
             std::vector<int> ix(nt);
             for (int k = 0; k < nt; ++k) ix[k] = k;
             std::stable_sort(ix.begin(), ix.end(), [&](int a, int b) { return off[a] < off[b]; });
+            std::vector<int32_t> o2;
+            std::vector<double> g2;
+            o2.reserve(nt);
+            g2.reserve(nt);
+            const int64_t n = info[p].out_n;
             for (int i = 0; i < nt;) {
                 int j = i + 1;
                 while (j < nt && off[ix[j]] == off[ix[i]]) ++j;
-                if (j - i > 1 && off[ix[i]] > 0) {
-                    double acc = g[ix[i]];
-                    for (int u = i + 1; u < j; ++u) { acc += g[ix[u]]; off[ix[u]] = -1; }
-                    g[ix[i]] = acc;
-                }
+                double acc = g[ix[i]];
+                for (int u = i + 1; u < j; ++u) acc += g[ix[u]];
+                if (off[ix[i]] > 0 && off[ix[i]] < n) { o2.push_back(off[ix[i]]); g2.push_back(acc); }
                 i = j;
             }
+            std::copy(o2.begin(), o2.end(), off);
+            std::copy(g2.begin(), g2.end(), g);
+            n_taps_live[p] = (int32_t)o2.size();
+            tap_max[p] = o2.empty() ? 0 : o2.back();
         };
         if (ctx->device_plan) for (int p = 0; p < P; ++p) merge(p);
         else HostPool::get().run(P, merge);
@@ -1158,10 +1167,11 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
         ir_off[i] = (int64_t)irbank.size();
         irbank.insert(irbank.end(), irs[i], irs[i] + ir_lens[i]);
     }
-    int64_t pool = 0, ysum = 0, hsum = 0, irs_sum = 0;
+    int64_t pool = 0, ysum = 0, hsum = 0;
     int32_t tiles = 0, fblocks = 0, hblocks = 0, stiles = 0;
-    std::vector<int32_t> conv_list, conv4_list;   // ER + IR presets: runtime-plan engine / k_fir4 engine
-    std::vector<int2> hpart_jobs;                  // (preset, q) of the conv4_list presets
+    std::vector<int2> hpart_jobs;                  // (preset, q) of the presets on the k_fir4 engine
+    std::vector<int32_t> h_tile_begin(P, 0);       // k_h_build tiles per preset (prefix)
+    int32_t htiles = 0;
     int32_t hblocks_gen = 0;                       // k_fir_h blocks of presets not on the k_fir4 engine
     int64_t hs_sum = 0;
     int spec_small_lds = 0, spec_big_lds = 0, fir_lds = 0;
@@ -1176,10 +1186,8 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
     const bool stop_cep = stop_env && std::strcmp(stop_env, "cep") == 0;
     std::vector<int32_t> spec3;                           // events of the band-pruned kernel
     std::vector<int32_t> f32_presets;                     // presets on the float32 chain
-    std::map<std::pair<int, int>, int64_t> ir_spec_of;   // (IR index, N) -> offset
     std::vector<int2> fjobs_by[6];                        // FIR output blocks per transform size; [5]: k_fir4s
     std::vector<int2> fir4s_presets;                      // (preset, blocks) on the streaming FIR
-    std::vector<int64_t> ir_jobs;                         // [ir_off, ir_len, plan, out_off] per job
     // float64 grain chain records
     std::vector<Ev64> ev64;
     std::vector<int32_t> gen64_list;                      // normal-driven float64 events (event slots)
@@ -1199,19 +1207,19 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
     int64_t g64_big_cap = 0;                              // slot size of the global-class grains
     std::vector<int32_t> g64_lds, g64_glb;                // Ev64 indices by class
     std::vector<Chain64> chains_glb;
-    // Space-FIR taps of preset p ((delta + ER) * IR, MS:409-445), 0 without a FIR;
-    // need: the smallest transform that builds h in one piece
-    auto fir_taps = [&](int p, int64_t& need) -> int64_t {
+    // Taps of the space filter h = (delta + ER) * IR of preset p (MS:409-445), 0
+    // without a FIR: the largest ER offset (planned span or actual) plus the IR
+    // length, at most out_n (later taps never reach y[:out_n]).
+    auto h_taps = [&](int p) -> int64_t {
         const msg_preset& pr = presets[p];
         const bool er = (pr.flags & MSG_F_ER_CLOUD) != 0;
         const int ic = pr.ir_conv;
         const bool ir = (pr.flags & MSG_F_SPACE_IR) && ic >= 0 && ir_lens[ic] > 0;
-        need = 0;
         if (!er && !ir) return 0;
-        const int64_t er_span = er ? (int64_t)std::nearbyint(pr.er_max_ms / 1000.0 * (double)pr.base_sr) + 1 : 0;
-        const int64_t M = (ir ? std::min<int64_t>(ir_lens[ic], 8192) : 1) + er_span;
-        need = er ? (ir ? M - 1 : M) : 0;
-        return M;
+        const int64_t irl = ir ? std::min<int64_t>(ir_lens[ic], 8192) : 1;
+        const int64_t span = er ? std::max<int64_t>((int64_t)std::nearbyint(pr.er_max_ms / 1000.0 * (double)pr.base_sr),
+                                                    tap_max[p]) : 0;
+        return std::max<int64_t>(1, std::min<int64_t>(span + irl, info[p].out_n));
     };
     // k_fir4s pays one extra forward transform per workgroup: it is offered only
     // when the batch's streaming-eligible blocks give >= 2 blocks per workgroup
@@ -1220,9 +1228,8 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
     if (ctx->fir4 && ctx->fir4s) {
         int64_t total = 0;
         for (int p = 0; p < P; ++p) {
-            int64_t need;
-            const int64_t M = fir_taps(p, need);
-            if (M > 0 && M <= 2 * FIR4S_P && need <= 2 * FIR4S_P)
+            const int64_t M = h_taps(p);
+            if (M > 0 && M <= 2 * FIR4S_P)
                 total += (info[p].out_n + FIR4S_P - 1) / FIR4S_P;
         }
         fir4s_k = (int)std::min<int64_t>(ctx->fir4s_kmax, total / std::max(1, ctx->fir4s_wgs));
@@ -1240,7 +1247,7 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
         r.ev_begin = slot_base[p];
         r.n_events = inf.n_events;
         r.er_base = tap_base[p];
-        r.n_taps = (pr.flags & MSG_F_ER_CLOUD) ? std::max(1, pr.er_taps) : 0;
+        r.n_taps = n_taps_live[p];          // merged, in-range, offset-sorted taps
         r.tile_begin = tiles;
         r.max_n = inf.max_n;
         // generator sources (MS:333-362)
@@ -1286,11 +1293,10 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
         r.h_block_begin = hblocks;
         r.h_fir4 = 0;
         if (r.fir_on) {
-            int64_t need;
-            const int64_t M = fir_taps(p, need);
+            const int64_t M = h_taps(p);
             int N, Pp, Q;
             bool stream = false;
-            choose_fir(M, inf.out_n, need, N, Pp, Q, fir4s_ok ? &stream : nullptr, fir4s_k);
+            choose_fir(M, inf.out_n, N, Pp, Q, fir4s_ok ? &stream : nullptr, fir4s_k);
             std::string why;
             const int fp = real_plan(ctx->fir_plans, N, why);
             if (fp < 0) return fail(ctx, MSG_E_DEVICE, "FIR plan: " + why);
@@ -1298,29 +1304,14 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
             fir_lds = std::max(fir_lds, ctx->fir_plans.host[fp].lds_bytes);
             r.fir_N = N; r.fir_P = Pp; r.fir_Q = Q; r.fir_B = stream ? Pp : N - Pp + 1;
             r.h_off = hsum;
-            if (er && ir) {
-                if (M - 1 > N)
-                    return fail(ctx, MSG_E_UNSUPPORTED, "early-reflection span + IR exceed the 32768-sample FIR "
-                                                        "transform (er_max_ms too long for this rate)");
-                auto key = std::make_pair(ic, N);
-                auto it = ir_spec_of.find(key);
-                if (it == ir_spec_of.end()) {
-                    it = ir_spec_of.emplace(key, irs_sum).first;
-                    ir_jobs.insert(ir_jobs.end(), {r.ir_off, (int64_t)r.ir_len, (int64_t)fp, irs_sum});
-                    irs_sum += N / 2 + 1;
-                }
-                r.irs_off = it->second;
-                r.hs_off = hs_sum;
-                hs_sum += N;
-                if (N == 2 * 16384 && ctx->fir4) {   // the C3/C4 size: k_fir4_hconv + k_fir4_hpart
-                    r.h_fir4 = 1;
-                    conv4_list.push_back(p);
-                    for (int q = 0; q < Q; ++q) hpart_jobs.push_back(make_int2(p, q));
-                } else {
-                    conv_list.push_back(p);
-                }
-            } else if (er && M > N) {
-                return fail(ctx, MSG_E_UNSUPPORTED, "early-reflection span exceeds the FIR transform");
+            r.h_len = (int32_t)M;
+            r.hs_off = hs_sum;
+            hs_sum += (M + 3) & ~int64_t(3);    // 16-byte aligned h regions
+            h_tile_begin[p] = htiles;
+            htiles += (int32_t)((M + H_BUILD_TILE - 1) / H_BUILD_TILE);
+            if (N == 2 * 16384 && ctx->fir4) {   // the C3/C4 size: k_fir4_hpart
+                r.h_fir4 = 1;
+                for (int q = 0; q < Q; ++q) hpart_jobs.push_back(make_int2(p, q));
             }
             const int32_t nblk = (int32_t)((inf.out_n + r.fir_B - 1) / r.fir_B);
             if (stream) {
@@ -1333,6 +1324,8 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
             hblocks += Q;
             if (!r.h_fir4) hblocks_gen += Q;
             hsum += (int64_t)Q * (N / 2 + 1);
+        } else {
+            h_tile_begin[p] = htiles;
         }
         fir_begin[p] = r.fir_block_begin;
         h_begin[p] = r.h_block_begin;
@@ -1341,9 +1334,9 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
         const bool stereo = (pr.flags & MSG_F_STEREO) && inf.out_n >= 64;
         r.stereo_fir = stereo ? 1 : 0;
         if (stereo && (inf.out_n % 2)) {      // full-length rotation through Bluestein (kernels_stereo_odd.h)
-            const int64_t M = stereo_odd_len(inf.out_n);
+            const int64_t M = stereo_odd_len(inf.out_n, ctx->so_row, ctx->so_col);
             if (M < 0)
-                return fail(ctx, MSG_E_UNSUPPORTED, "stereo diffusion of an odd output longer than 4194304 frames");
+                return fail(ctx, MSG_E_UNSUPPORTED, "stereo diffusion of an odd output beyond the 2^34-point transform");
             r.stereo_fir = 2;
             r.r2_off = r2_sum;
             r2_sum += (inf.out_n + 3) & ~int64_t(3);
@@ -1579,7 +1572,6 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
     HIPCHK(ctx, ctx->mono_a.ensure(ysum));
     HIPCHK(ctx, ctx->mono_y.ensure(ysum));
     HIPCHK(ctx, ctx->hspec.ensure(hsum));
-    HIPCHK(ctx, ctx->irspec.ensure(irs_sum));
     HIPCHK(ctx, ctx->hscratch.ensure(hs_sum));
     HIPCHK(ctx, ctx->maxbits.ensure(P));
     auto h2d = [&](auto** dst, const auto* src, size_t bytes) -> hipError_t {
@@ -1608,9 +1600,7 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
     HIPCHK(ctx, h2d(&ctx->st_begin.p, st_begin.data(), sizeof(int32_t) * P));
     HIPCHK(ctx, h2d(&ctx->fir_plan_of.p, fir_plan_of.data(), sizeof(int32_t) * P));
     HIPCHK(ctx, h2d(&ctx->irbank.p, irbank.data(), sizeof(double) * irbank.size()));
-    HIPCHK(ctx, h2d(&ctx->irjobs.p, ir_jobs.data(), sizeof(int64_t) * ir_jobs.size()));
-    HIPCHK(ctx, h2d(&ctx->conv_list.p, conv_list.data(), sizeof(int32_t) * conv_list.size()));
-    HIPCHK(ctx, h2d(&ctx->conv4_list.p, conv4_list.data(), sizeof(int32_t) * conv4_list.size()));
+    HIPCHK(ctx, h2d(&ctx->h_tile_begin.p, h_tile_begin.data(), sizeof(int32_t) * P));
     HIPCHK(ctx, h2d(&ctx->hpart_jobs.p, hpart_jobs.data(), sizeof(int2) * hpart_jobs.size()));
     HIPCHK(ctx, hipMemsetAsync(ctx->maxbits.p, 0, sizeof(unsigned) * P, s));
     HIPCHK(ctx, h2d(&ctx->ev64.p, ev64.data(), sizeof(Ev64) * ev64.size()));
@@ -1686,22 +1676,14 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
     stage_mark(ctx, 5, s);
     float* yb = ctx->mono_a.p;
     if (hblocks > 0) {
-        if (!ir_jobs.empty()) {
-            HIPCHK(ctx, launch_ir_spec((unsigned)(ir_jobs.size() / 4), fir_lds, s, ctx->irjobs.p,
-                                       (int)(ir_jobs.size() / 4), ctx->fir_plans.dev.p, ctx->irbank.p, ctx->irspec.p));
-        }
-        if (!conv_list.empty())
-            HIPCHK(ctx, launch_fir_hconv((unsigned)conv_list.size(), fir_lds, s, ctx->prt.p, ctx->conv_list.p,
-                                         ctx->fir_plans.dev.p, ctx->fir_plan_of.p, ctx->er_off.p, ctx->er_gain.p,
-                                         ctx->irspec.p, ctx->hscratch.p));
-        if (!conv4_list.empty())
-            HIPCHK(ctx, launch_fir4_h(16384, (unsigned)conv4_list.size(), (unsigned)hpart_jobs.size(), s, ctx->prt.p,
-                                      ctx->conv4_list.p, ctx->hpart_jobs.p, ctx->d_fir4tab, ctx->er_off.p,
-                                      ctx->er_gain.p, ctx->irspec.p, ctx->hscratch.p, ctx->hspec.p));
+        HIPCHK(ctx, launch_h_build((unsigned)htiles, s, ctx->prt.p, ctx->h_tile_begin.p, P, ctx->er_off.p,
+                                   ctx->er_gain.p, ctx->irbank.p, ctx->hscratch.p));
+        if (!hpart_jobs.empty())
+            HIPCHK(ctx, launch_fir4_hpart(16384, (unsigned)hpart_jobs.size(), s, ctx->prt.p, ctx->hpart_jobs.p,
+                                          ctx->d_fir4tab, ctx->hscratch.p, ctx->hspec.p));
         if (hblocks_gen > 0)   // blocks of k_fir4-engine presets return at once
             HIPCHK(ctx, launch_fir_h((unsigned)hblocks, fir_lds, s, ctx->prt.p, ctx->h_begin.p, P,
-                                     ctx->fir_plans.dev.p, ctx->fir_plan_of.p, ctx->er_off.p, ctx->er_gain.p,
-                                     ctx->irbank.p, ctx->hscratch.p, ctx->hspec.p));
+                                     ctx->fir_plans.dev.p, ctx->fir_plan_of.p, ctx->hscratch.p, ctx->hspec.p));
         stage_mark(ctx, 8, s);
         for (int i = 0; i < 6; ++i) {
             if (fjob_off[i + 1] <= fjob_off[i]) continue;
@@ -1731,11 +1713,11 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
         auto it = ctx->so_bp.find(n);
         if (it == ctx->so_bp.end()) {
             it = ctx->so_bp.emplace(n, DevBuf<float2>()).first;
-            HIPCHK(ctx, it->second.ensure(stereo_odd_len(n)));
-            HIPCHK(ctx, launch_stereo_odd_kernel(n, it->second.p, ctx->so_A.p, s));
+            HIPCHK(ctx, it->second.ensure(stereo_odd_len(n, ctx->so_row, ctx->so_col)));
+            HIPCHK(ctx, launch_stereo_odd_kernel(n, ctx->so_row, ctx->so_col, it->second.p, ctx->so_A.p, s));
         }
         const double w = std::min(std::max(presets[p].stereo_width, 0.0), 1.0);
-        HIPCHK(ctx, launch_stereo_odd(n, prt[p].dr, w, yb + prt[p].y_off, it->second.p, ctx->so_A.p,
+        HIPCHK(ctx, launch_stereo_odd(n, ctx->so_row, ctx->so_col, prt[p].dr, w, yb + prt[p].y_off, it->second.p, ctx->so_A.p,
                                       ctx->so_r2.p + prt[p].r2_off, s));
     }
     hipLaunchKernelGGL(k_stereo_max, dim3((unsigned)stiles), dim3(ST_T), 0, s, ctx->prt.p, ctx->st_begin.p, P,

@@ -4,7 +4,7 @@
 //   k_gen_normal                   grain generator, one wave per event              MS:219-269
 //   k_spectral<T>                  LDS-resident spectral chain, one WG per event    MS:39-128, 224-233, 690-702
 //   k_ola_env                      grain overlap-add x ADSR, one WG per tile        MS:742-764
-//   k_fir_h                        (delta + ER) * IR kernel spectra per partition   MS:409-445
+//   k_h_build / k_fir_h            h = (delta + ER) * IR, its partition spectra      MS:409-445
 //   k_fir2<M>                      register-resident FFT overlap-save FIR           MS:766-773
 //   k_stereo_max / k_stereo_out    25-tap Bessel stereo, tanh, peak normalise       MS:423-436, 775-781
 #pragma once
@@ -37,19 +37,20 @@ struct PresetRt {
     int32_t ir_len;        // taps of the IR (0 -> delta)
     int64_t ir_off;        // offset of the IR in the device IR bank (float64)
     int64_t h_off;         // offset of the Q partition spectra (float2)
-    int64_t irs_off;       // offset of the IR spectrum at size fir_N (float2)
+    int32_t h_len;         // taps of h = (delta + ER) * IR (k_h_build), <= out_n
+    int32_t h_pad;
     // stereo / saturation / normalisation
     int32_t stereo_fir;    // 1: 25-tap Bessel FIR (even n), 2: precomputed R (odd n), 0: L = R = y
     int32_t dl, dr;
     float bess[25];        // J_m(0.9 w), m = -12..12
     float drive, peak;
-    int32_t h_fir4;        // 1: partition spectra built on the k_fir4 engine (k_fir4_hconv/hpart)
+    int32_t h_fir4;        // 1: partition spectra built on the k_fir4 engine (k_fir4_hpart)
     // generator sources: IR fragment (float64 IR bank) and image (uint8 bank)
     int64_t frag_off, frag_len;
     int64_t img_off;
     int32_t img_h, img_w;
     int64_t r2_off;        // stereo_fir == 2: rotated right channel in the odd-stereo buffer
-    int64_t hs_off;        // ER + IR presets: h in the FIR scratch (fir_N floats, k_fir_hconv)
+    int64_t hs_off;        // h in the FIR scratch (h_len floats, k_h_build)
 };
 
 // Per-event spectral work descriptor (host-built after planning).

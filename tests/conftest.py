@@ -43,3 +43,27 @@ def irs():
 def golden_info():
     with open(os.path.join(GOLDEN, "golden_info.json")) as fh:
         return json.load(fh)
+
+
+@pytest.fixture(scope="session")
+def extra_renders():
+    return np.load(os.path.join(GOLDEN, "render_extra.npz"))
+
+
+@pytest.fixture(scope="session")
+def golden_extra():
+    with open(os.path.join(GOLDEN, "golden_extra.json")) as fh:
+        return json.load(fh)
+
+
+def extra_params(golden_extra, irs, name):
+    """The params dict of a render_extra.npz case (tools/gen_golden_r3.py)."""
+    import msgpu
+    if name.startswith("H48_"):
+        return msgpu.config_params("H48", seed=int(name.split("_")[1]), irs=irs)
+    p = dict(golden_extra["params"][name])
+    ir = p.pop("_ir", None)
+    p = msgpu.merged(p)
+    p["_ir_audio"] = irs[ir] if ir else None
+    p["_img_gray"] = None
+    return p

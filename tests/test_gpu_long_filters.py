@@ -1,0 +1,148 @@
+"""Inputs the UI reaches beyond one transform (round 3), against the reference.
+
+* Space filters longer than one 32 768-point transform: early reflections up to
+  er_max_ms = 150 (MS:1118) at 176.4 / 192 kHz followed by an 8192-tap IR
+  (MS:409-421, MS:438-445), and early reflections alone at a preset-JSON rate of
+  384 kHz (57 601-sample span).  h = (delta + ER) * IR is built in the time
+  domain (k_h_build) and partitioned like any other filter.
+* Odd-length stereo rotations above 2^22 frames (MS:423-436): 95.25 s at
+  44.1 kHz (4 200 525 frames, M = 2^24) and 60 s + 1 frame at 192 kHz
+  (11 520 001 frames, M = 2^25) run the three-level Bluestein transform.
+* The metric label's 384 kHz -> 48 kHz point (config H48), seeds 1000..1003.
+
+Goldens: tests/golden/render_extra.npz + golden_extra.json (tools/gen_golden_r3.py,
+rendered by the reference itself).  Tolerance: 1e-5 RMS (north star).
+"""
+import numpy as np
+import pytest
+
+from conftest import extra_params
+
+pytestmark = pytest.mark.gpu
+
+RMS_TOL = 1e-5
+
+
+def rms(a, b):
+    a = np.asarray(a, dtype=np.float64)
+    b = np.asarray(b, dtype=np.float64)
+    assert a.shape == b.shape, (a.shape, b.shape)
+    return float(np.sqrt(np.mean((a - b) ** 2)))
+
+
+@pytest.fixture(scope="module")
+def msgpu():
+    import msgpu as m
+    m.render(m.merged(out_dur_s=0.05, er_cloud_on=False))
+    assert "libmsgpu.so" in open("/proc/self/maps").read()
+    return m
+
+
+LONG = ["ERIR192", "ERIR192t2000", "ERIR176", "ER384"]
+
+
+def test_long_space_filters(msgpu, irs, extra_renders, golden_extra):
+    params = [extra_params(golden_extra, irs, n) for n in LONG]
+    outs = msgpu.render_batch(params)
+    for name, p, a in zip(LONG, params, outs):
+        err = rms(a, extra_renders[f"{name}_audio"])
+        print(f"{name}: rms err {err:.3e}")
+        assert err <= RMS_TOL, name
+    single, _ = msgpu.render(params[0])
+    assert np.array_equal(single, outs[0])          # batching does not change results
+
+
+def test_long_space_filter_partitions(msgpu, irs):
+    """The 36 992-tap filter of ERIR192 against the oracle over a longer output
+    (several output blocks of each partition) and on the runtime-plan FIR
+    (MSGPU_FIR4=0 moves the N = 32 768 blocks to k_fir2 / k_fir_h)."""
+    import torch
+    from oracle import msound_oracle as O
+    from msgpu.engine import Engine
+    from msgpu.pack import PackedBatch
+    p = msgpu.merged(base_sr=192000, out_dur_s=0.9, gen_mode="Resonant strike", event_process="Poisson", seed=77,
+                     er_cloud_on=True, er_max_ms=150.0, er_taps=700, space_ir_on=True, space_ir_max_samps=8192,
+                     _ir_audio=irs["tiny_room_ir"])
+    ref, _ = O.render(p)
+    packed = PackedBatch([p])
+    outs = {}
+    for flag in ("1", "0"):
+        import os
+        os.environ["MSGPU_FIR4"] = flag
+        try:
+            eng = Engine(0)
+            outs[flag] = eng.render_packed(packed)
+            torch.cuda.synchronize(0)
+            outs[flag] = outs[flag].cpu().numpy()
+        finally:
+            os.environ.pop("MSGPU_FIR4", None)
+        err = rms(outs[flag][: ref.shape[0]], ref)
+        print(f"MSGPU_FIR4={flag}: rms err vs oracle {err:.3e}")
+        assert err <= RMS_TOL
+
+
+@pytest.mark.parametrize("name", ["ODD44", "ODD192L"])
+def test_odd_stereo_beyond_2_22(msgpu, irs, extra_renders, golden_extra, name):
+    p = extra_params(golden_extra, irs, name)
+    audio, _ = msgpu.render(p)
+    info = golden_extra["summaries"][name]
+    assert list(audio.shape) == info["shape"] and audio.shape[0] % 2 == 1
+    step = int(golden_extra["decimation"])
+    errs = {}
+    for part, key in ((audio[::step], "dec"), (audio[:8192], "head"), (audio[-8192:], "tail")):
+        errs[key] = rms(part, extra_renders[f"{name}_{key}"])
+    print(f"{name} n={audio.shape[0]}: " + ", ".join(f"{k} {v:.3e}" for k, v in errs.items()))
+    assert all(v <= RMS_TOL for v in errs.values()), errs
+    a64 = audio.astype(np.float64)
+    n = audio.shape[0]
+    assert abs(float(np.sqrt(np.mean(a64 ** 2))) - info["rms"]) <= RMS_TOL
+    assert abs(float(a64[:, 0].sum()) - info["sum_l"]) <= RMS_TOL * n
+    assert abs(float(a64[:, 1].sum()) - info["sum_r"]) <= RMS_TOL * n
+
+
+@pytest.mark.parametrize("frames", [4097, 240001])
+def test_odd_stereo_three_level_split(msgpu, frames):
+    """The three-level split (top column level over chunks of M1 x M2) at small
+    n: MSGPU_SO_ROW=64 / MSGPU_SO_COL=16 make every M > 1024 take it; the render
+    matches the oracle and the default two-level split to float32 rounding."""
+    import os
+    import torch
+    from oracle import msound_oracle as O
+    from msgpu.engine import Engine
+    from msgpu.pack import PackedBatch
+    sr = 48000
+    p = msgpu.merged(base_sr=sr, out_dur_s=frames / sr, gen_mode="Resonant strike", event_process="Poisson",
+                     grains_per_sec=30.0, env_a=0.0, env_r=1.0, seed=frames + 5, stereo_width=0.9)
+    packed = PackedBatch([p])
+    ref, _ = O.render(p)
+    outs = {}
+    for key, env in (("split", {"MSGPU_SO_ROW": "64", "MSGPU_SO_COL": "16"}), ("default", {})):
+        os.environ.update(env)
+        try:
+            eng = Engine(0)
+        finally:
+            for k in env:
+                os.environ.pop(k, None)
+        o = eng.render_packed(packed)
+        torch.cuda.synchronize(0)
+        outs[key] = o.cpu().numpy()[:frames]
+        err = rms(outs[key], ref)
+        print(f"odd stereo n={frames} [{key}]: rms err {err:.3e}")
+        assert err <= RMS_TOL
+    assert rms(outs["split"], outs["default"]) <= RMS_TOL
+
+
+def test_h48_metric_point(msgpu, irs, extra_renders, golden_extra):
+    """H48 (design 384 kHz, 48 kHz out: the metric label's point) seeds 1000..1003
+    as one batch: seed 1000 whole-buffer, all four by summary."""
+    names = [f"H48_{s}" for s in (1000, 1001, 1002, 1003)]
+    outs = msgpu.render_batch([extra_params(golden_extra, irs, n) for n in names])
+    assert rms(outs[0], extra_renders["H48_1000_audio"]) <= RMS_TOL
+    for name, a in zip(names, outs):
+        g = golden_extra["summaries"][name]
+        a64 = a.astype(np.float64)
+        n = a.shape[0]
+        assert list(a.shape) == g["shape"]
+        assert abs(float(np.sqrt(np.mean(a64 ** 2))) - g["rms"]) <= RMS_TOL, name
+        assert abs(float(a64[:, 0].sum()) - g["sum_l"]) <= RMS_TOL * n, name
+        assert abs(float(a64[:, 1].sum()) - g["sum_r"]) <= RMS_TOL * n, name

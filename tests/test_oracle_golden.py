@@ -179,3 +179,30 @@ def test_fir_causal_is_the_capped_ir_convolution():
     np.testing.assert_array_equal(O.fir_causal(x, O.ir_kernel(ir)), O.convolve_ir_short(x, ir))
     h = O.synthetic_fir_taps(16384)
     assert h.shape == (16384,) and abs(np.max(np.abs(h)) - 0.9) < 1e-12
+
+
+@pytest.mark.parametrize("name", ["ERIR192", "ERIR192t2000", "ERIR176", "ER384", "H48_1000"])
+def test_extra_renders(irs, extra_renders, golden_extra, name):
+    """Round-3 goldens (tools/gen_golden_r3.py): space filters longer than one
+    32 768-point transform and the H48 metric point, whole buffers."""
+    from conftest import extra_params
+    a, _ = _render_f32(extra_params(golden_extra, irs, name))
+    close(a, extra_renders[f"{name}_audio"], 2e-7)
+
+
+def test_extra_h48_summaries(irs, golden_extra):
+    from conftest import extra_params
+    for s in (1001, 1002, 1003):
+        a, _ = O.render(extra_params(golden_extra, irs, f"H48_{s}"))
+        g = golden_extra["summaries"][f"H48_{s}"]
+        assert hashlib.sha1(a.astype(np.float32).tobytes()).hexdigest() == g["sha1_f32"]
+
+
+@pytest.mark.slow
+def test_extra_odd_stereo_long(irs, extra_renders, golden_extra):
+    """ODD44: the oracle's odd-length rotation at 4 200 525 frames."""
+    from conftest import extra_params
+    a, _ = O.render(extra_params(golden_extra, irs, "ODD44"))
+    step = int(golden_extra["decimation"])
+    close(a[::step].astype(np.float32), extra_renders["ODD44_dec"], 2e-7)
+    close(a[-8192:].astype(np.float32), extra_renders["ODD44_tail"], 2e-7)

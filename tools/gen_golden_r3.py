@@ -1,0 +1,157 @@
+#!/usr/bin/env python3
+"""Round-3 golden vectors, from the reference ``render`` itself.
+
+Container-only tool (imports microsound_0.2.1/main_v2.py with the GUI modules
+stubbed, exactly as tools/gen_golden.py does).  Writes DATA fixtures:
+
+* ``tests/golden/render_extra.npz`` + ``tests/golden/golden_extra.json``:
+  - long space filters: early reflections + IR whose combined kernel is longer
+    than one 32768-point transform (MS:409-421 then MS:438-445; UI ranges MS:895,
+    MS:1116-1118): 192 kHz with er_max_ms 150 (320 and 2000 taps) and the
+    tiny-room IR; 384 kHz early reflections alone with er_max_ms 150;
+  - odd-length stereo rotations above 2^22 frames (MS:423-436): 44.1 kHz for
+    95.25 s (4 200 525 frames) and 192 kHz for 60 s + 1 frame (11 520 001
+    frames) -- summaries, every 64th frame and the first/last 8192 frames;
+  - the metric label's 384 kHz -> 48 kHz point (config H48) for seeds
+    1000..1003: summaries, and the whole buffer of seed 1000.
+* ``tests/golden/stage_pins_all.npz``: EVERY call's input to ``cepstral_warp``
+  (MS:150-163) and ``SpectralImprint.apply`` (MS:565-581) in the seven
+  spread-held presets (0.5 s, tiny-room IR, the golden image), in call order.
+
+    python tools/gen_golden_r3.py [--only renders|pins]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+sys.dont_write_bytecode = True
+
+import numpy as np  # noqa: E402
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "tools"))
+sys.path.insert(0, os.path.join(REPO, "audio-suite_amd"))
+
+from gen_golden import REF_DIR, import_reference, load_irs, summary  # noqa: E402
+from msgpu.params import config_params, merged  # noqa: E402
+
+OUT = os.path.join(REPO, "tests", "golden")
+DSTEP = 64
+
+# name -> params builder (irs) ; "full": store the whole buffer, else summary + decimation
+def cases(irs):
+    tiny = irs["tiny_room_ir"]
+    space = dict(gen_mode="Resonant strike", event_process="Poisson", seed=1000)
+    return {
+        # 192 kHz, er_max 150 ms: 28 801-sample ER span + 8192-tap IR = 36 992 taps
+        "ERIR192": (merged(space, base_sr=192000, out_dur_s=0.3, er_cloud_on=True, er_max_ms=150.0,
+                           space_ir_on=True, space_ir_max_samps=8192, _ir_audio=tiny), "full"),
+        "ERIR192t2000": (merged(space, base_sr=192000, out_dur_s=0.3, er_cloud_on=True, er_max_ms=150.0,
+                                er_taps=2000, space_ir_on=True, space_ir_max_samps=8192, _ir_audio=tiny,
+                                seed=1001), "full"),
+        # 176.4 kHz, er_max 129 ms: just over one transform (22 757 + 8192 taps with 2 partitions)
+        "ERIR176": (merged(space, base_sr=176400, out_dur_s=0.25, er_cloud_on=True, er_max_ms=129.0,
+                           space_ir_on=True, space_ir_max_samps=8192, _ir_audio=tiny, seed=1002), "full"),
+        # early reflections alone, 57 601-sample span (preset JSON rate 384 kHz)
+        "ER384": (merged(space, base_sr=384000, out_dur_s=0.25, er_cloud_on=True, er_max_ms=150.0,
+                         space_ir_on=False, seed=1003), "full"),
+        # odd stereo above 2^22 frames
+        "ODD44": (merged(space, base_sr=44100, out_dur_s=95.25, er_cloud_on=True, stereo_width=0.8,
+                         grains_per_sec=18.0), "dec"),
+        "ODD192L": (merged(space, base_sr=192000, out_dur_s=60.0 + 1 / 192000, er_cloud_on=True,
+                           stereo_width=0.65, grains_per_sec=6.0, time_unfold=10.0), "dec"),
+    }
+
+
+def renders(ms, irs):
+    arrays, info = {}, {"summaries": {}, "params": {}, "timings_s": {}, "numpy": np.__version__,
+                        "generator": "tools/gen_golden_r3.py", "decimation": DSTEP}
+    todo = dict(cases(irs))
+    for s in (1000, 1001, 1002, 1003):
+        todo[f"H48_{s}"] = (config_params("H48", seed=s, irs=irs), "full" if s == 1000 else "summary")
+    for name, (p, mode) in todo.items():
+        t0 = time.time()
+        audio, meta = ms.render(p)
+        dt = time.time() - t0
+        info["summaries"][name] = summary(audio)
+        info["timings_s"][name] = dt
+        info["params"][name] = {k: v for k, v in p.items() if not k.startswith("_")}
+        if p.get("_ir_audio") is not None:
+            info["params"][name]["_ir"] = "tiny_room_ir" if p["_ir_audio"] is irs["tiny_room_ir"] else "?"
+        info["summaries"][name]["design_sr_base"] = int(meta["design_sr_base"])
+        if mode == "full":
+            arrays[f"{name}_audio"] = audio.astype(np.float32)
+        elif mode == "dec":
+            arrays[f"{name}_dec"] = audio[::DSTEP].astype(np.float32)
+            arrays[f"{name}_head"] = audio[:8192].astype(np.float32)
+            arrays[f"{name}_tail"] = audio[-8192:].astype(np.float32)
+        print(f"{name}: {audio.shape} {dt:.1f}s", flush=True)
+    np.savez_compressed(os.path.join(OUT, "render_extra.npz"), **arrays)
+    with open(os.path.join(OUT, "golden_extra.json"), "w") as fh:
+        json.dump(info, fh, indent=1)
+
+
+PIN_PRESETS = ["ghost_formants", "03_wavelet_ice_bloom", "wavelet_mist", "closed_curve_air",
+               "drifting_mode_fragments", "corona_glass_fog", "soft_ellipse_memory"]
+
+
+def pins(ms, irs):
+    img = (np.add.outer(np.arange(48), np.arange(64)) * 7 % 256).astype(np.uint8)   # as gen_golden.py
+    rec = {"cep": [], "imp": []}
+    cep0, imp0 = ms.cepstral_warp, ms.SpectralImprint.apply
+
+    def cep(x, *a, **k):
+        rec["cep"].append(np.array(x, dtype=np.float64, copy=True))
+        return cep0(x, *a, **k)
+
+    def imp(self, grain, *a, **k):
+        rec["imp"].append(np.array(grain, dtype=np.float64, copy=True))
+        return imp0(self, grain, *a, **k)
+
+    ms.cepstral_warp = cep
+    ms.SpectralImprint.apply = imp
+    out, meta = {}, {}
+    try:
+        for name in PIN_PRESETS:
+            with open(os.path.join(REF_DIR, "presets", f"{name}.json"), encoding="utf-8") as fh:
+                p = merged(json.load(fh))
+            p["out_dur_s"] = 0.5
+            p["_ir_audio"] = irs["tiny_room_ir"]
+            p["_img_gray"] = img
+            rec["cep"].clear()
+            rec["imp"].clear()
+            ms.render(p)
+            meta[name] = {}
+            for k, calls in rec.items():
+                if not calls:
+                    continue
+                lens = np.array([c.size for c in calls], dtype=np.int64)
+                out[f"{name}_{k}_lens"] = lens
+                out[f"{name}_{k}_data"] = np.concatenate(calls)
+                meta[name][k] = len(calls)
+            print(name, meta[name], flush=True)
+    finally:
+        ms.cepstral_warp, ms.SpectralImprint.apply = cep0, imp0
+    out["info"] = np.array(json.dumps({"numpy": np.__version__, "calls": meta,
+                                       "generator": "tools/gen_golden_r3.py"}))
+    np.savez_compressed(os.path.join(OUT, "stage_pins_all.npz"), **out)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--only", choices=["renders", "pins"])
+    a = ap.parse_args()
+    ms = import_reference()
+    irs = load_irs()
+    if a.only in (None, "pins"):
+        pins(ms, irs)
+    if a.only in (None, "renders"):
+        renders(ms, irs)
+
+
+if __name__ == "__main__":
+    main()
