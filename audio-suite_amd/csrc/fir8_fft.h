@@ -1,0 +1,316 @@
+// fir8_fft.h — overlap-save FIR with a 65 536-point transform (TU: k_fir.hip).
+//
+// One output block of B = N - P + 1 frames per workgroup, N = 65 536 real
+// samples, one partition (Q = 1, P <= ~45 000 taps): the C3/C4 space filter
+// (25 473 taps) takes 2 transforms of N per ~40 000 outputs instead of k_fir4's
+// 3 transforms of 32 768 per ~20 000 (a third fewer transform passes per output,
+// and each output goes through two transforms instead of three).
+//
+// The packed complex sequence z[m] = x[2m] + i x[2m+1] has M = 32 768 points,
+// twice what LDS holds.  It is split once, in registers, by a radix-2
+// decimation-in-frequency step:
+//     a[m] = z[m] + z[m + MH],  b[m] = (z[m] - z[m + MH]) W_M^m,   m < MH = M/2
+//     Z[2k] = FFT_MH(a)[k],     Z[2k+1] = FFT_MH(b)[k]
+// and each half runs on the k_fir4 engine (Fir4Geo<16384>: 1024 threads,
+// radices 16 16 8 8, LDS exchanges, last pass into registers).  Real-FFT pairs
+// (k, M - k) stay inside a half: even bins pair kappa <-> MH - kappa (k_fir4's
+// pairing: butterflies j, NB4 - j, thread 0 self-paired), odd bins kappa <->
+// MH - 1 - kappa (butterflies j, NB4 - 1 - j, no self-paired bins).  The
+// product with H and the inverse pre-step run per half in registers; the
+// inverse of each half is the k_fir4 inverse engine (forward FFT of conj Z'),
+// and the two halves are joined by the decimation-in-time step
+//     F[m] = A[m] + W_M^m B[m],  F[m + MH] = A[m] - W_M^m B[m]
+// before the outputs go to HBM.  Register live set at every point: one half
+// (32 VGPRs: b while the even half transforms, A while the odd half does)
+// beside the working set -- k_fir4's accumulator profile.
+//
+// H layout (k_fir8_hpart): He[kappa] = H[2 kappa] (kappa <= MH), then
+// Ho[kappa] = H[2 kappa + 1] (kappa < MH): M + 1 float2 per preset, contiguous
+// per half so the MAC reads are unit-stride.
+#pragma once
+#include "fir4_fft.h"
+
+namespace fir8 {
+using G = Fir4Geo<16384>;
+constexpr int MH = 16384, M = 2 * MH, N = 2 * M;
+constexpr int T = G::T, R1 = G::R1, R2 = G::R2, R3 = G::R3, R4 = G::R4;
+constexpr int NB1 = G::NB1, NB4 = G::NB4;
+static_assert(NB1 == T && NB4 == 2 * T, "fir8 geometry");
+
+// W_M^(1024 r) = W_32^r and exp(-2 pi i / N)
+template <int R> MSG_DEV float2 w32(int r) {
+    return make_float2((float)__builtin_cos(2.0 * 3.14159265358979323846 * r / 32),
+                       (float)-__builtin_sin(2.0 * 3.14159265358979323846 * r / 32));
+}
+MSG_DEV float2 wN1() {
+    return make_float2((float)__builtin_cos(2.0 * 3.14159265358979323846 / N),
+                       (float)-__builtin_sin(2.0 * 3.14159265358979323846 / N));
+}
+
+// butterflies of the last forward pass held by thread t
+template <bool ODD> MSG_DEV void js_of(int t, int (&js)[2]) {
+    js[0] = t;
+    js[1] = ODD ? NB4 - 1 - t : (t == 0 ? NB4 / 2 : NB4 - t);
+}
+
+// Forward FFT_MH of one half from registers (in[r] = element t + r NB1) to the
+// last pass's butterflies js in v (k_fir4's passes 1-4).
+template <bool ODD>
+MSG_DEV void fwd_half(float2* buf, const float2* tab, float2 (&in)[R1], float2 (&v)[2][R4]) {
+    const int t = otid();
+    Dft<R1, false>::run(in);
+    {
+        const int base = pads<G::S1>(t * R1);
+#pragma unroll
+        for (int r = 0; r < R1; ++r) buf[base + r] = in[r];
+    }
+    __syncthreads();
+    fir4_pass_lds<MH, R2, R1, G::BP2, G::S1, G::S2, true, G::OFF_TA>(buf, tab, t);
+    __syncthreads();
+    fir4_pass_lds<MH, R3, R1 * R2, G::BP3, G::S2, G::S3, false, 0>(buf, tab, t);
+    __syncthreads();
+    int js[2];
+    js_of<ODD>(t, js);
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int r = 0; r < R4; ++r) v[h][r] = buf[pads<G::S3>(js[h] + r * NB4)];
+    __syncthreads();   // LDS free for the inverse
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        twiddle_pow_ab<R4, tw_base<R4>()>(v[h], fir_wM(tab, G::OFF_MLO, G::OFF_MHI, js[h]),
+                                          fir_wM(tab, G::OFF_MLO, G::OFF_MHI, (js[h] * tw_base<R4>()) & (MH - 1)));
+        Dft<R4, false>::run(v[h]);
+    }
+}
+
+// Inverse of one half: the pre-stepped pairs acc (butterflies js) through the
+// k_fir4 inverse engine; u[r] = FFT_MH(conj Z'_half)[t + r NB1].
+template <bool ODD>
+MSG_DEV void inv_half(float2* buf, const float2* tab, float2 (&acc)[2][R4], float2 (&u)[R1]) {
+    const int t = otid();
+    int js[2];
+    js_of<ODD>(t, js);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        Dft<R4, false>::run(acc[h]);
+        const int base = pads<G::S1I>(js[h] * R4);
+#pragma unroll
+        for (int r = 0; r < R4; ++r) buf[base + r] = acc[h][r];
+    }
+    __syncthreads();
+    fir4_pass_lds<MH, R3, R4, G::BP3, G::S1I, G::S2I, true, G::OFF_TB>(buf, tab, t);
+    __syncthreads();
+    fir4_pass_lds<MH, R2, R4 * R3, G::BP2, G::S2I, G::S3I, false, 0>(buf, tab, t);
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < R1; ++r) u[r] = buf[pads<G::S3I>(t + r * NB1)];
+    __syncthreads();   // LDS free for the next half
+    twiddle_pow_ab<R1, tw_base<R1>()>(u, fir_wM(tab, G::OFF_MLO, G::OFF_MHI, t),
+                                      fir_wM(tab, G::OFF_MLO, G::OFF_MHI, (t * tw_base<R1>()) & (MH - 1)));
+    Dft<R1, false>::run(u);
+}
+
+// Even half: X[2 kappa] . He (k_fir4's split and MAC, thread 0's self-paired
+// slots included), then the inverse pre-step; acc leaves as conj Z' pairs.
+MSG_DEV void even_mac_pre(const float2* tab, const float2 (&v)[2][R4], const float2* __restrict__ He,
+                          float2 (&acc)[2][R4]) {
+    const int t = otid();
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int r = 0; r < R4; ++r) acc[h][r] = make_float2(0.f, 0.f);
+    if (t != 0) {
+        const float2 wA = fir_wM(tab, G::OFF_PLO, G::OFF_PHI, t);
+#pragma unroll
+        for (int r = 0; r < R4; ++r) {
+            const int kA = t + r * NB4;
+            const float2 wk = cmul_k(wA, fir_cr<R4>(r));
+            fir_pair_mac(v[0][r], v[1][R4 - 1 - r], wk, He[(uint32_t)kA], He[(uint32_t)(MH - kA)], acc[0][r],
+                         acc[1][R4 - 1 - r]);
+            fir_pair_pre(acc[0][r], acc[1][R4 - 1 - r], wk);
+        }
+    } else {
+        float2 a[R4], bb[R4];
+        fir_slots<R4>(v, a, bb, true);
+#pragma unroll
+        for (int r = 0; r < R4; ++r) {
+            const int kA = fir_k0<MH, R4>(r);
+            if (r < R4 - 1) {
+                fir_pair_mac(a[r], bb[R4 - 1 - r], fir_w0<MH, R4>(r), He[kA], He[MH - kA], acc[0][r],
+                             acc[1][R4 - 1 - r]);
+            } else {   // DC/Nyquist packed as (Y[0], Y[M]) and bin M/2
+                const float2 z0 = a[r];
+                acc[0][r] = make_float2((z0.x + z0.y) * He[0].x, (z0.x - z0.y) * He[MH].x);
+                acc[1][0] = cmul(cconj(bb[0]), He[MH / 2]);
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < R4 - 1; ++r) fir_pair_pre(acc[0][r], acc[1][R4 - 1 - r], fir_w0<MH, R4>(r));
+        const float y0 = acc[0][R4 - 1].x, yN = acc[0][R4 - 1].y;
+        acc[0][R4 - 1] = make_float2(0.5f * (y0 + yN), -0.5f * (y0 - yN));   // bin M/2: conj Z' = Y
+        fir_unslots<R4>(acc, true);
+    }
+}
+
+// Odd half: X[2 kappa + 1] . Ho and the inverse pre-step (pairs kappa, MH-1-kappa).
+MSG_DEV void odd_mac_pre(const float2* tab, const float2 (&v)[2][R4], const float2* __restrict__ Ho,
+                         float2 (&acc)[2][R4]) {
+    const int t = otid();
+    const float2 wA = cmul_k(fir_wM(tab, G::OFF_PLO, G::OFF_PHI, t), wN1());   // W_N^(2t+1)
+#pragma unroll
+    for (int r = 0; r < R4; ++r) {
+        const int kA = t + r * NB4;
+        const float2 wk = cmul_k(wA, fir_cr<R4>(r));
+        float2 xk, xm;
+        fir_split(v[0][r], v[1][R4 - 1 - r], wk, xk, xm);
+        acc[0][r] = cmul(xk, Ho[(uint32_t)kA]);
+        acc[1][R4 - 1 - r] = cmul(xm, Ho[(uint32_t)(MH - 1 - kA)]);
+        fir_pair_pre(acc[0][r], acc[1][R4 - 1 - r], wk);
+    }
+}
+
+// Load z[t + r NB1] and z[t + r NB1 + MH] of the segment x[s0, s0 + N) (zero
+// outside [0, n)) into a and (z0 - z1) into b (twiddled after the tables are in LDS).
+MSG_DEV void load_halves(const float* __restrict__ x, int64_t n, int64_t s0, float2 (&a)[R1], float2 (&b)[R1]) {
+    const int t = otid();
+    const bool fast = s0 >= 0 && s0 + N <= n && (((uintptr_t)(x + s0)) & 7) == 0;
+    if (fast) {
+        const float2* z = reinterpret_cast<const float2*>(x + s0);
+#pragma unroll
+        for (int r = 0; r < R1; ++r) {
+            a[r] = z[(uint32_t)(t + r * NB1)];
+            b[r] = z[(uint32_t)(t + r * NB1 + MH)];
+        }
+    } else {
+#pragma unroll
+        for (int r = 0; r < R1; ++r) {
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int64_t i = s0 + 2 * (int64_t)(t + r * NB1 + h * MH);
+                const bool in0 = i >= 0 && i < n, in1 = i + 1 >= 0 && i + 1 < n;
+                const float x0 = x[(uint32_t)(in0 ? i : 0)], x1 = x[(uint32_t)(in1 ? i + 1 : 0)];
+                (h ? b : a)[r] = make_float2(in0 ? x0 : 0.f, in1 ? x1 : 0.f);
+            }
+        }
+    }
+}
+
+// (a, b) <- (a + b, (a - b) W_M^(t + r NB1))
+MSG_DEV void dif_split(const float2* tab, float2 (&a)[R1], float2 (&b)[R1]) {
+    const float2 wt = fir_wM(tab, G::OFF_PLO, G::OFF_PHI, otid());   // W_M^t (PLO/PHI: W_{2 MH} = W_M)
+#pragma unroll
+    for (int r = 0; r < R1; ++r) {
+        const float2 z0 = a[r], z1 = b[r];
+        a[r] = ff(vv(z0) + vv(z1));
+        const float2 d = ff(vv(z0) - vv(z1));
+        b[r] = r == 0 ? cmul(d, wt) : cmul(d, cmul_k(wt, w32<R1>(r)));
+    }
+}
+}  // namespace fir8
+
+template <int UNUSED = 0>
+__global__ void __launch_bounds__(fir8::T)
+k_fir8(const PresetRt* __restrict__ rt, const int2* __restrict__ jobs, const float2* __restrict__ tables,
+       const float2* __restrict__ hspec, const float* __restrict__ x_in, float* __restrict__ y_out) {
+    using namespace fir8;
+    extern __shared__ __attribute__((aligned(16))) float2 lds[];
+    float2* tab = lds;
+    float2* buf = lds + G::TAB;
+    const int2 job = jobs[xcd_block(blockIdx.x, gridDim.x)];
+    const PresetRt& pr = rt[job.x];
+    const int P = pr.fir_P;                       // Q == 1
+    const int64_t n = pr.out_n;
+    const int64_t t0 = (int64_t)job.y * pr.fir_B;
+    for (int i = threadIdx.x; i < G::TAB_USED; i += T) tab[i] = tables[i];
+    float2 a[R1], b[R1];
+    load_halves(x_in + pr.y_off, n, t0 - (P - 1), a, b);
+    __syncthreads();                              // tables visible
+    dif_split(tab, a, b);
+    const float2* He = hspec + pr.h_off;
+    const float2* Ho = He + (MH + 1);
+    float2 v[2][R4], acc[2][R4], A[R1];
+    fwd_half<false>(buf, tab, a, v);
+    even_mac_pre(tab, v, He, acc);
+    inv_half<false>(buf, tab, acc, A);
+    fwd_half<true>(buf, tab, b, v);
+    odd_mac_pre(tab, v, Ho, acc);
+    float2 (&B)[R1] = a;                          // a is dead: its registers take B
+    inv_half<true>(buf, tab, acc, B);
+    // F[m] = A + W_M^m B, F[m + MH] = A - W_M^m B; z'[m] = conj(F[m]) / M
+    const int t = otid();
+    const float2 wt = fir_wM(tab, G::OFF_PLO, G::OFF_PHI, t);
+    float* y = y_out + pr.y_off;
+    const float s = 1.0f / (float)M;
+#pragma unroll
+    for (int r = 0; r < R1; ++r) {
+        const float2 wb = r == 0 ? cmul(B[r], wt) : cmul(B[r], cmul_k(wt, w32<R1>(r)));
+        const float2 f[2] = {ff(vv(A[r]) + vv(wb)), ff(vv(A[r]) - vv(wb))};
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int u = 2 * (t + r * NB1 + h * MH);        // segment sample of z'[u/2]
+            const int64_t o = t0 + u - (P - 1);
+            if (u >= P - 1 && o < n) y[(uint32_t)o] = f[h].x * s;
+            if (u + 1 >= P - 1 && o + 1 < n) y[(uint32_t)(o + 1)] = -f[h].y * s;
+        }
+    }
+}
+
+// H = rfft_N(h[0, P)) of one preset (Q = 1), in the even/odd layout above; h
+// from k_h_build's scratch.  One workgroup per preset.
+template <int UNUSED = 0>
+__global__ void __launch_bounds__(fir8::T)
+k_fir8_hpart(const PresetRt* __restrict__ rt, const int32_t* __restrict__ list, const float2* __restrict__ tables,
+             const float* __restrict__ hs, float2* __restrict__ hspec) {
+    using namespace fir8;
+    extern __shared__ __attribute__((aligned(16))) float2 lds[];
+    float2* tab = lds;
+    float2* buf = lds + G::TAB;
+    const PresetRt& r = rt[list[blockIdx.x]];
+    for (int i = threadIdx.x; i < G::TAB_USED; i += T) tab[i] = tables[i];
+    float2 a[R1], b[R1];
+    load_halves(hs + r.hs_off, r.h_len < r.fir_P ? r.h_len : r.fir_P, 0, a, b);
+    __syncthreads();
+    dif_split(tab, a, b);
+    float2* He = hspec + r.h_off;
+    float2* Ho = He + (MH + 1);
+    const int t = otid();
+    float2 v[2][R4];
+    fwd_half<false>(buf, tab, a, v);
+    if (t != 0) {
+        const float2 wA = fir_wM(tab, G::OFF_PLO, G::OFF_PHI, t);
+#pragma unroll
+        for (int q = 0; q < R4; ++q) {
+            const int kA = t + q * NB4;
+            float2 xk, xm;
+            fir_split(v[0][q], v[1][R4 - 1 - q], cmul_k(wA, fir_cr<R4>(q)), xk, xm);
+            He[(uint32_t)kA] = xk;
+            He[(uint32_t)(MH - kA)] = xm;
+        }
+    } else {
+        float2 aa[R4], bb[R4];
+        fir_slots<R4>(v, aa, bb, true);
+#pragma unroll
+        for (int q = 0; q < R4 - 1; ++q) {
+            const int kA = fir_k0<MH, R4>(q);
+            float2 xk, xm;
+            fir_split(aa[q], bb[R4 - 1 - q], fir_w0<MH, R4>(q), xk, xm);
+            He[kA] = xk;
+            He[MH - kA] = xm;
+        }
+        const float2 z0 = aa[R4 - 1];
+        He[0] = make_float2(z0.x + z0.y, 0.f);
+        He[MH] = make_float2(z0.x - z0.y, 0.f);
+        He[MH / 2] = cconj(bb[0]);
+    }
+    fwd_half<true>(buf, tab, b, v);
+    const float2 wA = cmul_k(fir_wM(tab, G::OFF_PLO, G::OFF_PHI, t), wN1());
+#pragma unroll
+    for (int q = 0; q < R4; ++q) {
+        const int kA = t + q * NB4;
+        float2 xk, xm;
+        fir_split(v[0][q], v[1][R4 - 1 - q], cmul_k(wA, fir_cr<R4>(q)), xk, xm);
+        Ho[(uint32_t)kA] = xk;
+        Ho[(uint32_t)(MH - 1 - kA)] = xm;
+    }
+}

@@ -15,6 +15,7 @@
 #include "ziggurat_tables.h"
 #include "nprng.h"
 #include "plan.h"
+#include "host_pool.h"
 #include "../../include/msgpu.h"
 
 namespace {
@@ -30,6 +31,7 @@ int no_device() { return fail(nullptr, MSG_E_DEVICE, "host sanitizer build: no d
 
 extern "C" {
 int msg_abi_version(void) { return MSG_ABI_VERSION; }
+int msg_host_threads(void) { return HostPool::get().threads(); }
 int64_t msg_sizeof(int32_t which) {
     switch (which) {
         case 0: return (int64_t)sizeof(msg_preset);
@@ -48,6 +50,7 @@ int msg_render_batch(msg_ctx*, const msg_preset*, int32_t, const double* const*,
 int msg_last_plan(msg_ctx*, msg_plan_info*, int32_t) { return no_device(); }
 int msg_last_events(msg_ctx*, int32_t, msg_event*, int32_t, int32_t*) { return no_device(); }
 int msg_last_meta(msg_ctx*, int32_t, double*, double*, int64_t, int64_t*) { return no_device(); }
+int msg_last_grain64(msg_ctx*, int32_t, int32_t, double*, int64_t, int64_t*) { return no_device(); }
 int msg_set_profiling(msg_ctx*, int32_t) { return no_device(); }
 int msg_stage_times(msg_ctx*, float*, int32_t) { return no_device(); }
 int msg_gate(msg_ctx*, msg_ctx*, int32_t, int32_t) { return no_device(); }

@@ -2,6 +2,7 @@
 #include "kernels_fir.h"
 #include "fir_fft.h"
 #include "fir4_fft.h"
+#include "fir8_fft.h"
 #include "launch.h"
 
 template <int M> static void fir2_attr() {
@@ -21,6 +22,10 @@ void fir_init_attrs() {
     (void)hipFuncSetAttribute((const void*)k_fir4s<16384>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               Fir4Geo<16384>::LDS_BYTES);
     (void)hipFuncSetAttribute((const void*)k_fir4_hpart<16384>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              Fir4Geo<16384>::LDS_BYTES);
+    (void)hipFuncSetAttribute((const void*)k_fir8<0>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              Fir4Geo<16384>::LDS_BYTES);
+    (void)hipFuncSetAttribute((const void*)k_fir8_hpart<0>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               Fir4Geo<16384>::LDS_BYTES);
     fir2_attr<1024>(); fir2_attr<2048>(); fir2_attr<4096>(); fir2_attr<8192>(); fir2_attr<16384>();
     (void)hipFuncSetAttribute((const void*)k_fir_h<FIR_T, FIR_M>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
@@ -108,6 +113,20 @@ hipError_t launch_fir4_hpart(int M, unsigned n_parts, hipStream_t s, const Prese
     if (M != 16384) return hipErrorInvalidValue;
     hipLaunchKernelGGL((k_fir4_hpart<16384>), dim3(n_parts), dim3(Fir4Geo<16384>::T), Fir4Geo<16384>::LDS_BYTES, s,
                        rt, part_jobs, tables, hs, hspec);
+    return hipGetLastError();
+}
+
+hipError_t launch_fir8(unsigned grid, hipStream_t s, const PresetRt* rt, const int2* jobs, const float2* tables,
+                       const float2* hspec, const float* x_in, float* y_out) {
+    hipLaunchKernelGGL((k_fir8<0>), dim3(grid), dim3(fir8::T), Fir4Geo<16384>::LDS_BYTES, s, rt, jobs, tables, hspec,
+                       x_in, y_out);
+    return hipGetLastError();
+}
+
+hipError_t launch_fir8_hpart(unsigned n_presets, hipStream_t s, const PresetRt* rt, const int32_t* list,
+                             const float2* tables, const float* hs, float2* hspec) {
+    hipLaunchKernelGGL((k_fir8_hpart<0>), dim3(n_presets), dim3(fir8::T), Fir4Geo<16384>::LDS_BYTES, s, rt, list,
+                       tables, hs, hspec);
     return hipGetLastError();
 }
 

@@ -65,6 +65,13 @@ constexpr int FIR4S_P = 16384;
 // partition spectra on the k_fir4 engine (fir4_fft.h): k_fir4_hpart over the (preset, q) jobs
 hipError_t launch_fir4_hpart(int M, unsigned n_parts, hipStream_t s, const PresetRt* rt, const int2* part_jobs,
                              const float2* tables, const float* hs, float2* hspec);
+// N = 65536 overlap-save, one partition (fir8_fft.h): blocks on the k_fir4 engine in
+// two halves; k_fir8_hpart builds H (even/odd bin layout, N/2 + 1 float2) per listed preset
+constexpr int FIR8_N = 65536;
+hipError_t launch_fir8(unsigned grid, hipStream_t s, const PresetRt* rt, const int2* jobs, const float2* tables,
+                       const float2* hspec, const float* x_in, float* y_out);
+hipError_t launch_fir8_hpart(unsigned n_presets, hipStream_t s, const PresetRt* rt, const int32_t* list,
+                             const float2* tables, const float* hs, float2* hspec);
 hipError_t launch_fir4s(int M, unsigned grid, hipStream_t s, const PresetRt* rt, const int2* jobs,
                         const float2* tables, const float2* hspec, const float* x_in, float* y_out, int kblk);
 

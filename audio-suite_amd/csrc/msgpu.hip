@@ -10,7 +10,9 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <deque>
 #include <map>
+#include <sched.h>
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
@@ -29,6 +31,7 @@
 #include "fft_lds.h"
 #include "kernels_core.h"
 #include "launch.h"
+#include "host_pool.h"
 #include "../../include/msgpu.h"
 
 namespace {
@@ -38,6 +41,7 @@ const nprng::Zig kHostZig = {zig_ki_double, zig_wi_double, zig_fi_double,
 
 
 thread_local std::string g_err;   // errors before a context exists
+std::mutex g_gate_mu;              // msg_gate links between contexts
 
 template <class T>
 struct DevBuf {
@@ -53,85 +57,6 @@ struct DevBuf {
         return e;
     }
     void release() { if (p) hipFree(p); p = nullptr; cap = 0; }
-};
-
-// Host worker pool for the per-preset planning of a batch (plan.h on the CPU).
-// One process-wide pool; the caller takes part in the work.  A call that finds
-// the pool busy (another thread rendering) runs its loop inline.
-class HostPool {
-  public:
-    static HostPool& get() {
-        static HostPool pool;
-        return pool;
-    }
-    template <class F>
-    void run(int count, F&& f) {
-        if (count <= 0) return;
-        std::unique_lock<std::mutex> busy(busy_, std::try_to_lock);
-        if (!busy.owns_lock() || workers_.empty() || count < 2) {
-            for (int i = 0; i < count; ++i) f(i);
-            return;
-        }
-        std::function<void(int)> fn(std::ref(f));
-        {
-            std::lock_guard<std::mutex> lk(m_);
-            job_ = &fn;
-            count_ = count;
-            next_.store(0);
-            running_ = (int)workers_.size();
-            ++gen_;
-        }
-        cv_.notify_all();
-        drain(fn);
-        std::unique_lock<std::mutex> lk(m_);
-        done_cv_.wait(lk, [&] { return running_ == 0; });
-        job_ = nullptr;
-    }
-    ~HostPool() {
-        {
-            std::lock_guard<std::mutex> lk(m_);
-            stop_ = true;
-            ++gen_;
-        }
-        cv_.notify_all();
-        for (auto& t : workers_) t.join();
-    }
-
-  private:
-    HostPool() {
-        int n = 16;                                   // the GPU box's CPU share per job
-        if (const char* e = getenv("MSGPU_HOST_THREADS")) n = atoi(e);
-        const int hw = (int)std::thread::hardware_concurrency();
-        if (hw > 0) n = std::min(n, hw);
-        for (int i = 0; i + 1 < n; ++i) workers_.emplace_back([this] { loop(); });
-    }
-    void drain(const std::function<void(int)>& fn) {
-        for (int i = next_.fetch_add(1); i < count_; i = next_.fetch_add(1)) fn(i);
-    }
-    void loop() {
-        uint64_t seen = 0;
-        for (;;) {
-            const std::function<void(int)>* fn;
-            {
-                std::unique_lock<std::mutex> lk(m_);
-                cv_.wait(lk, [&] { return stop_ || gen_ != seen; });
-                if (stop_) return;
-                seen = gen_;
-                fn = job_;
-            }
-            drain(*fn);
-            std::lock_guard<std::mutex> lk(m_);
-            if (--running_ == 0) done_cv_.notify_all();
-        }
-    }
-    std::vector<std::thread> workers_;
-    std::mutex busy_, m_;
-    std::condition_variable cv_, done_cv_;
-    const std::function<void(int)>* job_ = nullptr;
-    std::atomic<int> next_{0};
-    int count_ = 0, running_ = 0;
-    uint64_t gen_ = 0;
-    bool stop_ = false;
 };
 
 // Pinned staging for a batch's host -> device uploads.  Every per-batch input
@@ -236,10 +161,18 @@ struct msg_ctx {
     bool profiling = false;
     // msg_gate: this context's stream waits, before stage gate_wait, for the
     // peer's gate event, and records its own after stage gate_rec begins
+    // (gate_peer / gated_by change under g_gate_mu: msg_gate, msg_destroy)
     msg_ctx* gate_peer = nullptr;
+    std::vector<msg_ctx*> gated_by;   // contexts whose gate_peer is this one (cleared at msg_destroy)
     int gate_wait = -1, gate_rec = -1;
     hipEvent_t gate_ev = nullptr;
-    bool gate_armed = false;          // gate_ev recorded at least once
+    std::atomic<bool> gate_armed{false};   // gate_ev recorded at least once (read by the gated context)
+    // the stream of the last batch and an event at its end: a batch enqueued on
+    // another stream first waits for it (the staging arena and the per-batch
+    // buffers are reused in stream order only)
+    hipStream_t last_stream = nullptr;
+    hipEvent_t done_ev = nullptr;
+    bool done_armed = false;
     // stage events: two sets alternate between batches; a set is read (folded
     // into the sums) when it comes round again, two batches later, or at
     // msg_stage_times -- profiling never makes the host wait for the last batch
@@ -248,7 +181,9 @@ struct msg_ctx {
     int ev_cur = 0;
     double stage_sum[10] = {0};   // accumulated stage times since msg_set_profiling(ctx, 1)
     int64_t stage_cnt = 0;
-    double host_sum[3] = {0};     // host wall clock per batch: plan, records, pinned upload
+    // host wall clock per batch: plan, records, pinned upload, then the splits
+    // plan sizes, plan events + tap merge, preset records, event records, lists + buffers
+    double host_sum[8] = {0};
     int64_t host_cnt = 0;
     hipEvent_t ev[2][10] = {};
     bool device_plan = false;     // MSGPU_DEVICE_PLAN=1: plan on the device (k_plan_*), read back
@@ -260,6 +195,7 @@ struct msg_ctx {
     float2* d_fir2tab[5] = {};   // k_fir2 twiddle tables, M = 1024 << i
     float2* d_fir4tab = nullptr; // k_fir4 twiddle tables (M = 16384)
     bool fir4 = true;            // M = 16384 blocks on k_fir4 (MSGPU_FIR4=0: k_fir2, A/B and tests)
+    bool fir8 = true;            // N = 65536 one-partition filters on k_fir8 (MSGPU_FIR8=0: off, A/B and tests)
     // Q <= 2 presets on the streaming k_fir4s (MSGPU_FIR4S=1; off by default: at
     // C3's 24 blocks per preset its H re-reads miss L2 and cancel the saved transforms)
     bool fir4s = false;
@@ -293,7 +229,7 @@ struct msg_ctx {
     DevBuf<float> micro, grain, mono_a, mono_y;
     DevBuf<float2> hspec;
     DevBuf<float> hscratch;                     // h of every FIR preset (k_h_build -> k_fir_h / k_fir4_hpart)
-    Slice<int32_t> h_tile_begin;
+    Slice<int32_t> h_tile_begin, fir8_list;
     Slice<int2> hpart_jobs;
     Slice<int2> fir_jobs;
     Slice<int32_t> spec_ct_list;
@@ -316,6 +252,8 @@ struct msg_ctx {
     DevBuf<int64_t> sf_irjobs;
     DevBuf<double> sf_h;
     DevBuf<float2> sf_hspec, sf_xspec;
+    DevBuf<float> sf_hf;                        // float taps of a k_fir8 filter
+    DevBuf<int32_t> sf_list;
     // odd-length stereo rotation (kernels_stereo_odd.h)
     std::map<int64_t, DevBuf<float2>> so_bp;   // chirp kernel spectra by n
     int so_row = 0, so_col = 0;                // transform-split limits (MSGPU_SO_ROW / _COL, tests; 0 = default)
@@ -505,14 +443,16 @@ static double bessel_j(int m, double x) {
 
 // Choose (N, P, Q) minimising FFT work for an M-tap FIR over n outputs (h is
 // built in the time domain by k_h_build, so any N with P < N qualifies).
+// fir8: also consider N = 65536 with one partition (k_fir8: two half-size
+// transforms per transform of N, P = M).
 // stream: when non-null, also consider k_fir4s (N = 32768, P = B = 16384, Q <= 2:
 // one forward and one inverse transform per block plus, for Q = 2, one forward
 // per workgroup of kblk blocks) and report whether it won.
-static void choose_fir(int64_t M, int64_t n, int& N, int& P, int& Q, bool* stream = nullptr,
+static void choose_fir(int64_t M, int64_t n, int& N, int& P, int& Q, bool fir8, bool* stream = nullptr,
                        int kblk = 1) {
     double best = 1e300;
     N = FIR_NMAX; P = (int)std::min<int64_t>(M, FIR_NMAX / 2); Q = (int)((M + P - 1) / P);
-    for (int lg = 11; lg <= 15; ++lg) {   // k_fir2 sizes: M = N/2 in 1024..16384
+    for (int lg = 11; lg <= 15; ++lg) {   // k_fir2 / k_fir4 sizes: M = N/2 in 1024..16384
         const int NN = 1 << lg;
         for (int q = 1; q <= 64; ++q) {
             const int64_t pp = (M + q - 1) / q;
@@ -522,6 +462,12 @@ static void choose_fir(int64_t M, int64_t n, int& N, int& P, int& Q, bool* strea
             const double cost = (double)blocks * (q + 1) * NN * lg + (double)blocks * NN * 4.0;
             if (cost < best) { best = cost; N = NN; P = (int)pp; Q = q; }
         }
+    }
+    if (fir8 && M < FIR8_N / 2 + FIR8_N / 4) {   // B >= N/4
+        const int64_t B = FIR8_N - M + 1;
+        const int64_t blocks = (n + B - 1) / B;
+        const double cost = (double)blocks * 2 * FIR8_N * 16 + (double)blocks * FIR8_N * 4.0;
+        if (cost < best) { best = cost; N = FIR8_N; P = (int)M; Q = 1; }
     }
     if (stream) {
         *stream = false;
@@ -594,13 +540,31 @@ static int g64_ops(const msg_preset& p, const msg_event& e) {
 
 static void stage_mark(msg_ctx* ctx, int i, hipStream_t s) {
     if (ctx->profiling) hipEventRecord(ctx->ev[ctx->ev_cur][i], s);
+    if (ctx->gate_wait < 0 && ctx->gate_rec < 0) return;
+    std::lock_guard<std::mutex> lk(g_gate_mu);   // the peer may be unlinked by msg_destroy
     if (ctx->gate_peer) {
-        if (i == ctx->gate_wait && ctx->gate_peer->gate_armed) hipStreamWaitEvent(s, ctx->gate_peer->gate_ev, 0);
+        if (i == ctx->gate_wait && ctx->gate_peer->gate_armed.load()) hipStreamWaitEvent(s, ctx->gate_peer->gate_ev, 0);
         if (i == ctx->gate_rec) {
             hipEventRecord(ctx->gate_ev, s);
-            ctx->gate_armed = true;
+            ctx->gate_armed.store(true);
         }
     }
+}
+
+// A batch on a different stream than the context's last one waits for that
+// batch's end (the staging arena and buffers are stream-ordered).
+static hipError_t stream_handover(msg_ctx* ctx, hipStream_t s) {
+    if (ctx->done_armed && s != ctx->last_stream) return hipStreamWaitEvent(s, ctx->done_ev, 0);
+    return hipSuccess;
+}
+static hipError_t stream_done(msg_ctx* ctx, hipStream_t s) {
+    if (!ctx->done_ev) {
+        const hipError_t e = hipEventCreateWithFlags(&ctx->done_ev, hipEventDisableTiming);
+        if (e != hipSuccess) return e;
+    }
+    ctx->last_stream = s;
+    ctx->done_armed = true;
+    return hipEventRecord(ctx->done_ev, s);
 }
 
 // ---------------------------------------------------------------------------
@@ -609,6 +573,8 @@ static void stage_mark(msg_ctx* ctx, int i, hipStream_t s) {
 extern "C" {
 
 int msg_abi_version(void) { return MSG_ABI_VERSION; }
+
+int msg_host_threads(void) { return HostPool::get().threads(); }
 
 int64_t msg_sizeof(int32_t which) {
     switch (which) {
@@ -673,6 +639,7 @@ msg_ctx* msg_create(int device_ordinal) {
         }
     }
     if (const char* e = getenv("MSGPU_FIR4")) ctx->fir4 = e[0] != '0';
+    if (const char* e = getenv("MSGPU_FIR8")) ctx->fir8 = e[0] != '0';
     if (const char* e = getenv("MSGPU_FIR4S")) ctx->fir4s = e[0] == '1';
     if (const char* e = getenv("MSGPU_FIR4S_WGS")) ctx->fir4s_wgs = std::max(1, atoi(e));
     if (const char* e = getenv("MSGPU_FIR4S_K")) ctx->fir4s_kmax = std::max(2, std::min(64, atoi(e)));
@@ -721,10 +688,19 @@ void msg_destroy(msg_ctx* ctx) {
     for (float2* t : ctx->d_spec_ct_tab) hipFree(t);
     hipFree(ctx->d_spec3_tab);
     ctx->sf_prt.release(); ctx->sf_jobs.release(); ctx->sf_irjobs.release(); ctx->sf_h.release();
-    ctx->sf_hspec.release(); ctx->sf_xspec.release();
+    ctx->sf_hspec.release(); ctx->sf_xspec.release(); ctx->sf_hf.release(); ctx->sf_list.release();
     for (auto& set : ctx->ev)
         for (auto& ev : set) hipEventDestroy(ev);
+    {
+        std::lock_guard<std::mutex> lk(g_gate_mu);
+        for (msg_ctx* c : ctx->gated_by) { c->gate_peer = nullptr; c->gate_wait = c->gate_rec = -1; }
+        if (ctx->gate_peer) {
+            auto& v = ctx->gate_peer->gated_by;
+            v.erase(std::remove(v.begin(), v.end(), ctx), v.end());
+        }
+    }
     if (ctx->gate_ev) hipEventDestroy(ctx->gate_ev);
+    if (ctx->done_ev) hipEventDestroy(ctx->done_ev);
     ctx->staging.release();
     ctx->dp_presets.release(); ctx->frag_len.release(); ctx->info.release(); ctx->slot_base.release();
     ctx->tap_base.release(); ctx->dp_events.release(); ctx->dp_er_off.release(); ctx->dp_er_gain.release();
@@ -783,10 +759,16 @@ int msg_gate(msg_ctx* ctx, msg_ctx* peer, int32_t wait_stage, int32_t record_sta
     if (peer && peer->device != ctx->device) return MSG_E_ARG;
     if (peer && !ctx->gate_ev && hipEventCreateWithFlags(&ctx->gate_ev, hipEventDisableTiming) != hipSuccess)
         return fail(ctx, MSG_E_DEVICE, "hipEventCreate failed");
+    std::lock_guard<std::mutex> lk(g_gate_mu);
+    if (ctx->gate_peer) {
+        auto& v = ctx->gate_peer->gated_by;
+        v.erase(std::remove(v.begin(), v.end(), ctx), v.end());
+    }
     ctx->gate_peer = peer;
+    if (peer) peer->gated_by.push_back(ctx);
     ctx->gate_wait = peer ? wait_stage : -1;
     ctx->gate_rec = peer ? record_stage : -1;
-    ctx->gate_armed = false;
+    ctx->gate_armed.store(false);
     return MSG_OK;
 }
 
@@ -796,6 +778,8 @@ int msg_stage_times(msg_ctx* ctx, float* ms, int32_t n) {
     for (int i = 0; i < n && i < 10; ++i)
         ms[i] = ctx->stage_cnt ? (float)(ctx->stage_sum[i] / (double)ctx->stage_cnt) : 0.f;
     for (int i = 10; i < n && i < 13; ++i)
+        ms[i] = ctx->host_cnt ? (float)(ctx->host_sum[i - 10] / (double)ctx->host_cnt) : 0.f;
+    for (int i = 13; i < n && i < 18; ++i)
         ms[i] = ctx->host_cnt ? (float)(ctx->host_sum[i - 10] / (double)ctx->host_cnt) : 0.f;
     return MSG_OK;
 }
@@ -886,8 +870,9 @@ int msg_fir(msg_ctx* ctx, const float* x_dev, float* y_dev, int64_t n, int32_t n
     if (M > (int64_t)64 * (FIR_NMAX - 1)) return fail(ctx, MSG_E_UNSUPPORTED, "FIR longer than 64 partitions");
     HIPCHK(ctx, hipSetDevice(ctx->device));
     hipStream_t s = (hipStream_t)stream;
+    HIPCHK(ctx, stream_handover(ctx, s));
     int N = 0, Pp = 0, Q = 0;
-    choose_fir(M, n, N, Pp, Q);
+    choose_fir(M, n, N, Pp, Q, ctx->fir8);
     // Many partitions: a frequency-domain delay line (fir_fft.h) computes each
     // input segment's spectrum once and reuses it for Q blocks -- two transforms
     // per block of N/2 outputs instead of Q + 1 per block of N - P + 1, for
@@ -904,6 +889,38 @@ int msg_fir(msg_ctx* ctx, const float* x_dev, float* y_dev, int64_t n, int32_t n
     const int64_t blocks = (n + B - 1) / B;
     if (blocks * n_signals > INT32_MAX) return fail(ctx, MSG_E_UNSUPPORTED, "too many output blocks");
     if (fir_shape) { fir_shape[0] = N; fir_shape[1] = Pp; fir_shape[2] = Q; }
+    if (N == FIR8_N) {   // one partition on k_fir8: H from the float taps by k_fir8_hpart
+        std::vector<PresetRt> prt((size_t)n_signals);
+        std::vector<int2> fj;
+        fj.reserve((size_t)(blocks * n_signals));
+        for (int i = 0; i < n_signals; ++i) {
+            PresetRt& r = prt[i];
+            memset(&r, 0, sizeof(r));
+            r.out_n = n;
+            r.y_off = (int64_t)i * n;
+            r.fir_on = 1; r.fir_N = N; r.fir_P = Pp; r.fir_Q = 1; r.fir_B = (int32_t)B;
+            r.h_off = 0; r.hs_off = 0; r.h_len = (int32_t)M;
+            for (int64_t b = 0; b < blocks; ++b) fj.push_back(make_int2(i, (int)b));
+        }
+        std::vector<float> hf((size_t)M);
+        for (int64_t i = 0; i < M; ++i) hf[i] = (float)h[i];
+        const int32_t first = 0;
+        HIPCHK(ctx, ctx->sf_prt.ensure(prt.size()));
+        HIPCHK(ctx, ctx->sf_jobs.ensure(fj.size()));
+        HIPCHK(ctx, ctx->sf_hf.ensure((size_t)M));
+        HIPCHK(ctx, ctx->sf_list.ensure(1));
+        HIPCHK(ctx, ctx->sf_hspec.ensure((size_t)(N / 2 + 1)));
+        HIPCHK(ctx, hipMemcpyAsync(ctx->sf_prt.p, prt.data(), sizeof(PresetRt) * prt.size(), hipMemcpyHostToDevice, s));
+        HIPCHK(ctx, hipMemcpyAsync(ctx->sf_jobs.p, fj.data(), sizeof(int2) * fj.size(), hipMemcpyHostToDevice, s));
+        HIPCHK(ctx, hipMemcpyAsync(ctx->sf_hf.p, hf.data(), sizeof(float) * (size_t)M, hipMemcpyHostToDevice, s));
+        HIPCHK(ctx, hipMemcpyAsync(ctx->sf_list.p, &first, sizeof(int32_t), hipMemcpyHostToDevice, s));
+        HIPCHK(ctx, launch_fir8_hpart(1, s, ctx->sf_prt.p, ctx->sf_list.p, ctx->d_fir4tab, ctx->sf_hf.p,
+                                      ctx->sf_hspec.p));
+        HIPCHK(ctx, launch_fir8((unsigned)fj.size(), s, ctx->sf_prt.p, ctx->sf_jobs.p, ctx->d_fir4tab, ctx->sf_hspec.p,
+                                x_dev, y_dev));
+        HIPCHK(ctx, stream_done(ctx, s));
+        return MSG_OK;
+    }
     std::string why;
     const int fp = real_plan(ctx->fir_plans, N, why);
     if (fp < 0) return fail(ctx, MSG_E_DEVICE, "FIR plan: " + why);
@@ -953,6 +970,7 @@ int msg_fir(msg_ctx* ctx, const float* x_dev, float* y_dev, int64_t n, int32_t n
                                 ctx->sf_hspec.p, x_dev, y_dev));
     // pageable-host H2D copies are staged before hipMemcpyAsync returns (as in
     // msg_render_batch), so the host vectors may go; the FIR runs asynchronously.
+    HIPCHK(ctx, stream_done(ctx, s));
     return MSG_OK;
 }
 
@@ -1006,6 +1024,23 @@ int msg_last_meta(msg_ctx* ctx, int32_t preset, double* micro, double* grain, in
     return MSG_OK;
 }
 
+int msg_last_grain64(msg_ctx* ctx, int32_t preset, int32_t k, double* grain, int64_t cap, int64_t* n) {
+    if (!ctx || !n) return MSG_E_ARG;
+    if (preset < 0 || preset >= ctx->last_n) return fail(ctx, MSG_E_ARG, "bad preset index");
+    const int32_t l64 = ctx->h_last64.empty() ? -1 : ctx->h_last64[preset];
+    const int32_t ne = ctx->h_info[preset].n_events;
+    if (l64 < 0) return fail(ctx, MSG_E_ARG, "preset is not on the float64 chain");
+    if (k < 0 || k >= ne) return fail(ctx, MSG_E_ARG, "bad event index");
+    const Ev64& v = ctx->h_ev64[l64 - (ne - 1) + k];
+    *n = v.n;
+    if (!grain) return MSG_OK;
+    if (v.n > cap) return fail(ctx, MSG_E_ARG, "grain buffer too small");
+    hipSetDevice(ctx->device);
+    HIPCHK(ctx, hipDeviceSynchronize());
+    HIPCHK(ctx, hipMemcpy(grain, ctx->grain64.p + v.off64, v.n * sizeof(double), hipMemcpyDeviceToHost));
+    return MSG_OK;
+}
+
 int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
                      const double* const* irs, const int64_t* ir_lens, int32_t n_irs,
                      const uint8_t* const* images, const int32_t* img_h, const int32_t* img_w,
@@ -1013,6 +1048,7 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
     if (!ctx || !presets || P <= 0 || !out_dev || !out_offsets) return fail(ctx, MSG_E_ARG, "bad arguments");
     hipStream_t s = (hipStream_t)stream;
     HIPCHK(ctx, hipSetDevice(ctx->device));
+    HIPCHK(ctx, stream_handover(ctx, s));
     collect_stage_set(ctx, ctx->ev_cur);   // this batch's event set: from two batches back
     for (int p = 0; p < P; ++p) {
         std::string why;
@@ -1026,6 +1062,7 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
     stage_mark(ctx, 0, s);
     using hclock = std::chrono::steady_clock;
     const auto h0 = hclock::now();
+    auto hA = h0;
     std::vector<int64_t> flen(P, 0);
     for (int p = 0; p < P; ++p) {
         const int f = presets[p].ir_frag;
@@ -1053,6 +1090,7 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
         // no device round trip, so the call returns once the batch is enqueued
         HostPool& pool = HostPool::get();
         pool.run(P, [&](int p) { msgplan::plan_sizes(presets[p], kHostZig, flen[p], info[p]); });
+        hA = hclock::now();
         if (int st = bases()) return st;
         ctx->h_events.resize(nslots);
         ctx->h_er_off.resize(ntaps);
@@ -1061,7 +1099,7 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
             const bool er = (presets[p].flags & MSG_F_ER_CLOUD) != 0;
             msgplan::plan_events(presets[p], kHostZig, flen[p], p, info[p], ctx->h_events.data() + slot_base[p],
                                  er ? ctx->h_er_off.data() + tap_base[p] : nullptr,
-                                 er ? ctx->h_er_gain.data() + tap_base[p] : nullptr);
+                                 er ? ctx->h_er_gain.data() + tap_base[p] : nullptr, true);
         });
 
     } else {
@@ -1118,26 +1156,29 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
             const int nt = std::max(1, presets[p].er_taps);
             int32_t* off = ctx->h_er_off.data() + tap_base[p];
             double* g = ctx->h_er_gain.data() + tap_base[p];
-            std::vector<int> ix(nt);
-            for (int k = 0; k < nt; ++k) ix[k] = k;
-            std::stable_sort(ix.begin(), ix.end(), [&](int a, int b) { return off[a] < off[b]; });
-            std::vector<int32_t> o2;
-            std::vector<double> g2;
-            o2.reserve(nt);
-            g2.reserve(nt);
+            // (offset, tap index) packed in one key: a plain sort is the stable sort by offset
+            thread_local std::vector<uint64_t> key;
+            thread_local std::vector<double> g0;
+            key.resize(nt);
+            g0.assign(g, g + nt);
             const int64_t n = info[p].out_n;
-            for (int i = 0; i < nt;) {
+            int m = 0;
+            for (int k = 0; k < nt; ++k)
+                if (off[k] > 0 && off[k] < n) key[m++] = ((uint64_t)(uint32_t)off[k] << 32) | (uint32_t)k;
+            std::sort(key.begin(), key.begin() + m);
+            int live = 0;
+            for (int i = 0; i < m;) {
+                const uint32_t o = (uint32_t)(key[i] >> 32);
+                double acc = g0[(uint32_t)key[i]];
                 int j = i + 1;
-                while (j < nt && off[ix[j]] == off[ix[i]]) ++j;
-                double acc = g[ix[i]];
-                for (int u = i + 1; u < j; ++u) acc += g[ix[u]];
-                if (off[ix[i]] > 0 && off[ix[i]] < n) { o2.push_back(off[ix[i]]); g2.push_back(acc); }
+                for (; j < m && (uint32_t)(key[j] >> 32) == o; ++j) acc += g0[(uint32_t)key[j]];
+                off[live] = (int32_t)o;
+                g[live] = acc;
+                ++live;
                 i = j;
             }
-            std::copy(o2.begin(), o2.end(), off);
-            std::copy(g2.begin(), g2.end(), g);
-            n_taps_live[p] = (int32_t)o2.size();
-            tap_max[p] = o2.empty() ? 0 : o2.back();
+            n_taps_live[p] = live;
+            tap_max[p] = live ? off[live - 1] : 0;
         };
         if (ctx->device_plan) for (int p = 0; p < P; ++p) merge(p);
         else HostPool::get().run(P, merge);
@@ -1159,6 +1200,12 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
         ctx->h_ert_cap = (size_t)nslots + nslots / 4;
     }
     EventRt* const ert = ctx->h_ert.get();
+    // slots a preset reserves beyond its events are never written below: zero them
+    // so the whole uploaded range is defined
+    for (int p = 0; p < P; ++p)
+        if (info[p].n_slots > info[p].n_events)
+            memset(ert + slot_base[p] + info[p].n_events, 0,
+                   sizeof(EventRt) * (size_t)(info[p].n_slots - info[p].n_events));
     std::vector<int32_t> gen_list, spec_small, spec_big, tile_begin(P), fir_begin(P), h_begin(P), st_begin(P),
         fir_plan_of(P, 0);
     std::vector<double> irbank;
@@ -1186,7 +1233,8 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
     const bool stop_cep = stop_env && std::strcmp(stop_env, "cep") == 0;
     std::vector<int32_t> spec3;                           // events of the band-pruned kernel
     std::vector<int32_t> f32_presets;                     // presets on the float32 chain
-    std::vector<int2> fjobs_by[6];                        // FIR output blocks per transform size; [5]: k_fir4s
+    std::vector<int2> fjobs_by[7];                        // FIR output blocks per transform size; [5]: k_fir4s, [6]: k_fir8
+    std::vector<int32_t> fir8_list;                       // presets on k_fir8 (N = 65536)
     std::vector<int2> fir4s_presets;                      // (preset, blocks) on the streaming FIR
     // float64 grain chain records
     std::vector<Ev64> ev64;
@@ -1235,6 +1283,22 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
         fir4s_k = (int)std::min<int64_t>(ctx->fir4s_kmax, total / std::max(1, ctx->fir4s_wgs));
         fir4s_ok = fir4s_k >= 2;
     }
+    // the per-preset pure functions of the records (FIR partitioning, stereo
+    // Bessel taps) in parallel; the loop below does the prefix bookkeeping
+    struct FirPick { int64_t M; int N, P, Q; bool stream; float bess[25]; };
+    std::vector<FirPick> pick(P);
+    HostPool::get().run(P, [&](int p) {
+        FirPick& f = pick[p];
+        f.M = h_taps(p);
+        f.N = f.P = f.Q = 0;
+        f.stream = false;
+        if (f.M > 0) choose_fir(f.M, info[p].out_n, f.N, f.P, f.Q, ctx->fir8, fir4s_ok ? &f.stream : nullptr, fir4s_k);
+        const double w = std::min(std::max(presets[p].stereo_width, 0.0), 1.0);
+        for (int m = -12; m <= 12; ++m) {
+            const double j = bessel_j(std::abs(m), w * 0.9);
+            f.bess[m + 12] = (float)((m < 0 && (m & 1)) ? -j : j);
+        }
+    });
     for (int p = 0; p < P; ++p) {
         const msg_preset& pr = presets[p];
         const msg_plan_info& inf = info[p];
@@ -1293,15 +1357,16 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
         r.h_block_begin = hblocks;
         r.h_fir4 = 0;
         if (r.fir_on) {
-            const int64_t M = h_taps(p);
-            int N, Pp, Q;
-            bool stream = false;
-            choose_fir(M, inf.out_n, N, Pp, Q, fir4s_ok ? &stream : nullptr, fir4s_k);
-            std::string why;
-            const int fp = real_plan(ctx->fir_plans, N, why);
-            if (fp < 0) return fail(ctx, MSG_E_DEVICE, "FIR plan: " + why);
-            fir_plan_of[p] = fp;
-            fir_lds = std::max(fir_lds, ctx->fir_plans.host[fp].lds_bytes);
+            const int64_t M = pick[p].M;
+            const int N = pick[p].N, Pp = pick[p].P, Q = pick[p].Q;
+            const bool stream = pick[p].stream;
+            if (N != FIR8_N) {                     // runtime plan for k_fir_h (k_fir8 has its own engine)
+                std::string why;
+                const int fp = real_plan(ctx->fir_plans, N, why);
+                if (fp < 0) return fail(ctx, MSG_E_DEVICE, "FIR plan: " + why);
+                fir_plan_of[p] = fp;
+                fir_lds = std::max(fir_lds, ctx->fir_plans.host[fp].lds_bytes);
+            }
             r.fir_N = N; r.fir_P = Pp; r.fir_Q = Q; r.fir_B = stream ? Pp : N - Pp + 1;
             r.h_off = hsum;
             r.h_len = (int32_t)M;
@@ -1309,7 +1374,10 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
             hs_sum += (M + 3) & ~int64_t(3);    // 16-byte aligned h regions
             h_tile_begin[p] = htiles;
             htiles += (int32_t)((M + H_BUILD_TILE - 1) / H_BUILD_TILE);
-            if (N == 2 * 16384 && ctx->fir4) {   // the C3/C4 size: k_fir4_hpart
+            if (N == FIR8_N) {                     // k_fir8_hpart (one partition)
+                r.h_fir4 = 2;
+                fir8_list.push_back(p);
+            } else if (N == 2 * 16384 && ctx->fir4) {   // k_fir4_hpart
                 r.h_fir4 = 1;
                 for (int q = 0; q < Q; ++q) hpart_jobs.push_back(make_int2(p, q));
             }
@@ -1317,7 +1385,7 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
             if (stream) {
                 fir4s_presets.push_back(make_int2(p, nblk));   // jobs cut once the batch's total is known
             } else {
-                std::vector<int2>& fj = fjobs_by[__builtin_ctz(N) - 11];
+                std::vector<int2>& fj = fjobs_by[N == FIR8_N ? 6 : __builtin_ctz(N) - 11];
                 for (int32_t b = 0; b < nblk; ++b) fj.push_back(make_int2(p, b));
             }
             fblocks += nblk;
@@ -1345,10 +1413,7 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
         }
         r.dl = (int32_t)std::nearbyint((1 + 7 * w) * 0.0005 * sr);
         r.dr = (int32_t)std::nearbyint((1 + 9 * w) * 0.0007 * sr);
-        for (int m = -12; m <= 12; ++m) {
-            const double j = bessel_j(std::abs(m), w * 0.9);
-            r.bess[m + 12] = (float)((m < 0 && (m & 1)) ? -j : j);
-        }
+        std::memcpy(r.bess, pick[p].bess, sizeof(r.bess));
         r.drive = (float)pr.sat_drive;
         r.peak = (float)pr.peak;
         st_begin[p] = stiles;
@@ -1454,6 +1519,7 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
         }
         f32_presets.push_back(p);
     }
+    const auto hB = hclock::now();
     // ---- float32-chain event records (EventRt), presets in parallel on the host
     // pool; the per-kernel event lists are concatenated in preset order.  Events
     // that need a runtime FFT plan (no compile-time plan for their length) are
@@ -1522,6 +1588,7 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
             }
         }
     }
+    const auto hC = hclock::now();
     HIPCHK(ctx, sync_plans(ctx->grain_plans, s));
     HIPCHK(ctx, sync_plans(ctx->fir_plans, s));
     HIPCHK(ctx, sync_plans(ctx->plans64, s));
@@ -1561,12 +1628,12 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
     for (const int2& pb : fir4s_presets)
         for (int32_t b = 0; b < pb.y; b += fir4s_k) fjobs_by[5].push_back(make_int2(pb.x, b));
     std::vector<int2> fir_jobs;
-    int32_t fjob_off[7] = {0};
-    for (int i = 0; i < 6; ++i) {
+    int32_t fjob_off[8] = {0};
+    for (int i = 0; i < 7; ++i) {
         fjob_off[i] = (int32_t)fir_jobs.size();
         fir_jobs.insert(fir_jobs.end(), fjobs_by[i].begin(), fjobs_by[i].end());
     }
-    fjob_off[6] = (int32_t)fir_jobs.size();
+    fjob_off[7] = (int32_t)fir_jobs.size();
     HIPCHK(ctx, ctx->micro.ensure(pool));
     HIPCHK(ctx, ctx->grain.ensure(pool));
     HIPCHK(ctx, ctx->mono_a.ensure(ysum));
@@ -1601,6 +1668,7 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
     HIPCHK(ctx, h2d(&ctx->fir_plan_of.p, fir_plan_of.data(), sizeof(int32_t) * P));
     HIPCHK(ctx, h2d(&ctx->irbank.p, irbank.data(), sizeof(double) * irbank.size()));
     HIPCHK(ctx, h2d(&ctx->h_tile_begin.p, h_tile_begin.data(), sizeof(int32_t) * P));
+    HIPCHK(ctx, h2d(&ctx->fir8_list.p, fir8_list.data(), sizeof(int32_t) * fir8_list.size()));
     HIPCHK(ctx, h2d(&ctx->hpart_jobs.p, hpart_jobs.data(), sizeof(int2) * hpart_jobs.size()));
     HIPCHK(ctx, hipMemsetAsync(ctx->maxbits.p, 0, sizeof(unsigned) * P, s));
     HIPCHK(ctx, h2d(&ctx->ev64.p, ev64.data(), sizeof(Ev64) * ev64.size()));
@@ -1616,6 +1684,11 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
         ctx->host_sum[0] += std::chrono::duration<double, std::milli>(h1 - h0).count();
         ctx->host_sum[1] += std::chrono::duration<double, std::milli>(h2 - h1).count();
         ctx->host_sum[2] += std::chrono::duration<double, std::milli>(h3 - h2).count();
+        ctx->host_sum[3] += std::chrono::duration<double, std::milli>(hA - h0).count();
+        ctx->host_sum[4] += std::chrono::duration<double, std::milli>(h1 - hA).count();
+        ctx->host_sum[5] += std::chrono::duration<double, std::milli>(hB - h1).count();
+        ctx->host_sum[6] += std::chrono::duration<double, std::milli>(hC - hB).count();
+        ctx->host_sum[7] += std::chrono::duration<double, std::milli>(h2 - hC).count();
         ++ctx->host_cnt;
     }
 
@@ -1681,14 +1754,20 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
         if (!hpart_jobs.empty())
             HIPCHK(ctx, launch_fir4_hpart(16384, (unsigned)hpart_jobs.size(), s, ctx->prt.p, ctx->hpart_jobs.p,
                                           ctx->d_fir4tab, ctx->hscratch.p, ctx->hspec.p));
-        if (hblocks_gen > 0)   // blocks of k_fir4-engine presets return at once
+        if (!fir8_list.empty())
+            HIPCHK(ctx, launch_fir8_hpart((unsigned)fir8_list.size(), s, ctx->prt.p, ctx->fir8_list.p, ctx->d_fir4tab,
+                                          ctx->hscratch.p, ctx->hspec.p));
+        if (hblocks_gen > 0)   // blocks of k_fir4/k_fir8-engine presets return at once
             HIPCHK(ctx, launch_fir_h((unsigned)hblocks, fir_lds, s, ctx->prt.p, ctx->h_begin.p, P,
                                      ctx->fir_plans.dev.p, ctx->fir_plan_of.p, ctx->hscratch.p, ctx->hspec.p));
         stage_mark(ctx, 8, s);
-        for (int i = 0; i < 6; ++i) {
+        for (int i = 0; i < 7; ++i) {
             if (fjob_off[i + 1] <= fjob_off[i]) continue;
             const unsigned nj = (unsigned)(fjob_off[i + 1] - fjob_off[i]);
-            if (i == 5)
+            if (i == 6)
+                HIPCHK(ctx, launch_fir8(nj, s, ctx->prt.p, ctx->fir_jobs.p + fjob_off[i], ctx->d_fir4tab, ctx->hspec.p,
+                                        ctx->mono_a.p, ctx->mono_y.p));
+            else if (i == 5)
                 HIPCHK(ctx, launch_fir4s(16384, nj, s, ctx->prt.p, ctx->fir_jobs.p + fjob_off[i], ctx->d_fir4tab,
                                          ctx->hspec.p, ctx->mono_a.p, ctx->mono_y.p, fir4s_k));
             else if (i == 4 && ctx->fir4)
@@ -1727,6 +1806,7 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
                        yb, ctx->so_r2.p, ctx->maxbits.p, out_dev);
     HIPCHK(ctx, hipGetLastError());
     stage_mark(ctx, 7, s);
+    HIPCHK(ctx, stream_done(ctx, s));
     ctx->h_info = info;
     ctx->h_prt = prt;
     ctx->h_slot_base = slot_base;

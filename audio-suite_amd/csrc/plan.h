@@ -180,10 +180,13 @@ MSG_HD void sort_by_time(msg_event* ev, int32_t n) {
 }
 
 // Phase 2: fill ev[0..n_slots) (times, then per-event fields for the first
-// n_events), exact pool offsets, and the ER taps.
+// n_events), exact pool offsets, and the ER taps.  sizes_known: info already
+// holds this preset's plan_sizes (the host batch path runs phase 1 for every
+// preset first); otherwise phase 1 runs here.
 MSG_HD void plan_events(const msg_preset& p, const Zig& z, int64_t ir_frag_len, int32_t preset_index,
-                        msg_plan_info& info, msg_event* ev, int32_t* er_off, double* er_gain) {
-    plan_sizes(p, z, ir_frag_len, info);   // cheap; keeps both phases consistent
+                        msg_plan_info& info, msg_event* ev, int32_t* er_off, double* er_gain,
+                        bool sizes_known = false) {
+    if (!sizes_known) plan_sizes(p, z, ir_frag_len, info);
     int32_t k = 0;
     const bool ordered = time_order_is_generation_order(p);
     const int32_t cap = p.max_grains;

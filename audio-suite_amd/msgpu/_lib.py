@@ -82,6 +82,7 @@ class MsgPlanInfo(C.Structure):
 # name -> (restype, argtypes)
 _PROTOS = {
     "msg_abi_version": (C.c_int, []),
+    "msg_host_threads": (C.c_int, []),
     "msg_sizeof": (C.c_int64, [C.c_int32]),
     "msg_create": (C.c_void_p, [C.c_int]),
     "msg_destroy": (None, [C.c_void_p]),
@@ -99,6 +100,8 @@ _PROTOS = {
                                   C.POINTER(C.c_int32)]),
     "msg_last_meta": (C.c_int, [C.c_void_p, C.c_int32, C.POINTER(C.c_double), C.POINTER(C.c_double),
                                 C.c_int64, C.POINTER(C.c_int64)]),
+    "msg_last_grain64": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32, C.POINTER(C.c_double), C.c_int64,
+                                   C.POINTER(C.c_int64)]),
     "msg_set_profiling": (C.c_int, [C.c_void_p, C.c_int32]),
     "msg_gate": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.c_int32]),
     "msg_stage_times": (C.c_int, [C.c_void_p, C.POINTER(C.c_float), C.c_int32]),

@@ -55,10 +55,11 @@ class Engine:
         peer's latest batch to begin.  ``peer=None`` clears the gate."""
         L.check(L.lib().msg_gate(self._ctx, peer._ctx if peer is not None else None, int(wait_stage),
                                  int(record_stage)), self._ctx)
+        self._gate_peer = peer      # the peer context stays alive while this one gates on it
 
     def stage_times(self):
-        arr = (C.c_float * 13)()
-        L.check(L.lib().msg_stage_times(self._ctx, arr, 13), self._ctx)
+        arr = (C.c_float * 18)()
+        L.check(L.lib().msg_stage_times(self._ctx, arr, 18), self._ctx)
         return list(arr)
 
     def alloc_output(self, packed: PackedBatch):
@@ -148,6 +149,15 @@ class Engine:
         arr = (L.MsgEvent * max(n.value, 1))()
         L.check(L.lib().msg_last_events(self._ctx, preset, arr, n.value, C.byref(n)), self._ctx)
         return list(arr)[:n.value]
+
+    def last_grain64(self, preset: int, k: int):
+        """Float64 grain of event k of a float64-chain preset of the last batch."""
+        n = C.c_int64(0)
+        L.check(L.lib().msg_last_grain64(self._ctx, preset, k, None, 0, C.byref(n)), self._ctx)
+        g = np.zeros(max(n.value, 1), dtype=np.float64)
+        L.check(L.lib().msg_last_grain64(self._ctx, preset, k, g.ctypes.data_as(C.POINTER(C.c_double)), n.value,
+                                         C.byref(n)), self._ctx)
+        return g[:n.value].copy()
 
     def last_meta(self, preset: int, cap: int):
         micro = np.zeros(max(cap, 1), dtype=np.float64)

@@ -49,10 +49,13 @@ PROFILES = os.path.join(REPO, "profiles")
 STAGE_KERNEL = {"generate": ("k_gen_normal",), "spectral": ("k_spec3", "k_spectral"), "overlap_add": ("k_ola_env",),
                 "fir_kernel": ("k_fir4<", "k_fir2<"), "stereo": ("k_stereo_max", "k_stereo_out")}
 STAGE_NAMES = ["plan", "host_prep", "generate", "spectral", "overlap_add", "fir", "stereo", "total",
-               "fir_kernel", "fir_h", "host_plan_wall", "host_records_wall", "host_upload_wall"]
+               "fir_kernel", "fir_h", "host_plan_wall", "host_records_wall", "host_upload_wall",
+               "host_plan_sizes", "host_plan_events", "host_preset_records", "host_event_records", "host_lists"]
 KERNEL_STAGES = ["generate", "spectral", "overlap_add", "fir_kernel", "stereo"]
-# host cores of the GPU box available to one job (its CPU share; nproc shows the machine)
-BOX_CORES = 16
+# host cores one GPU's rank uses at most (the GPU box's CPU share per GPU; nproc
+# shows the whole machine).  The rank's actual set is its slice of the process
+# affinity (pin_rank_cpus).
+CORES_PER_GPU = 16
 
 # Per-GPU batch of each config (BASELINE.json configs: C2 batch 1; C3 1024 on one
 # GPU; C4 4096 and C5 8192 across 8 GPUs = 512 and 1024 per GPU) and the presets
@@ -149,7 +152,7 @@ def cpu_baseline(cfg, budget_s):
     import multiprocessing as mp
     done, frames, dt = _cpu_worker((cfg, 1000, 1, budget_s))
     single = frames / dt / 1e6
-    procs = max(1, min(BOX_CORES, len(os.sched_getaffinity(0))))
+    procs = max(1, min(CORES_PER_GPU, len(os.sched_getaffinity(0))))
     ctx = mp.get_context("fork")
     t0 = time.perf_counter()
     with ctx.Pool(procs) as pool:
@@ -202,6 +205,27 @@ def dropin_latency(cpu, reps=5):
             rec["speedup"] = round(c / rec["gpu_ms"], 1)
         out[cfg] = rec
     return out
+
+
+def pin_rank_cpus(local, local_world):
+    """Before the first GPU call: pin this rank to its own contiguous slice of the
+    process's CPU affinity (one host worker pool per GPU; on
+    a node whose GPUs 0..3 / 4..7 hang off NUMA nodes 0 / 1 the contiguous slices
+    follow the NUMA split) and size the library's host pool to the slice
+    (MSGPU_HOST_THREADS, at most CORES_PER_GPU).  Returns the slice."""
+    cpus = sorted(os.sched_getaffinity(0))
+    if local_world > 1 and len(cpus) >= local_world:
+        per = len(cpus) // local_world
+        cpus = cpus[local * per:(local + 1) * per]
+        os.sched_setaffinity(0, cpus)
+    cpus = cpus[:max(1, min(len(cpus), CORES_PER_GPU))] if local_world > 1 else cpus
+    os.environ.setdefault("MSGPU_HOST_THREADS", str(max(1, min(len(cpus), CORES_PER_GPU))))
+    return cpus
+
+
+def host_threads():
+    from msgpu import _lib as L
+    return int(L.lib().msg_host_threads())
 
 
 def rank_seeds(rank, batch):
@@ -335,7 +359,7 @@ class GpuRunner:
     plans one sub-batch while the device runs another and their kernels share
     the CUs."""
 
-    def __init__(self, dev, streams, gate=None):
+    def __init__(self, dev, streams, gate=None, threaded=True):
         import torch
         from msgpu.engine import Engine
         self.torch = torch
@@ -344,6 +368,13 @@ class GpuRunner:
         self.engs = [Engine(dev) for _ in range(streams)]
         self.streams = [torch.cuda.Stream(device=dev) for _ in range(streams)]
         self.set_gate(gate)
+        # one enqueueing host thread per context: the host plans / records / uploads
+        # of the contexts' sub-batches overlap (ctypes drops the GIL in the library,
+        # whose host pool runs the callers' jobs side by side)
+        self.pool = None
+        if threaded and streams > 1:
+            from concurrent.futures import ThreadPoolExecutor
+            self.pool = ThreadPoolExecutor(max_workers=streams, thread_name_prefix="msgpu-enqueue")
 
     def set_gate(self, gate):
         """msg_gate between the contexts: each waits for the previous one's stage
@@ -362,8 +393,16 @@ class GpuRunner:
 
     def step(self, w: Workload):
         S = len(self.engs)
-        for i, (p, o) in enumerate(zip(w.subs, w.outs)):
-            self.engs[i % S].render_packed(p, o, self.streams[i % S])
+        if self.pool is None:
+            for i, (p, o) in enumerate(zip(w.subs, w.outs)):
+                self.engs[i % S].render_packed(p, o, self.streams[i % S])
+            return
+
+        def run(e):
+            for i in range(e, len(w.subs), S):
+                self.engs[e].render_packed(w.subs[i], w.outs[i], self.streams[e])
+        for f in [self.pool.submit(run, e) for e in range(min(S, len(w.subs)))]:
+            f.result()
 
     def sync(self):
         self.torch.cuda.synchronize(self.dev)
@@ -543,6 +582,8 @@ def parse():
                          "runs beside that sub-batch's FIR and stereo passes rather than its spectral kernel "
                          "(C3: 9.43-9.45 vs 9.52-9.54 ms per step ungated, profiles/r02ze_gate.txt)")
     ap.add_argument("--iso-steps", type=int, default=3, help="single-stream renders for roofline_isolated")
+    ap.add_argument("--enqueue", choices=["threads", "serial"], default="threads",
+                    help="enqueue the contexts' sub-batches from one host thread each (threads) or in turn")
     ap.add_argument("--points", default="H48,C4,C5",
                     help="secondary configs timed after the headline (comma list, '' = none)")
     ap.add_argument("--point-steps", type=int, default=3)
@@ -603,6 +644,8 @@ def main():
         sys.exit(launch(args))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
+    cpus = pin_rank_cpus(local, local_world)
     cfg = args.config
     batch = default_batch(cfg, args)
     seeds = rank_seeds(rank, batch)
@@ -613,12 +656,12 @@ def main():
     comm = Comm(rank, world)
     try:
         if args.dry_run:
-            return dry_main(args, comm, cfg, seeds, local)
+            return dry_main(args, comm, cfg, seeds, local, cpus)
         irs = load_irs()
         with open(os.path.join(REPO, "tests", "golden", "golden_info.json")) as f:
             golden = json.load(f)["summaries"]
         gate = None if args.gate in ("", "none") else tuple(int(v) for v in args.gate.split(","))
-        runner = GpuRunner(local, max(1, args.streams), gate)
+        runner = GpuRunner(local, max(1, args.streams), gate, threaded=args.enqueue == "threads")
         head = measure(runner, cfg, seeds, default_sub(cfg, args, batch), args.steps, args.warmup, comm, irs,
                        golden, iso_steps=args.iso_steps)
         points = {}
@@ -630,6 +673,7 @@ def main():
                                  1, comm, irs, golden)
         lat = dropin_latency(cpu) if (rank == 0 and world == 1 and not args.no_cpu) else None
         ranks = comm.gather({"rank": rank, "pid": os.getpid(), "device": local,
+                             "cpus": [cpus[0], cpus[-1], len(cpus)], "host_threads": host_threads(),
                              "seeds": [seeds[0], seeds[-1]], "elapsed_s": round(head["_rank_s"], 6),
                              "frames": head["frames_per_gpu_step"] * args.steps})
         if rank == 0:
@@ -647,7 +691,7 @@ def main():
                            "design_samples_per_gpu_step": head["design_samples_per_gpu_step"],
                            "sub_batches_per_gpu": head["sub_batches"],
                            "parallelism": f"preset-sharded x{world}", "streams_per_gpu": len(runner.engs),
-                           "stream_gate": args.gate},
+                           "stream_gate": args.gate, "enqueue": args.enqueue},
                 "roofline": head["roofline"], "roofline_isolated": head.get("roofline_isolated"),
                 "stage_ms": head["stage_ms"], "stage_algorithmic_GBs": head["stage_algorithmic_GBs"],
                 "design_msamples_per_s": head["design_msamples_per_s"],
@@ -662,7 +706,7 @@ def main():
         comm.close()
 
 
-def dry_main(args, comm, cfg, seeds, local):
+def dry_main(args, comm, cfg, seeds, local, cpus):
     """The launcher path with the device work stubbed (CPU tests): same seeds,
     same timing protocol, per-rank record; prints a 'dry_run' line, no metric."""
     from msgpu.pack import PackedBatch
@@ -673,6 +717,7 @@ def dry_main(args, comm, cfg, seeds, local):
     frames = PackedBatch([msgpu.config_params(cfg, seed=s, irs=irs) for s in seeds]).total_frames
     mine, elapsed = timed(runner, w, args.steps, args.warmup, comm)
     ranks = comm.gather({"rank": comm.rank, "pid": os.getpid(), "device": local, "seeds": seeds,
+                         "cpus": sorted(os.sched_getaffinity(0)), "host_threads": host_threads(),
                          "elapsed_s": mine, "frames": frames * args.steps})
     if comm.rank == 0:
         total = sum(r["frames"] for r in ranks)

@@ -105,6 +105,9 @@ enum msg_status { MSG_OK = 0, MSG_E_VALUE = 1 /* ValueError */, MSG_E_UNSUPPORTE
 typedef struct msg_ctx msg_ctx;
 
 int         msg_abi_version(void);
+/* Threads of the process-wide host planning pool (the caller included):
+ * MSGPU_HOST_THREADS, else the CPU affinity / LOCAL_WORLD_SIZE, at most 16. */
+int         msg_host_threads(void);
 /* sizeof of the ABI structs (0 msg_preset, 1 msg_event, 2 msg_plan_info) for binding checks */
 int64_t     msg_sizeof(int32_t which);
 msg_ctx*    msg_create(int device_ordinal);
@@ -145,6 +148,12 @@ int msg_last_events(msg_ctx* ctx, int32_t preset, msg_event* events, int32_t cap
 int msg_last_meta(msg_ctx* ctx, int32_t preset, double* micro, double* grain,
                   int64_t cap, int64_t* n);
 
+/* Float64-chain presets: the float64 grain of event k of preset i of the last
+ * batch as the grain chain left it (before feedback / imprint, MS:729; under
+ * MSGPU_G64_STOP=cep the input of cepstral_warp, MS:696-697), for the per-event
+ * stage pins.  MSG_E_ARG for a float32-chain preset or k out of range. */
+int msg_last_grain64(msg_ctx* ctx, int32_t preset, int32_t k, double* grain, int64_t cap, int64_t* n);
+
 /* Device time of each stage in ms (HIP events on the batch's stream),
  * averaged over the batches rendered since msg_set_profiling(ctx, 1):
  * [0] device plan + read-back, [1] host prep + uploads, [2] generate,
@@ -152,7 +161,9 @@ int msg_last_meta(msg_ctx* ctx, int32_t preset, double* micro, double* grain,
  * [5] FIR (h build + FIR), [6] stereo+clip+normalise, [7] total,
  * [8] the FIR kernel alone, [9] the h build (IR spectra + h spectra);
  * with n >= 13 also the host wall clock per batch: [10] plan (host pool),
- * [11] runtime records, [12] pinned staging + upload enqueue.
+ * [11] runtime records, [12] pinned staging + upload enqueue; host splits:
+ * [13] plan sizes, [14] plan events + ER tap merge, [15] preset records,
+ * [16] event records, [17] lists, buffers and staging adds.
  * Events are read lazily, so profiling does not block the host.             */
 int msg_set_profiling(msg_ctx* ctx, int32_t on);
 int msg_stage_times(msg_ctx* ctx, float* ms, int32_t n);

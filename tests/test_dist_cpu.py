@@ -96,6 +96,18 @@ def test_launcher_two_ranks_dry_run():
     assert d["elapsed_max_s"] == pytest.approx(max(r["elapsed_s"] for r in ranks), rel=0.05)
     assert ranks[0]["elapsed_s"] < d["elapsed_max_s"] + 1e-9
     assert d["value"] == pytest.approx(2 * 4 * 3 * 192000 / d["elapsed_max_s"] / 1e6)
+    _check_rank_cpus(ranks)
+
+
+def _check_rank_cpus(ranks):
+    """Each rank runs on its own slice of the CPUs with a host pool sized to it."""
+    have = len(os.sched_getaffinity(0))
+    sets = [set(r["cpus"]) for r in ranks]
+    if have >= len(ranks):
+        assert not set.intersection(*sets), sets                        # disjoint
+        assert all(len(c) == have // len(ranks) for c in sets), sets
+    for r in ranks:
+        assert 1 <= r["host_threads"] <= min(16, max(1, len(r["cpus"]))), r
 
 
 def test_torchrun_two_ranks_dry_run():
@@ -118,6 +130,7 @@ def test_torchrun_two_ranks_dry_run():
     assert len({q["pid"] for q in ranks}) == 2
     assert [s for q in ranks for s in q["seeds"]] == list(range(1000, 1004))
     assert d["elapsed_max_s"] == pytest.approx(max(q["elapsed_s"] for q in ranks), rel=0.05)
+    _check_rank_cpus(ranks)
 
 
 def test_launcher_one_rank_dry_run():

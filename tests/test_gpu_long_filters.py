@@ -146,3 +146,48 @@ def test_h48_metric_point(msgpu, irs, extra_renders, golden_extra):
         assert abs(float(np.sqrt(np.mean(a64 ** 2))) - g["rms"]) <= RMS_TOL, name
         assert abs(float(a64[:, 0].sum()) - g["sum_l"]) <= RMS_TOL * n, name
         assert abs(float(a64[:, 1].sum()) - g["sum_r"]) <= RMS_TOL * n, name
+
+
+def test_fir8_kernel_agrees(msgpu, irs, full_renders):
+    """One-partition filters of 12 k .. 45 k taps run on k_fir8 (N = 65 536, two
+    half-size transforms on the k_fir4 engine); MSGPU_FIR8=0 puts them back on
+    k_fir4 (N = 32 768, two partitions).  Both match the reference / oracle, and
+    each other to float32 rounding: C3 (25 473 taps), the 192 kHz ER + IR case,
+    an IR-only and an ER-only filter."""
+    import os
+    import torch
+    from oracle import msound_oracle as O
+    from msgpu.engine import Engine
+    from msgpu.pack import PackedBatch
+    base = dict(gen_mode="Resonant strike", event_process="Poisson", _ir_audio=irs["tiny_room_ir"])
+    params = [msgpu.config_params("C3", seed=1001, irs=irs, out_dur_s=0.25),
+              msgpu.merged(base, base_sr=192000, out_dur_s=0.6826, space_ir_on=True, seed=21, er_cloud_on=True,
+                           space_ir_max_samps=8192),
+              msgpu.merged(base, base_sr=384000, out_dur_s=0.2, space_ir_on=True, seed=5, er_cloud_on=True,
+                           er_max_ms=90.0, space_ir_max_samps=8192),
+              msgpu.merged(base, base_sr=384000, out_dur_s=0.3, space_ir_on=False, seed=6, er_cloud_on=True,
+                           er_max_ms=60.0)]
+    packed = PackedBatch(params)
+    outs = {}
+    for flag in ("1", "0"):
+        os.environ["MSGPU_FIR8"] = flag
+        try:
+            eng = Engine(0)
+        finally:
+            os.environ.pop("MSGPU_FIR8", None)
+        o = eng.render_packed(packed)
+        torch.cuda.synchronize(0)
+        outs[flag] = o.cpu().numpy()
+    off0, n0 = int(packed.offsets[0]), int(packed.out_n[0])
+    for flag in outs:
+        e = rms(outs[flag][off0:off0 + n0], full_renders["C3s1001_audio"])
+        print(f"C3 seed 1001 [MSGPU_FIR8={flag}]: rms err vs reference {e:.3e}")
+        assert e <= RMS_TOL
+    for i, p in enumerate(params):
+        ref, _ = O.render(p)
+        off, n = int(packed.offsets[i]), int(packed.out_n[i])
+        for flag in outs:
+            e = rms(outs[flag][off:off + n], ref)
+            print(f"case {i} [MSGPU_FIR8={flag}]: rms err vs oracle {e:.3e}")
+            assert e <= RMS_TOL, (i, flag)
+    assert rms(outs["0"], outs["1"]) <= RMS_TOL

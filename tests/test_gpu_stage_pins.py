@@ -80,3 +80,49 @@ def test_pins_cover_the_spread_presets():
     names = {k.rsplit("_", 1)[0] for k in z.files if k != "info"}
     held = {k for k, v in spread.items() if 1.5 * v > 1e-5}        # the presets held to the spread
     assert held <= names, held - names
+
+
+# ---- every event (round 3): tests/golden/stage_pins_all.npz holds every call's input
+@pytest.fixture(scope="module")
+def pins_all():
+    return np.load(os.path.join(GOLDEN, "stage_pins_all.npz"))
+
+
+def _per_event(name, stage, golden_info, irs, full_renders, pins_all):
+    """Device float64 grain of every event vs the reference's input to `stage` in
+    the same call order; returns the relative errors."""
+    import torch
+    from msgpu.engine import default_engine
+    from msgpu.pack import PackedBatch
+    lens = pins_all[f"{name}_{stage}_lens"]
+    data = pins_all[f"{name}_{stage}_data"]
+    eng = default_engine(0)
+    eng.render_packed(PackedBatch([_preset(name, golden_info, irs, full_renders)]))
+    torch.cuda.synchronize(0)
+    assert len(eng.last_events(0)) == len(lens), (name, len(eng.last_events(0)), len(lens))
+    errs, at = [], 0
+    for k, n in enumerate(lens):
+        ref = data[at:at + n]
+        at += n
+        g = eng.last_grain64(0, k)
+        assert g.shape == ref.shape, (name, k, g.shape, ref.shape)
+        errs.append(_rel(g, ref))
+    return errs
+
+
+@pytest.mark.parametrize("name", ["ghost_formants", "03_wavelet_ice_bloom", "wavelet_mist", "closed_curve_air",
+                                  "drifting_mode_fragments", "corona_glass_fog"])
+def test_cepstral_input_every_event(name, pins_all, golden_info, irs, full_renders, monkeypatch):
+    monkeypatch.setenv("MSGPU_G64_STOP", "cep")
+    errs = _per_event(name, "cep", golden_info, irs, full_renders, pins_all)
+    print(f"{name}: cepstral_warp inputs of {len(errs)} events, rel rms err max {max(errs):.3e} "
+          f"median {float(np.median(errs)):.3e}: " + " ".join(f"{e:.1e}" for e in errs))
+    assert max(errs) <= TOL
+
+
+def test_imprint_input_every_event(pins_all, golden_info, irs, full_renders):
+    name = "soft_ellipse_memory"
+    errs = _per_event(name, "imp", golden_info, irs, full_renders, pins_all)
+    print(f"{name}: SpectralImprint.apply inputs of {len(errs)} events, rel rms err max {max(errs):.3e}: "
+          + " ".join(f"{e:.1e}" for e in errs))
+    assert max(errs) <= TOL

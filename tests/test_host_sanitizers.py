@@ -44,3 +44,21 @@ def test_plan_and_rng_under_asan_ubsan(tmp_path):
     assert r.returncode == 0, out[-4000:]
     assert "ERROR: AddressSanitizer" not in out and "runtime error:" not in out, out[-4000:]
     assert " passed" in out
+
+
+@pytest.mark.skipif(shutil.which("g++") is None, reason="needs g++")
+def test_host_pool_under_tsan(tmp_path):
+    """The host pool (csrc/host_pool.h) under ThreadSanitizer: four caller threads
+    submit jobs concurrently, as bench.py's per-context enqueue threads do."""
+    tsan = _runtime("libtsan.so")
+    if not tsan:
+        pytest.skip("ThreadSanitizer runtime not installed")
+    exe = str(tmp_path / "host_pool_tsan")
+    subprocess.run(["g++", "-std=c++17", "-O1", "-g", "-fsanitize=thread", "-Wall", "-Werror", "-I", CSRC,
+                    "-o", exe, os.path.join(REPO, "tests", "host_pool_tsan.cpp"), "-pthread"], check=True)
+    env = dict(os.environ, MSGPU_HOST_THREADS="6", TSAN_OPTIONS="halt_on_error=1:second_deadlock_stack=1")
+    r = subprocess.run([exe], capture_output=True, text=True, env=env, timeout=600)
+    out = r.stdout + r.stderr
+    assert r.returncode == 0, out[-4000:]
+    assert "WARNING: ThreadSanitizer" not in out, out[-4000:]
+    assert "bad 0" in out
