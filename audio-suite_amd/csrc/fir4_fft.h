@@ -29,6 +29,27 @@ template <> struct Fir4Cfg<16384> { static constexpr int R1 = 16, R2 = 16, R3 = 
 
 template <int S> MSG_HD constexpr int pads(int x) { return S ? x + x / S : x; }
 
+// v[r] *= W_M^(e r), r = 1 .. R-1, W_M from the two-level table at (lo, hi).
+// Table twiddles: each is one product of two correctly rounded entries (~1 ulp,
+// two LDS reads and a complex multiply); power twiddles (twiddle_pow_ab): from
+// two table values by up to ~6 roundings at R = 16 (R = 8: ~3).
+// MSG_FIR_TWTAB = 1: table twiddles in every pass, 2: for the radix-16 passes
+// (the inverse's passes 3' and 4'; the forward's radix-16 pass 2 reads exact
+// [r][k] tables), powers for radix 8, 0: powers everywhere.
+#ifndef MSG_FIR_TWTAB
+#define MSG_FIR_TWTAB 2
+#endif
+template <int M, int R>
+MSG_DEV void fir_twiddle(float2 (&v)[R], const float2* tab, int lo, int hi, int e) {
+    if constexpr (MSG_FIR_TWTAB == 1 || (MSG_FIR_TWTAB == 2 && R >= 16)) {
+#pragma unroll
+        for (int r = 1; r < R; ++r) v[r] = cmul(v[r], fir_wM(tab, lo, hi, (e * r) & (M - 1)));
+    } else {
+        constexpr int B = tw_base<R>();
+        twiddle_pow_ab<R, B>(v, fir_wM(tab, lo, hi, e), fir_wM(tab, lo, hi, (e * B) & (M - 1)));
+    }
+}
+
 template <int M> struct Fir4Geo {
     static constexpr int R1 = Fir4Cfg<M>::R1, R2 = Fir4Cfg<M>::R2, R3 = Fir4Cfg<M>::R3, R4 = Fir4Cfg<M>::R4;
     static_assert(R1 * R2 * R3 * R4 == M, "four passes");
@@ -82,9 +103,7 @@ MSG_DEV void fir4_pass_lds(float2* buf, const float2* tab, int t) {
 #pragma unroll
             for (int r = 1; r < R; ++r) v[b][r] = cmul(v[b][r], tab[OFF_T + r * NS + k]);
         } else {
-            constexpr int B = tw_base<R>();
-            twiddle_pow_ab<R, B>(v[b], fir_wM(tab, G::OFF_MLO, G::OFF_MHI, k * STEP),
-                                 fir_wM(tab, G::OFF_MLO, G::OFF_MHI, (k * STEP * B) & (M - 1)));
+            fir_twiddle<M, R>(v[b], tab, G::OFF_MLO, G::OFF_MHI, k * STEP);
         }
         Dft<R, false>::run(v[b]);
         const int lo = q * NS * R + k;
@@ -160,8 +179,7 @@ k_fir4(const PresetRt* __restrict__ rt, const int2* __restrict__ jobs, const flo
         __syncthreads();   // LDS free for the next segment / the inverse
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
-            twiddle_pow_ab<R4, tw_base<R4>()>(v[h], fir_wM(tab, G::OFF_MLO, G::OFF_MHI, js[h]),
-                                              fir_wM(tab, G::OFF_MLO, G::OFF_MHI, (js[h] * tw_base<R4>()) & (M - 1)));
+            fir_twiddle<M, R4>(v[h], tab, G::OFF_MLO, G::OFF_MHI, js[h]);
             Dft<R4, false>::run(v[h]);
         }
         // ---- real split, X . H_q accumulated in registers (k_fir2's pairing)
@@ -232,8 +250,7 @@ k_fir4(const PresetRt* __restrict__ rt, const int2* __restrict__ jobs, const flo
         float2 v[R1];
 #pragma unroll
         for (int r = 0; r < R1; ++r) v[r] = buf[pads<G::S3I>(t + r * NB1)];
-        twiddle_pow_ab<R1, tw_base<R1>()>(v, fir_wM(tab, G::OFF_MLO, G::OFF_MHI, t),
-                                          fir_wM(tab, G::OFF_MLO, G::OFF_MHI, (t * tw_base<R1>()) & (M - 1)));
+        fir_twiddle<M, R1>(v, tab, G::OFF_MLO, G::OFF_MHI, t);
         Dft<R1, false>::run(v);
 #pragma unroll
         for (int r = 0; r < R1; ++r) {
@@ -350,8 +367,7 @@ MSG_DEV void fir4s_forward(float2* buf, const float2* tab, const float* x, int64
     __syncthreads();   // LDS free for the inverse
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-        twiddle_pow_ab<R4, tw_base<R4>()>(v[h], fir_wM(tab, G::OFF_MLO, G::OFF_MHI, js[h]),
-                                          fir_wM(tab, G::OFF_MLO, G::OFF_MHI, (js[h] * tw_base<R4>()) & (M - 1)));
+        fir_twiddle<M, R4>(v[h], tab, G::OFF_MLO, G::OFF_MHI, js[h]);
         Dft<R4, false>::run(v[h]);
     }
     if (!t0z) {
@@ -476,8 +492,7 @@ k_fir4s(const PresetRt* __restrict__ rt, const int2* __restrict__ jobs, const fl
             float2 u[R1];
 #pragma unroll
             for (int r = 0; r < R1; ++r) u[r] = buf[pads<G::S3I>(t + r * NB1)];
-            twiddle_pow_ab<R1, tw_base<R1>()>(u, fir_wM(tab, G::OFF_MLO, G::OFF_MHI, t),
-                                              fir_wM(tab, G::OFF_MLO, G::OFF_MHI, (t * tw_base<R1>()) & (M - 1)));
+            fir_twiddle<M, R1>(u, tab, G::OFF_MLO, G::OFF_MHI, t);
             Dft<R1, false>::run(u);
 #pragma unroll
             for (int r = 0; r < R1; ++r) {

@@ -78,8 +78,7 @@ MSG_DEV void fwd_half(float2* buf, const float2* tab, float2 (&in)[R1], float2 (
     __syncthreads();   // LDS free for the inverse
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-        twiddle_pow_ab<R4, tw_base<R4>()>(v[h], fir_wM(tab, G::OFF_MLO, G::OFF_MHI, js[h]),
-                                          fir_wM(tab, G::OFF_MLO, G::OFF_MHI, (js[h] * tw_base<R4>()) & (MH - 1)));
+        fir_twiddle<MH, R4>(v[h], tab, G::OFF_MLO, G::OFF_MHI, js[h]);
         Dft<R4, false>::run(v[h]);
     }
 }
@@ -106,8 +105,7 @@ MSG_DEV void inv_half(float2* buf, const float2* tab, float2 (&acc)[2][R4], floa
 #pragma unroll
     for (int r = 0; r < R1; ++r) u[r] = buf[pads<G::S3I>(t + r * NB1)];
     __syncthreads();   // LDS free for the next half
-    twiddle_pow_ab<R1, tw_base<R1>()>(u, fir_wM(tab, G::OFF_MLO, G::OFF_MHI, t),
-                                      fir_wM(tab, G::OFF_MLO, G::OFF_MHI, (t * tw_base<R1>()) & (MH - 1)));
+    fir_twiddle<MH, R1>(u, tab, G::OFF_MLO, G::OFF_MHI, t);
     Dft<R1, false>::run(u);
 }
 
@@ -256,36 +254,47 @@ k_fir8(const PresetRt* __restrict__ rt, const int2* __restrict__ jobs, const flo
     }
 }
 
-// H = rfft_N(h[0, P)) of one preset (Q = 1), in the even/odd layout above; h
-// from k_h_build's scratch.  One workgroup per preset.
-template <int UNUSED = 0>
-__global__ void __launch_bounds__(fir8::T)
-k_fir8_hpart(const PresetRt* __restrict__ rt, const int32_t* __restrict__ list, const float2* __restrict__ tables,
-             const float* __restrict__ hs, float2* __restrict__ hspec) {
-    using namespace fir8;
-    extern __shared__ __attribute__((aligned(16))) float2 lds[];
-    float2* tab = lds;
-    float2* buf = lds + G::TAB;
-    const PresetRt& r = rt[list[blockIdx.x]];
-    for (int i = threadIdx.x; i < G::TAB_USED; i += T) tab[i] = tables[i];
-    float2 a[R1], b[R1];
-    load_halves(hs + r.hs_off, r.h_len < r.fir_P ? r.h_len : r.fir_P, 0, a, b);
-    __syncthreads();
-    dif_split(tab, a, b);
-    float2* He = hspec + r.h_off;
-    float2* Ho = He + (MH + 1);
+// ---------------------------------------------------------------------------
+// Filter spectra in the even/odd layout, one workgroup per (filter, half): the
+// even half needs a = z0 + z1 and the odd half b = (z0 - z1) W only, so each
+// half is its own workgroup (twice the workgroups of a per-filter kernel, each
+// half as long: the h stage had 1.3 rounds of 256 long workgroups per launch).
+//   k_fir8_hconv   ER (+ IR) presets: H = rfft(delta + ER taps) . S_IR.  The
+//                  linear convolution fits the transform (h_len < N for one
+//                  partition), so h never exists in the time domain: the taps
+//                  are scattered into LDS as a (or z0 - z1) directly, and the
+//                  IR's spectrum S_IR (k_fir8_spec, once per IR of the batch)
+//                  multiplies the result.  IR-only presets use S_IR itself.
+//   k_fir8_spec    H = rfft of float64 (IR bank) or float32 (msg_fir taps)
+//                  samples: jobs (source offset, length, spectrum offset).
+// ---------------------------------------------------------------------------
+namespace fir8 {
+// X of one half, from the last forward pass (v, butterflies js), times S (if
+// non-null, same layout) into Hh (He or Ho).
+template <bool ODD>
+MSG_DEV void store_half(const float2* tab, const float2 (&v)[2][R4], const float2* __restrict__ S,
+                        float2* __restrict__ Hh) {
     const int t = otid();
-    float2 v[2][R4];
-    fwd_half<false>(buf, tab, a, v);
-    if (t != 0) {
+    auto put = [&](int k, float2 x) { Hh[(uint32_t)k] = S ? cmul(x, S[(uint32_t)k]) : x; };
+    if (ODD) {
+        const float2 wA = cmul_k(fir_wM(tab, G::OFF_PLO, G::OFF_PHI, t), wN1());
+#pragma unroll
+        for (int q = 0; q < R4; ++q) {
+            const int kA = t + q * NB4;
+            float2 xk, xm;
+            fir_split(v[0][q], v[1][R4 - 1 - q], cmul_k(wA, fir_cr<R4>(q)), xk, xm);
+            put(kA, xk);
+            put(MH - 1 - kA, xm);
+        }
+    } else if (t != 0) {
         const float2 wA = fir_wM(tab, G::OFF_PLO, G::OFF_PHI, t);
 #pragma unroll
         for (int q = 0; q < R4; ++q) {
             const int kA = t + q * NB4;
             float2 xk, xm;
             fir_split(v[0][q], v[1][R4 - 1 - q], cmul_k(wA, fir_cr<R4>(q)), xk, xm);
-            He[(uint32_t)kA] = xk;
-            He[(uint32_t)(MH - kA)] = xm;
+            put(kA, xk);
+            put(MH - kA, xm);
         }
     } else {
         float2 aa[R4], bb[R4];
@@ -295,22 +304,106 @@ k_fir8_hpart(const PresetRt* __restrict__ rt, const int32_t* __restrict__ list, 
             const int kA = fir_k0<MH, R4>(q);
             float2 xk, xm;
             fir_split(aa[q], bb[R4 - 1 - q], fir_w0<MH, R4>(q), xk, xm);
-            He[kA] = xk;
-            He[MH - kA] = xm;
+            put(kA, xk);
+            put(MH - kA, xm);
         }
         const float2 z0 = aa[R4 - 1];
-        He[0] = make_float2(z0.x + z0.y, 0.f);
-        He[MH] = make_float2(z0.x - z0.y, 0.f);
-        He[MH / 2] = cconj(bb[0]);
+        put(0, make_float2(z0.x + z0.y, 0.f));
+        put(MH, make_float2(z0.x - z0.y, 0.f));
+        put(MH / 2, cconj(bb[0]));
     }
-    fwd_half<true>(buf, tab, b, v);
-    const float2 wA = cmul_k(fir_wM(tab, G::OFF_PLO, G::OFF_PHI, t), wN1());
+}
+
+// one half of the input: a = z0 + z1 (ODD = false) or (z0 - z1) W_M^m, from x[0, n) of type T
+template <bool ODD, class T>
+MSG_DEV void load_half(const float2* tab, const T* __restrict__ x, int64_t n, float2 (&in)[R1]) {
+    const int t = otid();
 #pragma unroll
-    for (int q = 0; q < R4; ++q) {
-        const int kA = t + q * NB4;
-        float2 xk, xm;
-        fir_split(v[0][q], v[1][R4 - 1 - q], cmul_k(wA, fir_cr<R4>(q)), xk, xm);
-        Ho[(uint32_t)kA] = xk;
-        Ho[(uint32_t)(MH - 1 - kA)] = xm;
+    for (int r = 0; r < R1; ++r) {
+        float2 z[2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int64_t i = 2 * (int64_t)(t + r * NB1 + h * MH);
+            z[h] = make_float2(i < n ? (float)x[i] : 0.f, i + 1 < n ? (float)x[i + 1] : 0.f);
+        }
+        in[r] = ODD ? ff(vv(z[0]) - vv(z[1])) : ff(vv(z[0]) + vv(z[1]));
+    }
+    if (ODD) {
+        const float2 wt = fir_wM(tab, G::OFF_PLO, G::OFF_PHI, t);
+#pragma unroll
+        for (int r = 0; r < R1; ++r) in[r] = r == 0 ? cmul(in[r], wt) : cmul(in[r], cmul_k(wt, w32<R1>(r)));
+    }
+}
+}  // namespace fir8
+
+// jobs[4 i ..]: source offset (elements of T), length, spectrum offset (float2), unused
+template <class SRC>
+__global__ void __launch_bounds__(fir8::T)
+k_fir8_spec(const int64_t* __restrict__ jobs, const float2* __restrict__ tables, const SRC* __restrict__ src,
+            float2* __restrict__ hspec) {
+    using namespace fir8;
+    extern __shared__ __attribute__((aligned(16))) float2 lds[];
+    float2* tab = lds;
+    float2* buf = lds + G::TAB;
+    const int64_t* j = jobs + 4 * (blockIdx.x >> 1);
+    const bool odd = blockIdx.x & 1;
+    for (int i = threadIdx.x; i < G::TAB_USED; i += T) tab[i] = tables[i];
+    __syncthreads();
+    float2 in[R1], v[2][R4];
+    float2* He = hspec + j[2];
+    if (!odd) {
+        load_half<false>(tab, src + j[0], j[1], in);
+        fwd_half<false>(buf, tab, in, v);
+        store_half<false>(tab, v, nullptr, He);
+    } else {
+        load_half<true>(tab, src + j[0], j[1], in);
+        fwd_half<true>(buf, tab, in, v);
+        store_half<true>(tab, v, nullptr, He + (MH + 1));
+    }
+}
+
+template <int UNUSED = 0>
+__global__ void __launch_bounds__(fir8::T)
+k_fir8_hconv(const PresetRt* __restrict__ rt, const int32_t* __restrict__ list, const float2* __restrict__ tables,
+             const int32_t* __restrict__ er_off, const double* __restrict__ er_gain, float2* __restrict__ hspec) {
+    using namespace fir8;
+    extern __shared__ __attribute__((aligned(16))) float2 lds[];
+    float2* tab = lds;
+    float2* buf = lds + G::TAB;
+    const PresetRt& r = rt[list[blockIdx.x >> 1]];
+    const bool odd = blockIdx.x & 1;
+    for (int i = threadIdx.x; i < G::TAB_USED; i += T) tab[i] = tables[i];
+    for (int m = threadIdx.x; m < MH; m += T) buf[m] = make_float2(0.f, 0.f);
+    __syncthreads();
+    // e = delta + taps as the half's input: slot m & (MH-1), minus for m >= MH in the odd half
+    // (the host merged equal offsets, so a slot takes at most one tap from each half, and
+    // the LDS float adds of at most two values in either order give the same sum)
+    float* e = reinterpret_cast<float*>(buf);
+    if (threadIdx.x == 0) atomicAdd(e, 1.0f);
+    for (int k = threadIdx.x; k < r.n_taps; k += T) {
+        const int o = er_off[r.er_base + k];
+        const int m = o >> 1;
+        const float g = (float)er_gain[r.er_base + k];
+        atomicAdd(e + 2 * (m & (MH - 1)) + (o & 1), (odd && m >= MH) ? -g : g);
+    }
+    __syncthreads();
+    float2 in[R1], v[2][R4];
+    const int t = otid();
+#pragma unroll
+    for (int q = 0; q < R1; ++q) in[q] = buf[t + q * NB1];
+    if (odd) {
+        const float2 wt = fir_wM(tab, G::OFF_PLO, G::OFF_PHI, t);
+#pragma unroll
+        for (int q = 0; q < R1; ++q) in[q] = q == 0 ? cmul(in[q], wt) : cmul(in[q], cmul_k(wt, w32<R1>(q)));
+    }
+    __syncthreads();                                  // every read done before pass 1 writes buf
+    const float2* S = r.ir_len > 0 ? hspec + r.irs_off : nullptr;
+    float2* He = hspec + r.h_off;
+    if (!odd) {
+        fwd_half<false>(buf, tab, in, v);
+        store_half<false>(tab, v, S, He);
+    } else {
+        fwd_half<true>(buf, tab, in, v);
+        store_half<true>(tab, v, S ? S + (MH + 1) : nullptr, He + (MH + 1));
     }
 }

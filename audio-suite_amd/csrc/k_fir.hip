@@ -25,7 +25,11 @@ void fir_init_attrs() {
                               Fir4Geo<16384>::LDS_BYTES);
     (void)hipFuncSetAttribute((const void*)k_fir8<0>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               Fir4Geo<16384>::LDS_BYTES);
-    (void)hipFuncSetAttribute((const void*)k_fir8_hpart<0>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    (void)hipFuncSetAttribute((const void*)k_fir8_hconv<0>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              Fir4Geo<16384>::LDS_BYTES);
+    (void)hipFuncSetAttribute((const void*)k_fir8_spec<double>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              Fir4Geo<16384>::LDS_BYTES);
+    (void)hipFuncSetAttribute((const void*)k_fir8_spec<float>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               Fir4Geo<16384>::LDS_BYTES);
     fir2_attr<1024>(); fir2_attr<2048>(); fir2_attr<4096>(); fir2_attr<8192>(); fir2_attr<16384>();
     (void)hipFuncSetAttribute((const void*)k_fir_h<FIR_T, FIR_M>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
@@ -123,10 +127,24 @@ hipError_t launch_fir8(unsigned grid, hipStream_t s, const PresetRt* rt, const i
     return hipGetLastError();
 }
 
-hipError_t launch_fir8_hpart(unsigned n_presets, hipStream_t s, const PresetRt* rt, const int32_t* list,
-                             const float2* tables, const float* hs, float2* hspec) {
-    hipLaunchKernelGGL((k_fir8_hpart<0>), dim3(n_presets), dim3(fir8::T), Fir4Geo<16384>::LDS_BYTES, s, rt, list,
-                       tables, hs, hspec);
+hipError_t launch_fir8_hconv(unsigned n_presets, hipStream_t s, const PresetRt* rt, const int32_t* list,
+                             const float2* tables, const int32_t* er_off, const double* er_gain, float2* hspec) {
+    hipLaunchKernelGGL((k_fir8_hconv<0>), dim3(2 * n_presets), dim3(fir8::T), Fir4Geo<16384>::LDS_BYTES, s, rt, list,
+                       tables, er_off, er_gain, hspec);
+    return hipGetLastError();
+}
+
+hipError_t launch_fir8_spec64(unsigned n_jobs, hipStream_t s, const int64_t* jobs, const float2* tables,
+                              const double* src, float2* hspec) {
+    hipLaunchKernelGGL((k_fir8_spec<double>), dim3(2 * n_jobs), dim3(fir8::T), Fir4Geo<16384>::LDS_BYTES, s, jobs,
+                       tables, src, hspec);
+    return hipGetLastError();
+}
+
+hipError_t launch_fir8_spec32(unsigned n_jobs, hipStream_t s, const int64_t* jobs, const float2* tables,
+                              const float* src, float2* hspec) {
+    hipLaunchKernelGGL((k_fir8_spec<float>), dim3(2 * n_jobs), dim3(fir8::T), Fir4Geo<16384>::LDS_BYTES, s, jobs,
+                       tables, src, hspec);
     return hipGetLastError();
 }
 

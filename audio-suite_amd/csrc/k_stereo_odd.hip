@@ -36,10 +36,10 @@ int64_t stereo_odd_len(int64_t n, int row_max, int col_max) {
     return so_shape(n, row_max, col_max, g) ? g.M : -1;
 }
 
-static size_t so_col_lds(int Mc, int C) { return (size_t)(Mc + C * Mc) * sizeof(float2); }
+static size_t so_col_lds(int Mc, int C) { return (size_t)(Mc + C * Mc) * sizeof(double2); }
 
 // forward FFT_M of A up to (not including) the row transforms
-static void so_fwd_cols(float2* A, const SoShape& g, hipStream_t s) {
+static void so_fwd_cols(double2* A, const SoShape& g, hipStream_t s) {
     const int64_t L = (int64_t)g.M1 * g.M2;
     if (g.M0 > 1)
         hipLaunchKernelGGL(k_so_cols<false>, dim3((unsigned)(L / g.C0), 1), dim3(SO_T), so_col_lds(g.M0, g.C0), s, A,
@@ -48,7 +48,7 @@ static void so_fwd_cols(float2* A, const SoShape& g, hipStream_t s) {
         hipLaunchKernelGGL(k_so_cols<false>, dim3((unsigned)(g.M2 / g.C), (unsigned)g.M0), dim3(SO_T),
                            so_col_lds(g.M1, g.C), s, A, g.M1, g.M2, g.C, L);
 }
-static void so_inv_cols(float2* A, const SoShape& g, hipStream_t s) {
+static void so_inv_cols(double2* A, const SoShape& g, hipStream_t s) {
     const int64_t L = (int64_t)g.M1 * g.M2;
     if (g.M1 > 1)
         hipLaunchKernelGGL(k_so_cols<true>, dim3((unsigned)(g.M2 / g.C), (unsigned)g.M0), dim3(SO_T),
@@ -59,28 +59,28 @@ static void so_inv_cols(float2* A, const SoShape& g, hipStream_t s) {
 }
 
 // A <- F(A) . Bp -> inverse (natural order, unscaled but Bp carries 1/M)
-static hipError_t so_conv(float2* A, const float2* Bp, const SoShape& g, hipStream_t s) {
+static hipError_t so_conv(double2* A, const double2* Bp, const SoShape& g, hipStream_t s) {
     so_fwd_cols(A, g, s);
-    hipLaunchKernelGGL(k_so_rows, dim3((unsigned)(g.M / g.M2)), dim3(SO_T), (size_t)2 * g.M2 * sizeof(float2), s, A,
+    hipLaunchKernelGGL(k_so_rows, dim3((unsigned)(g.M / g.M2)), dim3(SO_T), (size_t)2 * g.M2 * sizeof(double2), s, A,
                        g.M2, Bp);
     so_inv_cols(A, g, s);
     return hipGetLastError();
 }
 
-hipError_t launch_stereo_odd_kernel(int64_t n, int row_max, int col_max, float2* Bp, float2* A, hipStream_t s) {
+hipError_t launch_stereo_odd_kernel(int64_t n, int row_max, int col_max, double2* Bp, double2* A, hipStream_t s) {
     SoShape g;
     if (!so_shape(n, row_max, col_max, g)) return hipErrorInvalidValue;
     const unsigned grid = (unsigned)((g.M + 255) / 256);
     hipLaunchKernelGGL(k_so_bfill, dim3(grid), dim3(256), 0, s, Bp, n, g.M);
     so_fwd_cols(Bp, g, s);
-    hipLaunchKernelGGL(k_so_rows, dim3((unsigned)(g.M / g.M2)), dim3(SO_T), (size_t)2 * g.M2 * sizeof(float2), s, Bp,
-                       g.M2, (const float2*)nullptr);
+    hipLaunchKernelGGL(k_so_rows, dim3((unsigned)(g.M / g.M2)), dim3(SO_T), (size_t)2 * g.M2 * sizeof(double2), s, Bp,
+                       g.M2, (const double2*)nullptr);
     (void)A;
     return hipGetLastError();
 }
 
 hipError_t launch_stereo_odd(int64_t n, int row_max, int col_max, int dr, double width, const float* y,
-                             const float2* Bp, float2* A, float* r2, hipStream_t s) {
+                             const double2* Bp, double2* A, float* r2, hipStream_t s) {
     SoShape sh;
     if (!so_shape(n, row_max, col_max, sh)) return hipErrorInvalidValue;
     const int64_t M = sh.M;

@@ -27,31 +27,35 @@ k_ir_spec(const int64_t* __restrict__ jobs /* [ir_off, ir_len, plan, out_off] */
     for (int k = threadIdx.x; k <= rp.n / 2; k += T) dst[k] = cx(lds, k);
 }
 
-// The space filter h = (delta + ER taps) * IR (MS:409-445) in the time domain,
-// float64: h[t] = ir[t] + sum_k g_k ir[t - o_k] over the preset's merged,
-// offset-sorted taps (o_k in (0, out_n), msg_render_batch), with ir = delta
-// when the preset has no IR.  One workgroup per tile of H_TILE taps; the IR is
-// staged in LDS as float64 and each tile walks only the taps whose shifted IR
-// overlaps it (the offsets are sorted).  Any length: the ER span is not limited
-// by a transform size (192 kHz x 150 ms + 8192 IR taps = 36 992 taps).  Output:
-// h_len floats at hs_off, cut into partitions by k_fir_h / k_fir4_hpart.
+// The space filter h = (delta + ER taps) * IR (MS:409-445) in the time domain:
+// h[t] = ir[t] + sum_k g_k ir[t - o_k] over the preset's merged, offset-sorted
+// taps (o_k in (0, out_n), msg_render_batch), ir = delta without an IR, summed
+// in float64.  One workgroup per tile of H_TILE taps of h.  The IR sits in LDS
+// zero-padded by H_TILE on both sides, so every (tap, output) pair is one LDS
+// read at a tap-uniform base plus the thread's fixed offsets (no bounds tests),
+// and only the taps whose shifted IR overlaps the tile are walked, staged
+// through LDS H_T at a time.  Any length: the ER span is not limited by a
+// transform size (192 kHz x 150 ms + 8192 IR taps = 36 992 taps).  Output:
+// h_len floats at hs_off, cut into partitions by k_fir_h / k_fir4_hpart / k_fir8_hpart.
 constexpr int H_T = 256, H_PER = 4, H_TILE = H_T * H_PER, H_IRMAX = 8192;
 __global__ void __launch_bounds__(H_T)
 k_h_build(const PresetRt* __restrict__ rt, const int32_t* __restrict__ tile_begin, int n_presets,
           const int32_t* __restrict__ er_off, const double* __restrict__ er_gain,
           const double* __restrict__ ir_bank, float* __restrict__ hs) {
-    __shared__ double ir[H_IRMAX];
+    __shared__ float irp[H_IRMAX + 2 * H_TILE];          // irp[H_TILE + d] = ir[d], zero outside [0, irl)
+    __shared__ int32_t s_off[H_T];
+    __shared__ double s_g[H_T];
     const int b = blockIdx.x;
     const int p = find_preset(tile_begin, n_presets, b);
     const PresetRt& r = rt[p];
     const int hl = r.h_len;
     const int irl = r.ir_len > 0 ? r.ir_len : 1;
     const int t0 = (b - tile_begin[p]) * H_TILE;
-    if (r.ir_len > 0) {
-        const double* src = ir_bank + r.ir_off;
-        for (int i = threadIdx.x; i < irl; i += H_T) ir[i] = src[i];
-    } else if (threadIdx.x == 0) {
-        ir[0] = 1.0;
+    const int tid = threadIdx.x;
+    const double* src = ir_bank + r.ir_off;
+    for (int i = tid; i < irl + 2 * H_TILE; i += H_T) {
+        const int d = i - H_TILE;
+        irp[i] = (d >= 0 && d < irl) ? (r.ir_len > 0 ? (float)src[d] : 1.0f) : 0.0f;
     }
     // taps whose shifted IR reaches [t0, t0 + H_TILE): o in (t0 - irl, t0 + H_TILE)
     const int32_t* off = er_off + r.er_base;
@@ -65,23 +69,26 @@ k_h_build(const PresetRt* __restrict__ rt, const int32_t* __restrict__ tile_begi
     __syncthreads();
     double acc[H_PER];
 #pragma unroll
-    for (int i = 0; i < H_PER; ++i) {
-        const int t = t0 + (int)threadIdx.x + i * H_T;
-        acc[i] = t < irl ? ir[t] : 0.0;                       // the direct path (delta * IR)
+    for (int i = 0; i < H_PER; ++i) {                          // delta * IR
+        const int t = t0 + tid + i * H_T;
+        acc[i] = t < irl ? (double)irp[H_TILE + t] : 0.0;
     }
-    for (int k = klo; k < khi; ++k) {
-        const int o = off[k];
-        const double g = gain[k];
+    for (int k0 = klo; k0 < khi; k0 += H_T) {
+        const int kn = khi - k0 < H_T ? khi - k0 : H_T;
+        __syncthreads();                                        // previous chunk's reads done
+        if (tid < kn) { s_off[tid] = off[k0 + tid]; s_g[tid] = gain[k0 + tid]; }
+        __syncthreads();
+        for (int k = 0; k < kn; ++k) {
+            const float* base = irp + (H_TILE + t0 - s_off[k]) + tid;   // in [0, irl + H_TILE]
+            const double g = s_g[k];
 #pragma unroll
-        for (int i = 0; i < H_PER; ++i) {
-            const int d = t0 + (int)threadIdx.x + i * H_T - o;
-            if ((unsigned)d < (unsigned)irl) acc[i] = fma(g, ir[d], acc[i]);
+            for (int i = 0; i < H_PER; ++i) acc[i] = fma(g, (double)base[i * H_T], acc[i]);
         }
     }
     float* h = hs + r.hs_off;
 #pragma unroll
     for (int i = 0; i < H_PER; ++i) {
-        const int t = t0 + (int)threadIdx.x + i * H_T;
+        const int t = t0 + tid + i * H_T;
         if (t < hl) h[t] = (float)acc[i];
     }
 }

@@ -66,12 +66,18 @@ constexpr int FIR4S_P = 16384;
 hipError_t launch_fir4_hpart(int M, unsigned n_parts, hipStream_t s, const PresetRt* rt, const int2* part_jobs,
                              const float2* tables, const float* hs, float2* hspec);
 // N = 65536 overlap-save, one partition (fir8_fft.h): blocks on the k_fir4 engine in
-// two halves; k_fir8_hpart builds H (even/odd bin layout, N/2 + 1 float2) per listed preset
+// two halves.  Spectra (even/odd bin layout, N/2 + 1 float2): k_fir8_hconv per listed
+// ER preset (rfft(delta + taps) . S_IR), k_fir8_spec per job [src off, len, spec off, 0]
+// of float64 (IR bank) or float32 samples.
 constexpr int FIR8_N = 65536;
 hipError_t launch_fir8(unsigned grid, hipStream_t s, const PresetRt* rt, const int2* jobs, const float2* tables,
                        const float2* hspec, const float* x_in, float* y_out);
-hipError_t launch_fir8_hpart(unsigned n_presets, hipStream_t s, const PresetRt* rt, const int32_t* list,
-                             const float2* tables, const float* hs, float2* hspec);
+hipError_t launch_fir8_hconv(unsigned n_presets, hipStream_t s, const PresetRt* rt, const int32_t* list,
+                             const float2* tables, const int32_t* er_off, const double* er_gain, float2* hspec);
+hipError_t launch_fir8_spec64(unsigned n_jobs, hipStream_t s, const int64_t* jobs, const float2* tables,
+                              const double* src, float2* hspec);
+hipError_t launch_fir8_spec32(unsigned n_jobs, hipStream_t s, const int64_t* jobs, const float2* tables,
+                              const float* src, float2* hspec);
 hipError_t launch_fir4s(int M, unsigned grid, hipStream_t s, const PresetRt* rt, const int2* jobs,
                         const float2* tables, const float2* hspec, const float* x_in, float* y_out, int kblk);
 
@@ -114,9 +120,9 @@ hipError_t launch_fft64_one(int lds_bytes, hipStream_t s, const Real64Plan* plan
 void stereo_odd_init_attrs();
 // row_max / col_max: transform-split limits (0: the defaults 4096 / 2048)
 int64_t stereo_odd_len(int64_t n, int row_max, int col_max);   // M, or -1 when n is too long
-hipError_t launch_stereo_odd_kernel(int64_t n, int row_max, int col_max, float2* Bp, float2* A, hipStream_t s);
+hipError_t launch_stereo_odd_kernel(int64_t n, int row_max, int col_max, double2* Bp, double2* A, hipStream_t s);
 hipError_t launch_stereo_odd(int64_t n, int row_max, int col_max, int dr, double width, const float* y,
-                             const float2* Bp, float2* A, float* r2, hipStream_t s);
+                             const double2* Bp, double2* A, float* r2, hipStream_t s);
 // the app's spectrogram (stft_mag_db, MS:197-212) on the float64 engine
 hipError_t launch_stft64(unsigned frames, int lds_bytes, hipStream_t s, const Real64Plan* plans, int plan,
                          const void* x, int elem_bytes, int64_t n, int channels, int win, int hop, double* S);

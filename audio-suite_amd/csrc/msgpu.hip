@@ -230,6 +230,7 @@ struct msg_ctx {
     DevBuf<float2> hspec;
     DevBuf<float> hscratch;                     // h of every FIR preset (k_h_build -> k_fir_h / k_fir4_hpart)
     Slice<int32_t> h_tile_begin, fir8_list;
+    Slice<int64_t> ir8_jobs;
     Slice<int2> hpart_jobs;
     Slice<int2> fir_jobs;
     Slice<int32_t> spec_ct_list;
@@ -253,11 +254,10 @@ struct msg_ctx {
     DevBuf<double> sf_h;
     DevBuf<float2> sf_hspec, sf_xspec;
     DevBuf<float> sf_hf;                        // float taps of a k_fir8 filter
-    DevBuf<int32_t> sf_list;
     // odd-length stereo rotation (kernels_stereo_odd.h)
-    std::map<int64_t, DevBuf<float2>> so_bp;   // chirp kernel spectra by n
+    std::map<int64_t, DevBuf<double2>> so_bp;  // chirp kernel spectra by n (float64)
     int so_row = 0, so_col = 0;                // transform-split limits (MSGPU_SO_ROW / _COL, tests; 0 = default)
-    DevBuf<float2> so_A;
+    DevBuf<double2> so_A;
     DevBuf<float> so_r2;
     // host mirrors of the last batch
     std::vector<msg_plan_info> h_info;
@@ -688,7 +688,7 @@ void msg_destroy(msg_ctx* ctx) {
     for (float2* t : ctx->d_spec_ct_tab) hipFree(t);
     hipFree(ctx->d_spec3_tab);
     ctx->sf_prt.release(); ctx->sf_jobs.release(); ctx->sf_irjobs.release(); ctx->sf_h.release();
-    ctx->sf_hspec.release(); ctx->sf_xspec.release(); ctx->sf_hf.release(); ctx->sf_list.release();
+    ctx->sf_hspec.release(); ctx->sf_xspec.release(); ctx->sf_hf.release();
     for (auto& set : ctx->ev)
         for (auto& ev : set) hipEventDestroy(ev);
     {
@@ -904,18 +904,17 @@ int msg_fir(msg_ctx* ctx, const float* x_dev, float* y_dev, int64_t n, int32_t n
         }
         std::vector<float> hf((size_t)M);
         for (int64_t i = 0; i < M; ++i) hf[i] = (float)h[i];
-        const int32_t first = 0;
+        const int64_t job[4] = {0, M, 0, 0};      // k_fir8_spec: taps [0, M) -> spectrum at 0
         HIPCHK(ctx, ctx->sf_prt.ensure(prt.size()));
         HIPCHK(ctx, ctx->sf_jobs.ensure(fj.size()));
         HIPCHK(ctx, ctx->sf_hf.ensure((size_t)M));
-        HIPCHK(ctx, ctx->sf_list.ensure(1));
+        HIPCHK(ctx, ctx->sf_irjobs.ensure(4));
         HIPCHK(ctx, ctx->sf_hspec.ensure((size_t)(N / 2 + 1)));
         HIPCHK(ctx, hipMemcpyAsync(ctx->sf_prt.p, prt.data(), sizeof(PresetRt) * prt.size(), hipMemcpyHostToDevice, s));
         HIPCHK(ctx, hipMemcpyAsync(ctx->sf_jobs.p, fj.data(), sizeof(int2) * fj.size(), hipMemcpyHostToDevice, s));
         HIPCHK(ctx, hipMemcpyAsync(ctx->sf_hf.p, hf.data(), sizeof(float) * (size_t)M, hipMemcpyHostToDevice, s));
-        HIPCHK(ctx, hipMemcpyAsync(ctx->sf_list.p, &first, sizeof(int32_t), hipMemcpyHostToDevice, s));
-        HIPCHK(ctx, launch_fir8_hpart(1, s, ctx->sf_prt.p, ctx->sf_list.p, ctx->d_fir4tab, ctx->sf_hf.p,
-                                      ctx->sf_hspec.p));
+        HIPCHK(ctx, hipMemcpyAsync(ctx->sf_irjobs.p, job, sizeof(job), hipMemcpyHostToDevice, s));
+        HIPCHK(ctx, launch_fir8_spec32(1, s, ctx->sf_irjobs.p, ctx->d_fir4tab, ctx->sf_hf.p, ctx->sf_hspec.p));
         HIPCHK(ctx, launch_fir8((unsigned)fj.size(), s, ctx->sf_prt.p, ctx->sf_jobs.p, ctx->d_fir4tab, ctx->sf_hspec.p,
                                 x_dev, y_dev));
         HIPCHK(ctx, stream_done(ctx, s));
@@ -1234,7 +1233,11 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
     std::vector<int32_t> spec3;                           // events of the band-pruned kernel
     std::vector<int32_t> f32_presets;                     // presets on the float32 chain
     std::vector<int2> fjobs_by[7];                        // FIR output blocks per transform size; [5]: k_fir4s, [6]: k_fir8
-    std::vector<int32_t> fir8_list;                       // presets on k_fir8 (N = 65536)
+    std::vector<int32_t> fir8_list;                       // ER presets on k_fir8 (N = 65536): k_fir8_hconv
+    std::vector<int32_t> ir_only8;                        // IR-only presets on k_fir8: H = the IR's spectrum
+    std::map<int, int64_t> ir8_spec_of;                   // IR index -> spectrum offset (before relocation)
+    std::vector<int64_t> ir8_jobs;                        // k_fir8_spec jobs: [ir_off, len, spec_off, 0]
+    int64_t ir8_sum = 0;
     std::vector<int2> fir4s_presets;                      // (preset, blocks) on the streaming FIR
     // float64 grain chain records
     std::vector<Ev64> ev64;
@@ -1370,16 +1373,37 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
             r.fir_N = N; r.fir_P = Pp; r.fir_Q = Q; r.fir_B = stream ? Pp : N - Pp + 1;
             r.h_off = hsum;
             r.h_len = (int32_t)M;
-            r.hs_off = hs_sum;
-            hs_sum += (M + 3) & ~int64_t(3);    // 16-byte aligned h regions
             h_tile_begin[p] = htiles;
-            htiles += (int32_t)((M + H_BUILD_TILE - 1) / H_BUILD_TILE);
-            if (N == FIR8_N) {                     // k_fir8_hpart (one partition)
+            if (N == FIR8_N) {
+                // one partition: H = rfft(delta + ER taps) . S_IR straight into the spectrum
+                // (k_fir8_hconv), or the IR's spectrum itself for an IR-only preset
                 r.h_fir4 = 2;
-                fir8_list.push_back(p);
-            } else if (N == 2 * 16384 && ctx->fir4) {   // k_fir4_hpart
-                r.h_fir4 = 1;
-                for (int q = 0; q < Q; ++q) hpart_jobs.push_back(make_int2(p, q));
+                const bool er = (pr.flags & MSG_F_ER_CLOUD) != 0;
+                int64_t irs = -1;
+                if (r.ir_len > 0) {
+                    auto it = ir8_spec_of.find(pr.ir_conv);
+                    if (it == ir8_spec_of.end()) {
+                        it = ir8_spec_of.emplace(pr.ir_conv, ir8_sum).first;
+                        ir8_jobs.insert(ir8_jobs.end(), {r.ir_off, (int64_t)r.ir_len, ir8_sum, 0});
+                        ir8_sum += N / 2 + 1;
+                    }
+                    irs = it->second;
+                }
+                if (er) {
+                    r.irs_off = irs;
+                    fir8_list.push_back(p);
+                } else {
+                    r.h_off = irs;                 // relocated past the per-preset spectra below
+                    ir_only8.push_back(p);
+                }
+            } else {                               // h in the time domain (k_h_build), cut into partitions
+                r.hs_off = hs_sum;
+                hs_sum += (M + 3) & ~int64_t(3);    // 16-byte aligned h regions
+                htiles += (int32_t)((M + H_BUILD_TILE - 1) / H_BUILD_TILE);
+                if (N == 2 * 16384 && ctx->fir4) {   // k_fir4_hpart
+                    r.h_fir4 = 1;
+                    for (int q = 0; q < Q; ++q) hpart_jobs.push_back(make_int2(p, q));
+                }
             }
             const int32_t nblk = (int32_t)((inf.out_n + r.fir_B - 1) / r.fir_B);
             if (stream) {
@@ -1391,7 +1415,8 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
             fblocks += nblk;
             hblocks += Q;
             if (!r.h_fir4) hblocks_gen += Q;
-            hsum += (int64_t)Q * (N / 2 + 1);
+            if (!(N == FIR8_N && r.ir_len > 0 && !(pr.flags & MSG_F_ER_CLOUD)))
+                hsum += (int64_t)Q * (N / 2 + 1);
         } else {
             h_tile_begin[p] = htiles;
         }
@@ -1638,7 +1663,12 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
     HIPCHK(ctx, ctx->grain.ensure(pool));
     HIPCHK(ctx, ctx->mono_a.ensure(ysum));
     HIPCHK(ctx, ctx->mono_y.ensure(ysum));
-    HIPCHK(ctx, ctx->hspec.ensure(hsum));
+    // the IR spectra of the k_fir8 presets follow the per-preset spectra in hspec
+    for (int p : fir8_list)
+        if (prt[p].ir_len > 0) prt[p].irs_off += hsum;
+    for (int p : ir_only8) prt[p].h_off += hsum;
+    for (size_t j = 0; j < ir8_jobs.size(); j += 4) ir8_jobs[j + 2] += hsum;
+    HIPCHK(ctx, ctx->hspec.ensure(hsum + ir8_sum));
     HIPCHK(ctx, ctx->hscratch.ensure(hs_sum));
     HIPCHK(ctx, ctx->maxbits.ensure(P));
     auto h2d = [&](auto** dst, const auto* src, size_t bytes) -> hipError_t {
@@ -1669,6 +1699,7 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
     HIPCHK(ctx, h2d(&ctx->irbank.p, irbank.data(), sizeof(double) * irbank.size()));
     HIPCHK(ctx, h2d(&ctx->h_tile_begin.p, h_tile_begin.data(), sizeof(int32_t) * P));
     HIPCHK(ctx, h2d(&ctx->fir8_list.p, fir8_list.data(), sizeof(int32_t) * fir8_list.size()));
+    HIPCHK(ctx, h2d(&ctx->ir8_jobs.p, ir8_jobs.data(), sizeof(int64_t) * ir8_jobs.size()));
     HIPCHK(ctx, h2d(&ctx->hpart_jobs.p, hpart_jobs.data(), sizeof(int2) * hpart_jobs.size()));
     HIPCHK(ctx, hipMemsetAsync(ctx->maxbits.p, 0, sizeof(unsigned) * P, s));
     HIPCHK(ctx, h2d(&ctx->ev64.p, ev64.data(), sizeof(Ev64) * ev64.size()));
@@ -1749,14 +1780,18 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
     stage_mark(ctx, 5, s);
     float* yb = ctx->mono_a.p;
     if (hblocks > 0) {
-        HIPCHK(ctx, launch_h_build((unsigned)htiles, s, ctx->prt.p, ctx->h_tile_begin.p, P, ctx->er_off.p,
-                                   ctx->er_gain.p, ctx->irbank.p, ctx->hscratch.p));
+        if (htiles > 0)
+            HIPCHK(ctx, launch_h_build((unsigned)htiles, s, ctx->prt.p, ctx->h_tile_begin.p, P, ctx->er_off.p,
+                                       ctx->er_gain.p, ctx->irbank.p, ctx->hscratch.p));
+        if (!ir8_jobs.empty())
+            HIPCHK(ctx, launch_fir8_spec64((unsigned)(ir8_jobs.size() / 4), s, ctx->ir8_jobs.p, ctx->d_fir4tab,
+                                           ctx->irbank.p, ctx->hspec.p));
         if (!hpart_jobs.empty())
             HIPCHK(ctx, launch_fir4_hpart(16384, (unsigned)hpart_jobs.size(), s, ctx->prt.p, ctx->hpart_jobs.p,
                                           ctx->d_fir4tab, ctx->hscratch.p, ctx->hspec.p));
         if (!fir8_list.empty())
-            HIPCHK(ctx, launch_fir8_hpart((unsigned)fir8_list.size(), s, ctx->prt.p, ctx->fir8_list.p, ctx->d_fir4tab,
-                                          ctx->hscratch.p, ctx->hspec.p));
+            HIPCHK(ctx, launch_fir8_hconv((unsigned)fir8_list.size(), s, ctx->prt.p, ctx->fir8_list.p, ctx->d_fir4tab,
+                                          ctx->er_off.p, ctx->er_gain.p, ctx->hspec.p));
         if (hblocks_gen > 0)   // blocks of k_fir4/k_fir8-engine presets return at once
             HIPCHK(ctx, launch_fir_h((unsigned)hblocks, fir_lds, s, ctx->prt.p, ctx->h_begin.p, P,
                                      ctx->fir_plans.dev.p, ctx->fir_plan_of.p, ctx->hscratch.p, ctx->hspec.p));
@@ -1791,7 +1826,7 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
         const int64_t n = info[p].out_n;
         auto it = ctx->so_bp.find(n);
         if (it == ctx->so_bp.end()) {
-            it = ctx->so_bp.emplace(n, DevBuf<float2>()).first;
+            it = ctx->so_bp.emplace(n, DevBuf<double2>()).first;
             HIPCHK(ctx, it->second.ensure(stereo_odd_len(n, ctx->so_row, ctx->so_col)));
             HIPCHK(ctx, launch_stereo_odd_kernel(n, ctx->so_row, ctx->so_col, it->second.p, ctx->so_A.p, s));
         }

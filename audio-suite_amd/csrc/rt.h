@@ -51,6 +51,7 @@ struct PresetRt {
     int32_t img_h, img_w;
     int64_t r2_off;        // stereo_fir == 2: rotated right channel in the odd-stereo buffer
     int64_t hs_off;        // h in the FIR scratch (h_len floats, k_h_build)
+    int64_t irs_off;       // k_fir8 ER + IR presets: the IR's spectrum in hspec (k_fir8_spec)
 };
 
 // Per-event spectral work descriptor (host-built after planning).

@@ -28,9 +28,6 @@ from .engine import default_engine
 from .pack import PackedBatch, design_sr
 from .params import first_missing_key, merged
 
-_NOTE = {"IR fragment": "IR fragment", "Image scanline": ""}
-
-
 def render(params, progress=None, device: int = 0):
     missing = first_missing_key(params)
     if missing is not None:
@@ -46,9 +43,9 @@ def render(params, progress=None, device: int = 0):
     if progress:                              # MS:757-758, while the device renders
         events = eng.last_events(0)
         n = len(events)
-        note = _fragment_note(p)
         for e in events:
             if e.len > 0 and e.index % 50 == 0:
+                note = _event_note(p, e.index)
                 progress(int(5 + 70 * (e.index / max(1, n))), f"Events {e.index}/{n}  {note}".strip())
     eng.torch.cuda.synchronize(eng.device)
     audio = out.cpu().numpy().reshape(packed.total_frames, 2)
@@ -62,13 +59,24 @@ def render(params, progress=None, device: int = 0):
     return np.ascontiguousarray(audio), meta
 
 
-def _fragment_note(p):
+def _event_note(p, i):
+    """The generator note of event i (MS:342-362, shown by MS:758): "IR fragment",
+    "Image line y=<row>" with the row drawn by default_rng(seed + i).integers(0, h)
+    (the library's NumPy-exact stream, msg_rng_integers), or the no-source notes."""
     mode = p["gen_mode"]
     if mode == "IR fragment":
         ir = p.get("_ir_audio")
-        return "No IR loaded" if (ir is None or ir.size < 32) else "IR fragment"
-    if mode == "Image scanline" and p.get("_img_gray") is None:
-        return "No image loaded"
+        return "No IR loaded" if (ir is None or np.asarray(ir).size < 32) else "IR fragment"
+    if mode == "Image scanline":
+        img = p.get("_img_gray")
+        if img is None:
+            return "No image loaded"
+        from . import _lib as L
+        import ctypes as C
+        y = C.c_int64(0)
+        L.check(L.lib().msg_rng_integers(int(p["seed"]) + int(i), 0, int(np.asarray(img).shape[0]), C.byref(y), 1),
+                None)
+        return f"Image line y={y.value}"
     return ""
 
 

@@ -206,3 +206,24 @@ def test_extra_odd_stereo_long(irs, extra_renders, golden_extra):
     step = int(golden_extra["decimation"])
     close(a[::step].astype(np.float32), extra_renders["ODD44_dec"], 2e-7)
     close(a[-8192:].astype(np.float32), extra_renders["ODD44_tail"], 2e-7)
+
+
+def _progress_params(case, irs, img):
+    p = merged(case["params"])
+    p["_img_gray"] = img if case["image"] else None
+    p["_ir_audio"] = irs["tiny_room_ir"] if case["ir"] else None
+    return p
+
+
+def test_progress_messages_pinned(irs, full_renders):
+    """The oracle's progress messages equal the reference's (tests/golden/progress.json):
+    the SR line, every 50th event with its generator note (Image line y=..., IR
+    fragment, no-source notes, MS:342-362, 757-758) and Done."""
+    import json
+    import os
+    cases = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "progress.json")))
+    for name, case in cases.items():
+        msgs = []
+        O.render(_progress_params(case, irs, full_renders["image_gray"]),
+                 progress=lambda v, m: msgs.append([int(v), str(m)]))
+        assert msgs == case["messages"], name

@@ -14,6 +14,9 @@ stubbed, exactly as tools/gen_golden.py does).  Writes DATA fixtures:
     frames) -- summaries, every 64th frame and the first/last 8192 frames;
   - the metric label's 384 kHz -> 48 kHz point (config H48) for seeds
     1000..1003: summaries, and the whole buffer of seed 1000.
+* ``tests/golden/progress.json``: the reference's progress messages (MS:599-600,
+  757-758, 783-784) for Image scanline (with and without an image), IR
+  fragment and a default preset.
 * ``tests/golden/stage_pins_all.npz``: EVERY call's input to ``cepstral_warp``
   (MS:150-163) and ``SpectralImprint.apply`` (MS:565-581) in the seven
   spread-held presets (0.5 s, tiny-room IR, the golden image), in call order.
@@ -141,12 +144,38 @@ def pins(ms, irs):
     np.savez_compressed(os.path.join(OUT, "stage_pins_all.npz"), **out)
 
 
+def progress_cases(irs, img):
+    base = dict(event_process="Poisson", grains_per_sec=120.0, out_dur_s=1.0, base_sr=48000, time_unfold=4.0)
+    return {
+        "image": merged(base, gen_mode="Image scanline", seed=321, _img_gray=img, _ir_audio=None),
+        "image_none": merged(base, gen_mode="Image scanline", seed=322, _img_gray=None, _ir_audio=None),
+        "irfrag": merged(base, gen_mode="IR fragment", seed=323, _ir_audio=irs["tiny_room_ir"], _img_gray=None),
+        "default": merged(base, seed=324, _ir_audio=None, _img_gray=None),
+    }
+
+
+def progress(ms, irs):
+    """The reference's progress messages (MS:599-600, 757-758, 783-784), per case."""
+    img = (np.add.outer(np.arange(48), np.arange(64)) * 7 % 256).astype(np.uint8)   # as gen_golden.py
+    out = {}
+    for name, p in progress_cases(irs, img).items():
+        msgs = []
+        ms.render(p, progress=lambda v, m: msgs.append([int(v), str(m)]))
+        out[name] = {"params": {k: v for k, v in p.items() if not k.startswith("_")},
+                     "image": p["_img_gray"] is not None, "ir": p["_ir_audio"] is not None, "messages": msgs}
+        print(name, msgs[:3], flush=True)
+    with open(os.path.join(OUT, "progress.json"), "w") as fh:
+        json.dump(out, fh, indent=1)
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--only", choices=["renders", "pins"])
+    ap.add_argument("--only", choices=["renders", "pins", "progress"])
     a = ap.parse_args()
     ms = import_reference()
     irs = load_irs()
+    if a.only in (None, "progress"):
+        progress(ms, irs)
     if a.only in (None, "pins"):
         pins(ms, irs)
     if a.only in (None, "renders"):

@@ -15,3 +15,4 @@ print("H48", sys.argv[1], "step", d["ms_per_step"], "value", d["value"],
       {k: t[k] for k in t if k.startswith("host")})
 PY
 done
+timeout -k 10 200 python -u -m pytest tests/test_gpu_parity.py -k "progress or gated or two_engines" -v --timeout 120 --timeout-method thread 2>&1 | tail -6
