@@ -587,7 +587,7 @@ def parse():
                     help="enqueue the contexts' sub-batches from one host thread each (threads) or in turn")
     ap.add_argument("--points", default="H48,C4,C5",
                     help="secondary configs timed after the headline (comma list, '' = none)")
-    ap.add_argument("--point-steps", type=int, default=3)
+    ap.add_argument("--point-steps", type=int, default=10)
     ap.add_argument("--dry-run", type=float, default=0.0, metavar="MS",
                     help="CPU launcher test: a step sleeps MS*(rank+1) ms instead of rendering")
     return ap.parse_args()
