@@ -51,6 +51,19 @@ constexpr int GEN_G = MSG_GEN_G;   // chunks of 64 draws classified per pass
 #ifndef MSG_GEN_LDS
 #define MSG_GEN_LDS 1
 #endif
+// Emission of a chunk (tuning macro): 2 = the resonant value from per-group chunk
+// bases and a 128-entry offset table, rank by v_mbcnt, the valid lanes as the
+// exec mask; 1 = the round-2 form (the chunk's base evaluated per chunk, rank by
+// popcount); 0 = cost experiment only (raw normals, wrong output).
+#ifndef MSG_GEN_NOSLOW
+#define MSG_GEN_NOSLOW 0
+#endif
+#ifndef MSG_GEN_EMIT
+#define MSG_GEN_EMIT 2
+#endif
+#if MSG_GEN_EMIT != 1 && !MSG_GEN_LDS
+#error "MSG_GEN_EMIT 0/2 need MSG_GEN_LDS"
+#endif
 // Jump-ahead constants and the ziggurat fast-path table (ki >> 20, wi * 2^20 as
 // float32 bits).
 struct JumpTab { nprng::u128 a[GEN_T]; nprng::u128 s[GEN_T]; nprng::u128 a64, s64, aG, sG; uint2 kw[256]; };
@@ -155,7 +168,12 @@ k_gen_normal(const msg_preset* __restrict__ presets, const msg_event* __restrict
     __shared__ uint64_t s_ki[256];
     __shared__ double s_wi[256];
     __shared__ uint2 s_kw[256];          // (ki >> 20, wi * 2^20 as float32 bits): the fast path's one read
+#if MSG_GEN_EMIT == 2
+    __shared__ float4 s_rot[128];        // resonant: (cos, sin)(2 pi r f/sr), 0.9 * 2^(r k_ring), 0.25 * 2^(r k_exc), r = i - 64
+    __shared__ float4 s_grp[GEN_G];      // resonant: (sin, cos, 2^(j k_ring), 2^(j k_exc)) at j = group start + 64 g
+#else
     __shared__ float4 s_rot[64];         // resonant: (cos, sin)(2 pi r f/sr), 2^(r k_ring), 2^(r k_exc), r < 64
+#endif
 #else
     const uint64_t* __restrict__ s_ki = z.ki;
     const double* __restrict__ s_wi = z.wi;
@@ -198,6 +216,21 @@ k_gen_normal(const msg_preset* __restrict__ presets, const msg_event* __restrict
     // at j0 and the per-rank rotation/decay table (angle addition, one ds_read
     // per sample instead of the phase reduction, a sine and two exponentials).
     float4 rot = make_float4(0.f, 0.f, 0.f, 0.f);
+#if MSG_GEN_EMIT == 2
+    // Two-level form: the value at j = B + t (B = a group's chunk base, |t| < 64
+    // or t in [-64, 0) after slow draws shifted the chunk) is the rotation of the
+    // base's (sin, cos, decays) by the offset table entry t, with the 0.9 and
+    // 0.25 gains folded into the table.
+    if (!RAW64 && c.mode == MSG_GEN_RESONANT) {
+        for (int i = lane; i < 128; i += GEN_T) {
+            const float rf = (float)(i - 64);
+            const float ph = ring_phase(rf, c.fa, c.fb);
+            s_rot[i] = make_float4(__builtin_amdgcn_cosf(ph), __builtin_amdgcn_sinf(ph),
+                                   0.9f * __builtin_amdgcn_exp2f(rf * c.k_ring),
+                                   0.25f * __builtin_amdgcn_exp2f(rf * c.k_exc));
+        }
+    }
+#else
     if (!RAW64 && c.mode == MSG_GEN_RESONANT) {
         const float rf = (float)lane;
         const float ph = ring_phase(rf, c.fa, c.fb);
@@ -207,6 +240,7 @@ k_gen_normal(const msg_preset* __restrict__ presets, const msg_event* __restrict
         s_rot[lane] = rot;
 #endif
     }
+#endif
 
     // default_rng(seed + i): every lane computes the (uniform) seed state.
     const nprng::Pcg64 g0 = nprng::default_rng((uint64_t)(pr.seed + e.index));
@@ -274,6 +308,9 @@ k_gen_normal(const msg_preset* __restrict__ presets, const msg_event* __restrict
             F[g] = __ballot(fast);
             if (!fast) slow |= 1u << g;
         }
+#if MSG_GEN_NOSLOW                                // cost experiment only: slow draws left as classified
+        slow = 0;
+#endif
         while (slow) {                            // divergent: each lane walks its own slow draws
             const int gs = __builtin_ctz(slow);
             slow &= slow - 1;
@@ -293,6 +330,22 @@ k_gen_normal(const msg_preset* __restrict__ presets, const msg_event* __restrict
             for (int g = 0; g < G; ++g)
                 if (gs == g) { x[g] = (XT)v; consumed[g] = cn; }
         }
+#if MSG_GEN_EMIT == 2
+        // resonant: lanes g < G evaluate the group's chunk bases p0 + 64 g (one set
+        // of transcendentals per group instead of per chunk)
+        const bool reson = !RAW64 && c.mode == MSG_GEN_RESONANT;
+        const int p0 = produced;
+        if (reson) {
+            if (lane < G) {
+                const float jb = (float)(p0 + 64 * lane);
+                const float ph = ring_phase(jb, c.fa, c.fb);
+                s_grp[lane] = make_float4(__builtin_amdgcn_sinf(ph), __builtin_amdgcn_cosf(ph),
+                                          __builtin_amdgcn_exp2f(fmaxf(jb * c.k_ring, -126.f)),
+                                          __builtin_amdgcn_exp2f(fmaxf(jb * c.k_exc, -126.f)));
+            }
+            __syncthreads();                      // one wave: orders the LDS writes before the reads
+        }
+#endif
 #pragma unroll
         for (int g = 0; g < G; ++g) {
             if (local >= 64) { local -= 64; continue; }   // chunk consumed by an earlier slow normal
@@ -314,7 +367,50 @@ k_gen_normal(const msg_preset* __restrict__ presets, const msg_event* __restrict
                     const int j = produced + __popcll(valid & ((1ULL << lane) - 1));
                     if (j < n) out64[j] = x[g];
                 }
-            } else if (c.mode == MSG_GEN_RESONANT) {
+            }
+#if MSG_GEN_EMIT == 2
+            else {
+                // rank among the valid lanes (v_mbcnt), the valid mask as the exec mask
+                const int rk = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(valid >> 32),
+                                                              __builtin_amdgcn_mbcnt_lo((uint32_t)valid, 0u));
+                const bool vl = __builtin_amdgcn_inverse_ballot_w64(valid);
+                const int room = n - produced;    // uniform
+                float* __restrict__ ob = out + produced;
+                if (reson) {
+                    // j = produced + rk = B_g + (d + rk), d = produced - B_g in [-64, 0]
+                    const int d = produced - (p0 + 64 * g);
+                    float4 u;
+                    int off;
+                    if (d >= -64) {
+                        u = s_grp[g];
+                        off = d + 64;
+                    } else {                          // a slow normal spanned > 64 draws: exact base
+                        const float j0 = (float)produced;
+                        const float ph0 = ring_phase(j0, c.fa, c.fb);
+                        u = make_float4(__builtin_amdgcn_sinf(ph0), __builtin_amdgcn_cosf(ph0),
+                                        __builtin_amdgcn_exp2f(fmaxf(j0 * c.k_ring, -126.f)),
+                                        __builtin_amdgcn_exp2f(fmaxf(j0 * c.k_exc, -126.f)));
+                        off = 64;
+                    }
+                    const bool edge = produced < c.fade || produced + 64 > c.n - c.fade;
+                    if (vl && rk < room) {
+                        const float4 tb = s_rot[rk + off];
+                        float v = fmaf(u.x, tb.x, u.y * tb.y) * (u.z * tb.z) + x[g] * (u.w * tb.w);
+                        if (edge) v = gen_fade(c, produced + rk, v);
+                        ob[rk] = v;
+                    }
+                } else if (vl && rk < room) {
+                    ob[rk] = gen_basic_sample(c, produced + rk, (float)x[g]);
+                }
+            }
+#elif MSG_GEN_EMIT == 0
+            else {                                // cost experiment only: raw normals, no generator formula
+                const int rk = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(valid >> 32),
+                                                              __builtin_amdgcn_mbcnt_lo((uint32_t)valid, 0u));
+                if (__builtin_amdgcn_inverse_ballot_w64(valid) && rk < n - produced) out[produced + rk] = (float)x[g];
+            }
+#else
+            else if (c.mode == MSG_GEN_RESONANT) {
                 // chunk-uniform phase and decays at j0 = produced
                 const float j0 = (float)produced;
                 const float ph0 = ring_phase(j0, c.fa, c.fb);
@@ -343,6 +439,7 @@ k_gen_normal(const msg_preset* __restrict__ presets, const msg_event* __restrict
                     if (j < n) out[j] = gen_basic_sample(c, j, (float)x[g]);
                 }
             }
+#endif
             produced += __popcll(valid);
             local = pos - 64;
         }

@@ -427,3 +427,33 @@ def test_progress_messages_match_reference(msgpu, irs, full_renders):
         msgs = []
         msgpu.render(p, progress=lambda v, m: msgs.append([int(v), str(m)]))
         assert msgs == case["messages"], (name, msgs[:4], case["messages"][:4])
+
+
+@pytest.mark.parametrize("stretch,roll,cut", [(0.5, None, None), (2.0, 0.0, None), (4.0, None, 36000.0),
+                                              (4.0, 0.0, 37400.0), (1.0, None, None)])
+def test_spec3_band_pruned_vs_general(msgpu, irs, monkeypatch, stretch, roll, cut):
+    """The band-pruned 37 500-sample spectral kernel (k_spec3, default) against
+    the general compile-time-plan kernel (MSGPU_SPEC3=0): stretch below 1, at 1
+    and above, no roll-off, and stretched bands whose top bin ky nears M/2 (a
+    36 kHz or 37.4 kHz cutoff at x100 unfold, stretch x4).  Both match the
+    oracle at 1e-5 RMS and each other, audio and meta grain_last."""
+    from oracle import msound_oracle as O
+    kw = dict(seed=31, out_dur_s=0.1, partial_stretch=stretch)
+    if roll is not None:
+        kw["bandlimit_roll_hz"] = roll
+    if cut is not None:
+        kw["bandlimit_out_hz"] = cut
+    p = msgpu.config_params("C3", irs=irs, **kw)
+    got = {}
+    for flag in ("0", "1"):
+        monkeypatch.setenv("MSGPU_SPEC3", flag)
+        got[flag] = msgpu.render(p)
+    ref, ref_meta = O.render(p)
+    for flag, (audio, meta) in got.items():
+        err = rms(audio, ref)
+        g = np.asarray(meta["grain_last"], np.float64)
+        gref = np.asarray(ref_meta["grain_last"], np.float64)
+        gerr = float(np.sqrt(np.mean((g - gref) ** 2)) / max(1e-30, np.sqrt(np.mean(gref ** 2))))
+        print(f"stretch {stretch} roll {roll} cut {cut} MSGPU_SPEC3={flag}: audio rms {err:.3e}, grain rel {gerr:.3e}")
+        assert err <= RMS_TOL and gerr <= 1e-5
+    assert rms(got["0"][0], got["1"][0]) <= RMS_TOL
