@@ -66,10 +66,15 @@ constexpr int GEN_G = MSG_GEN_G;   // chunks of 64 draws classified per pass
 #endif
 // Jump-ahead constants and the ziggurat fast-path table (ki >> 20, wi * 2^20 as
 // float32 bits).
-struct JumpTab { nprng::u128 a[GEN_T]; nprng::u128 s[GEN_T]; nprng::u128 a64, s64, aG, sG; uint2 kw[256]; };
+struct JumpTab { nprng::u128 a[GEN_T]; nprng::u128 s[GEN_T]; nprng::u128 a64, s64, aG, sG; uint2 kw[256]; float fif[256]; };
 
+// The slow part of NumPy's ziggurat normal (legacy_gauss / random_standard_normal,
+// the same walk as nprng::standard_normal) from a draw that missed the fast test.
+// ki / wi / fif are the LDS copies of the tables (fif: fi as float32); the global
+// float64 fi is read only when the wedge test is too close to call in float32.
 MSG_DEV double slow_normal(nprng::u128 st, nprng::u128 inc, uint64_t rabs, int idx, double x,
-                           const nprng::Zig& z, int& consumed) {
+                           const nprng::Zig& z, const uint64_t* ki, const double* wi, const float* fif,
+                           int& consumed) {
     nprng::Pcg64 g;
     g.state = st; g.inc = inc; g.has_u32 = 0; g.u32 = 0;
     int c = 1;
@@ -87,12 +92,19 @@ MSG_DEV double slow_normal(nprng::u128 st, nprng::u128 inc, uint64_t rabs, int i
         }
         const double u = nprng::next_double(g);
         c += 1;
-        // the wedge test lhs < exp(-x^2/2): decided by the hardware exp2 unless the
-        // two sides are within 1e-5 (its error is ~1e-6 relative), then in float64
-        const double lhs = (z.fi[idx - 1] - z.fi[idx]) * u + z.fi[idx];
-        const double ef = (double)__builtin_amdgcn_exp2f((float)(-0.72134752044448170 * x * x));
-        const double dd = lhs - ef;
-        const bool accept = fabs(dd) > 1e-5 * ef ? dd < 0.0 : lhs < exp(-0.5 * x * x);
+        // the wedge test lhs < exp(-x^2/2), decided in float32 (lhs from the float32
+        // table: relative error <~ 3e-7; the hardware exp2: ~1e-6) unless the two
+        // sides are within 2e-5, then in float64 from the float64 table
+        const float lhf = fmaf(fif[idx - 1] - fif[idx], (float)u, fif[idx]);
+        const float ef = __builtin_amdgcn_exp2f((float)(-0.72134752044448170 * x * x));
+        const float dd = lhf - ef;
+        bool accept;
+        if (fabsf(dd) > 2e-5f * ef) {
+            accept = dd < 0.f;
+        } else {
+            const double lhs = (z.fi[idx - 1] - z.fi[idx]) * u + z.fi[idx];
+            accept = lhs < exp(-0.5 * x * x);
+        }
         if (accept) { consumed = c; return x; }
         uint64_t r = nprng::next_u64(g);
         c += 1;
@@ -100,9 +112,9 @@ MSG_DEV double slow_normal(nprng::u128 st, nprng::u128 inc, uint64_t rabs, int i
         r >>= 8;
         const int sign = (int)(r & 1);
         rabs = (r >> 1) & 0x000fffffffffffffULL;
-        x = (double)rabs * z.wi[idx];
+        x = (double)rabs * wi[idx];
         if (sign) x = -x;
-        if (rabs < z.ki[idx]) { consumed = c; return x; }
+        if (rabs < ki[idx]) { consumed = c; return x; }
     }
 }
 
@@ -168,6 +180,7 @@ k_gen_normal(const msg_preset* __restrict__ presets, const msg_event* __restrict
     __shared__ uint64_t s_ki[256];
     __shared__ double s_wi[256];
     __shared__ uint2 s_kw[256];          // (ki >> 20, wi * 2^20 as float32 bits): the fast path's one read
+    __shared__ float s_fif[256];         // fi as float32: the slow path's wedge test
 #if MSG_GEN_EMIT == 2
     __shared__ float4 s_rot[128];        // resonant: (cos, sin)(2 pi r f/sr), 0.9 * 2^(r k_ring), 0.25 * 2^(r k_exc), r = i - 64
     __shared__ float4 s_grp[GEN_G];      // resonant: (sin, cos, 2^(j k_ring), 2^(j k_exc)) at j = group start + 64 g
@@ -178,6 +191,7 @@ k_gen_normal(const msg_preset* __restrict__ presets, const msg_event* __restrict
     const uint64_t* __restrict__ s_ki = z.ki;
     const double* __restrict__ s_wi = z.wi;
     const uint2* __restrict__ s_kw = jt->kw;
+    const float* __restrict__ s_fif = jt->fif;
 #endif
     const int li = blockIdx.x;
     if (li >= n_list) return;
@@ -187,6 +201,7 @@ k_gen_normal(const msg_preset* __restrict__ presets, const msg_event* __restrict
         s_ki[i] = z.ki[i];
         s_wi[i] = z.wi[i];
         s_kw[i] = jt->kw[i];
+        s_fif[i] = jt->fif[i];
     }
 #endif
     const msg_event& e = events[ev_list[li]];
@@ -325,7 +340,7 @@ k_gen_normal(const msg_preset* __restrict__ presets, const msg_event* __restrict
             double xv = (double)ra * s_wi[id];
             if ((raw >> 8) & 1) xv = -xv;
             int cn = 1;
-            const double v = slow_normal(s0, inc, ra, id, xv, z, cn);
+            const double v = slow_normal(s0, inc, ra, id, xv, z, s_ki, s_wi, s_fif, cn);
 #pragma unroll
             for (int g = 0; g < G; ++g)
                 if (gs == g) { x[g] = (XT)v; consumed[g] = cn; }

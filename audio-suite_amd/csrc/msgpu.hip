@@ -621,6 +621,7 @@ msg_ctx* msg_create(int device_ordinal) {
         uint32_t wb;
         memcpy(&wb, &w, 4);
         jt.kw[i] = make_uint2((uint32_t)(zig_ki_double[i] >> 20), wb);
+        jt.fif[i] = (float)zig_fi_double[i];
     }
     if (!up(ctx->d_jump, &jt, 1)) { g_err = "uploading jump table failed"; return nullptr; }
     for (int i = 0; i < 5; ++i) {
