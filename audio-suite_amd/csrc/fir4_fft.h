@@ -27,7 +27,82 @@
 template <int M> struct Fir4Cfg;
 template <> struct Fir4Cfg<16384> { static constexpr int R1 = 16, R2 = 16, R3 = 8, R4 = 8; };
 
-template <int S> MSG_HD constexpr int pads(int x) { return S ? x + x / S : x; }
+// Exchange-buffer layouts.  S > 0: one pad slot per S elements.  S < 0: XOR
+// swizzles that keep the buffer unpadded and every access of the k_fir4 engine
+// bank-conflict-free in the MI355X_MICROARCH.md LDS model (tools/lds_banks_fir8.py):
+//   -16  x ^ ((x >> 4) & 15)        pass-1 writes of 16 consecutive, reads of consecutive
+//    -8  x ^ ((x >> 4) & 7)         pass-1' writes of 8 consecutive, reads of consecutive
+//    -1  x ^ (((x >> 6) & 1) << 3)  pass-2' writes of 8-runs at stride 8 (NS R = 64), consecutive reads
+// (additive pads cannot serve both sides of E1 / E1': the reads of 32 consecutive
+// elements wrap the 64 banks when a pad falls inside them).  The swizzles move
+// bits below 8 only, so lay(x + r NB) = lay(x) + r NB for the 1024-multiples NB.
+template <int S> MSG_HD constexpr int pads(int x) {
+    if constexpr (S > 0) return x + x / S;
+    else if constexpr (S == -16) return x ^ ((x >> 4) & 15);
+    else if constexpr (S == -8) return x ^ ((x >> 4) & 7);
+    else if constexpr (S == -1) return x ^ (((x >> 6) & 1) << 3);
+    else return x;
+}
+// x[i] of a uniform base with the byte offset formed in 32 bits, so the load or
+// store takes the base in SGPRs (a 64-bit index costs two VALU per access).
+template <class T> MSG_DEV T& at32(T* base, uint32_t i) {
+    return *reinterpret_cast<T*>(reinterpret_cast<char*>(base) + i * (uint32_t)sizeof(T));
+}
+template <class T> MSG_DEV const T& at32(const T* base, uint32_t i) {
+    return *reinterpret_cast<const T*>(reinterpret_cast<const char*>(base) + i * (uint32_t)sizeof(T));
+}
+
+// Block epilogue of the overlap-save kernels: segment samples (u, u + 1) go to
+// frames t0 + d, d = u - (P - 1), kept for d in [0, span), span = min(n - t0,
+// B).  32-bit offsets from the block's (uniform) first frame, one unsigned
+// compare per value (d < 0 wraps), and the pair as one 8-byte store when P is
+// odd (d even) and the mono region is 8-byte aligned.
+struct SegOut {
+    float* yt;
+    uint32_t span;
+    bool pairs;
+    MSG_DEV void put(uint32_t d, float2 val) const {
+        if (pairs) {
+            if (d + 1 < span) *reinterpret_cast<float2*>(reinterpret_cast<char*>(yt) + d * 4u) = val;
+            else if (d < span) at32(yt, d) = val.x;
+        } else {
+            if (d < span) at32(yt, d) = val.x;
+            if (d + 1 < span) at32(yt, d + 1) = val.y;
+        }
+    }
+};
+MSG_DEV SegOut seg_out(float* y_out, int64_t y_off, int64_t t0, int64_t n, int B, int P) {
+    SegOut so;
+    so.yt = y_out + y_off + t0;
+    so.span = (uint32_t)(n - t0 < (int64_t)B ? n - t0 : (int64_t)B);
+    so.pairs = (P & 1) && ((y_off & 1) == 0);
+    return so;
+}
+
+// Pass-1 style writes of R consecutive elements from R j: element r at base + r
+// (pads) or base ^ r (swizzles, whose source bits lie above log2 R).
+template <int S, int R> MSG_DEV void put_run(float2* buf, int j, const float2 (&v)[R]) {
+    const int b = pads<S>(R * j);
+    if constexpr (S < 0) {
+#pragma unroll
+        for (int r = 0; r < R; ++r) buf[b ^ r] = v[r];
+    } else {
+#pragma unroll
+        for (int r = 0; r < R; ++r) buf[b + r] = v[r];
+    }
+}
+
+// Two-level twiddle table of Fir4Geo: w_M^j = hi[j >> 7] * lo[j & 127].  The lo
+// table is stored padded, lo[x] at x + (x >> 5): the radix-16 table passes and
+// the radix-8 power passes read lo at (e r) & 127 for power-of-two multiples e,
+// which the unpadded layout put on 2 - 8 banks of a 32-lane read group
+// (tools/lds_banks_fir8.py: 2240 -> 704 extra LDS cycles per forward + inverse
+// transform pair of k_fir8).
+constexpr int FIR4_LO = 132;                       // padded lo entries (127 + 3 + 1, rounded)
+MSG_HD constexpr int fir4_lo(int x) { return x + (x >> 5); }
+MSG_DEV float2 fir4_wM(const float2* tab, int lo, int hi, int j) {
+    return cmul(tab[hi + (j >> 7)], tab[lo + fir4_lo(j & 127)]);
+}
 
 // v[r] *= W_M^(e r), r = 1 .. R-1, W_M from the two-level table at (lo, hi).
 // Table twiddles: each is one product of two correctly rounded entries (~1 ulp,
@@ -43,10 +118,10 @@ template <int M, int R>
 MSG_DEV void fir_twiddle(float2 (&v)[R], const float2* tab, int lo, int hi, int e) {
     if constexpr (MSG_FIR_TWTAB == 1 || (MSG_FIR_TWTAB == 2 && R >= 16)) {
 #pragma unroll
-        for (int r = 1; r < R; ++r) v[r] = cmul(v[r], fir_wM(tab, lo, hi, (e * r) & (M - 1)));
+        for (int r = 1; r < R; ++r) v[r] = cmul(v[r], fir4_wM(tab, lo, hi, (e * r) & (M - 1)));
     } else {
         constexpr int B = tw_base<R>();
-        twiddle_pow_ab<R, B>(v, fir_wM(tab, lo, hi, e), fir_wM(tab, lo, hi, (e * B) & (M - 1)));
+        twiddle_pow_ab<R, B>(v, fir4_wM(tab, lo, hi, e), fir4_wM(tab, lo, hi, (e * B) & (M - 1)));
     }
 }
 
@@ -58,23 +133,24 @@ template <int M> struct Fir4Geo {
     static constexpr int BP1 = NB1 / T, BP2 = NB2 / T, BP3 = NB3 / T;
     static_assert(NB1 % T == 0 && NB2 % T == 0 && NB3 % T == 0 && NB4 == 2 * T, "FIR4 plan");
     // exchange pads: forward E1..E3, inverse E1'..E3'
-#ifndef MSG_FIR4_PADS   // tuning builds: exchange pads S2, S3, S2I, S3I (S1 = R1, S1I = R4 fixed)
-#define MSG_FIR4_PADS 0, 0, 8, 0
+#ifndef MSG_FIR4_PADS   // tuning builds: exchange layouts S1, S2, S3, S1I, S2I, S3I (pads()); round 2: 16, 0, 0, 8, 8, 0
+#define MSG_FIR4_PADS -16, 0, 0, -8, -1, 0
 #endif
-    static constexpr int PADS_[4] = {MSG_FIR4_PADS};
-    static constexpr int S1 = 16, S2 = PADS_[0], S3 = PADS_[1], S1I = 8, S2I = PADS_[2], S3I = PADS_[3];
-    static_assert(S1 == R1 && S1I == R4, "pass-1 writes of R consecutive elements: pad S = R");
+    static constexpr int PADS_[6] = {MSG_FIR4_PADS};
+    static constexpr int S1 = PADS_[0], S2 = PADS_[1], S3 = PADS_[2], S1I = PADS_[3], S2I = PADS_[4], S3I = PADS_[5];
+    static_assert((S1 == R1 || S1 == -16) && (S1I == R4 || S1I == -8), "pass-1 writes of R consecutive elements");
+    static_assert(S2I != -1 || R3 * R4 == 64, "swizzle -1: pass-2' writes of 8-runs at stride 8");
     // twiddle tables at LDS offset 0 (float2 entries): exact [r][k] tables for the
     // two passes with small NS, two-level w_M and w_2M tables for the rest
     static constexpr int OFF_TA = 0;                    // forward pass 2: radix R2, NS = R1, [R2][R1]
     static constexpr int OFF_TB = OFF_TA + R2 * R1;     // inverse pass 2': radix R3, NS = R4, [R3][R4]
-    static constexpr int OFF_MLO = OFF_TB + R3 * R4;    // w_M^x, x < 128
-    static constexpr int OFF_MHI = OFF_MLO + 128;       // w_M^(128 x), x < M / 128
-    static constexpr int OFF_PLO = OFF_MHI + M / 128;   // w_2M^x, x < 128
-    static constexpr int OFF_PHI = OFF_PLO + 128;       // w_2M^(128 x), 128 x <= NB4
+    static constexpr int OFF_MLO = OFF_TB + R3 * R4;    // w_M^x, x < 128 (at fir4_lo(x))
+    static constexpr int OFF_MHI = OFF_MLO + FIR4_LO;   // w_M^(128 x), x < M / 128
+    static constexpr int OFF_PLO = OFF_MHI + M / 128;   // w_2M^x, x < 128 (at fir4_lo(x))
+    static constexpr int OFF_PHI = OFF_PLO + FIR4_LO;   // w_2M^(128 x), 128 x <= NB4
     static constexpr int TAB_USED = OFF_PHI + NB4 / 128 + 1;
     static constexpr int TAB = (TAB_USED + 15) & ~15;
-    static constexpr int BUF = M + M / 8;
+    static constexpr int BUF = M + ((S1 > 0 || S2 > 0 || S3 > 0 || S1I > 0 || S2I > 0 || S3I > 0) ? M / 8 : 0);
     static constexpr int LDS_BYTES = (TAB + BUF) * 8;
     static_assert(LDS_BYTES <= 163840, "FIR4 LDS budget");
 };
@@ -107,8 +183,14 @@ MSG_DEV void fir4_pass_lds(float2* buf, const float2* tab, int t) {
         }
         Dft<R, false>::run(v[b]);
         const int lo = q * NS * R + k;
+        if constexpr (SO == -1) {                   // lo + r NS = lo | r NS (NS R = 64): base ^ r NS
+            const int bb = lo | (((lo >> 6) & 1) << 3);
 #pragma unroll
-        for (int r = 0; r < R; ++r) buf[pads<SO>(lo + r * NS)] = v[b][r];
+            for (int r = 0; r < R; ++r) buf[bb ^ (r * NS)] = v[b][r];
+        } else {
+#pragma unroll
+            for (int r = 0; r < R; ++r) buf[pads<SO>(lo + r * NS)] = v[b][r];
+        }
     }
 }
 
@@ -159,9 +241,7 @@ k_fir4(const PresetRt* __restrict__ rt, const int2* __restrict__ jobs, const flo
                 }
             }
             Dft<R1, false>::run(v);
-            const int base = pads<G::S1>(t * R1);
-#pragma unroll
-            for (int r = 0; r < R1; ++r) buf[base + r] = v[r];
+            put_run<G::S1, R1>(buf, t, v);
         }
         __syncthreads();
         // ---- passes 2, 3: LDS -> LDS (E1 -> E2 -> E3)
@@ -185,11 +265,11 @@ k_fir4(const PresetRt* __restrict__ rt, const int2* __restrict__ jobs, const flo
         // ---- real split, X . H_q accumulated in registers (k_fir2's pairing)
         const float2* H = hspec + pr.h_off + (int64_t)q * (M + 1);
         if (!t0z) {
-            const float2 wA = fir_wM(tab, G::OFF_PLO, G::OFF_PHI, js[0]);
+            const float2 wA = fir4_wM(tab, G::OFF_PLO, G::OFF_PHI, js[0]);
 #pragma unroll
             for (int r = 0; r < R4; ++r) {
                 const int kA = js[0] + r * NB4;
-                const float2 hk = H[(uint32_t)kA], hm = H[(uint32_t)(M - kA)];
+                const float2 hk = at32(H, kA), hm = at32(H, M - kA);
                 fir_pair_mac(v[0][r], v[1][R4 - 1 - r], cmul_k(wA, fir_cr<R4>(r)), hk, hm, acc[0][r],
                              acc[1][R4 - 1 - r]);
             }
@@ -200,7 +280,7 @@ k_fir4(const PresetRt* __restrict__ rt, const int2* __restrict__ jobs, const flo
 #pragma unroll
             for (int r = 0; r < R4; ++r) {
                 const int kA = fir_k0<M, R4>(r);
-                const float2 hk = H[(uint32_t)kA], hm = H[(uint32_t)(M - kA)];
+                const float2 hk = at32(H, kA), hm = at32(H, M - kA);
                 if (r < R4 - 1) {
                     fir_pair_mac(a[r], bb[R4 - 1 - r], fir_w0<M, R4>(r), hk, hm, acc[0][r], acc[1][R4 - 1 - r]);
                 } else {   // DC/Nyquist packed as (Y[0], Y[M]) and bin M/2
@@ -216,7 +296,7 @@ k_fir4(const PresetRt* __restrict__ rt, const int2* __restrict__ jobs, const flo
     {
         const int t = otid();
         if (t != 0) {
-            const float2 wA = fir_wM(tab, G::OFF_PLO, G::OFF_PHI, t);
+            const float2 wA = fir4_wM(tab, G::OFF_PLO, G::OFF_PHI, t);
 #pragma unroll
             for (int r = 0; r < R4; ++r) fir_pair_pre(acc[0][r], acc[1][R4 - 1 - r], cmul_k(wA, fir_cr<R4>(r)));
         } else {
@@ -233,9 +313,7 @@ k_fir4(const PresetRt* __restrict__ rt, const int2* __restrict__ jobs, const flo
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
         Dft<R4, false>::run(acc[h]);
-        const int base = pads<G::S1I>(js[h] * R4);
-#pragma unroll
-        for (int r = 0; r < R4; ++r) buf[base + r] = acc[h][r];
+        put_run<G::S1I, R4>(buf, js[h], acc[h]);
     }
     __syncthreads();
     // ---- passes 2', 3': LDS -> LDS (E1' -> E2' -> E3')
@@ -244,7 +322,6 @@ k_fir4(const PresetRt* __restrict__ rt, const int2* __restrict__ jobs, const flo
     fir4_pass_lds<M, R2, R4 * R3, G::BP2, G::S2I, G::S3I, false, 0>(buf, tab, t);
     __syncthreads();
     // ---- pass 4': LDS (E3') -> DFT_R1 -> output block (samples u >= P-1 of the segment)
-    float* y = y_out + pr.y_off;
     const float s = 1.0f / (float)M;
     {
         float2 v[R1];
@@ -252,13 +329,10 @@ k_fir4(const PresetRt* __restrict__ rt, const int2* __restrict__ jobs, const flo
         for (int r = 0; r < R1; ++r) v[r] = buf[pads<G::S3I>(t + r * NB1)];
         fir_twiddle<M, R1>(v, tab, G::OFF_MLO, G::OFF_MHI, t);
         Dft<R1, false>::run(v);
+        const SegOut so = seg_out(y_out, pr.y_off, t0, n, 2 * M - P + 1, P);
 #pragma unroll
-        for (int r = 0; r < R1; ++r) {
-            const int u = 2 * (t + r * NB1);                 // z[u/2] = x[u] + i x[u+1]
-            const int64_t o = t0 + u - (P - 1);
-            if (u >= P - 1 && o < n) y[(uint32_t)o] = v[r].x * s;
-            if (u + 1 >= P - 1 && o + 1 < n) y[(uint32_t)(o + 1)] = -v[r].y * s;
-        }
+        for (int r = 0; r < R1; ++r)                         // z[u/2] = x[u] + i x[u+1], u = 2 (t + r NB1)
+            so.put((uint32_t)(2 * (t + r * NB1) - (P - 1)), make_float2(v[r].x * s, -v[r].y * s));
     }
 }
 
@@ -350,9 +424,7 @@ MSG_DEV void fir4s_forward(float2* buf, const float2* tab, const float* x, int64
             }
         }
         Dft<R1, false>::run(u);
-        const int base = pads<G::S1>(t * R1);
-#pragma unroll
-        for (int r = 0; r < R1; ++r) buf[base + r] = u[r];
+        put_run<G::S1, R1>(buf, t, u);
     }
     __syncthreads();
     fir4_pass_lds<M, R2, R1, G::BP2, G::S1, G::S2, true, G::OFF_TA>(buf, tab, t);
@@ -371,7 +443,7 @@ MSG_DEV void fir4s_forward(float2* buf, const float2* tab, const float* x, int64
         Dft<R4, false>::run(v[h]);
     }
     if (!t0z) {
-        const float2 wA = fir_wM(tab, G::OFF_PLO, G::OFF_PHI, js[0]);
+        const float2 wA = fir4_wM(tab, G::OFF_PLO, G::OFF_PHI, js[0]);
 #pragma unroll
         for (int r = 0; r < R4; ++r) {
             float2 xk, xm;
@@ -402,8 +474,8 @@ MSG_DEV void fir4s_mac(float2 (&acc)[2][Fir4Geo<M>::R4], const float2 (&v)[2][Fi
 #pragma unroll
         for (int r = 0; r < R4; ++r) {
             const int kA = t + r * NB4;
-            acc[0][r] = cfma(acc[0][r], v[0][r], H[(uint32_t)kA]);
-            acc[1][R4 - 1 - r] = cfma(acc[1][R4 - 1 - r], v[1][R4 - 1 - r], H[(uint32_t)(M - kA)]);
+            acc[0][r] = cfma(acc[0][r], v[0][r], at32(H, kA));
+            acc[1][R4 - 1 - r] = cfma(acc[1][R4 - 1 - r], v[1][R4 - 1 - r], at32(H, M - kA));
         }
     } else {
 #pragma unroll
@@ -455,7 +527,7 @@ k_fir4s(const PresetRt* __restrict__ rt, const int2* __restrict__ jobs, const fl
         {
             const int t = otid();
             if (t != 0) {
-                const float2 wA = fir_wM(tab, G::OFF_PLO, G::OFF_PHI, t);
+                const float2 wA = fir4_wM(tab, G::OFF_PLO, G::OFF_PHI, t);
 #pragma unroll
                 for (int r = 0; r < R4; ++r) fir_pair_pre(acc[0][r], acc[1][R4 - 1 - r], cmul_k(wA, fir_cr<R4>(r)));
             } else {
@@ -469,9 +541,7 @@ k_fir4s(const PresetRt* __restrict__ rt, const int2* __restrict__ jobs, const fl
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
                 Dft<R4, false>::run(acc[h]);
-                const int base = pads<G::S1I>(js[h] * R4);
-#pragma unroll
-                for (int r = 0; r < R4; ++r) buf[base + r] = acc[h][r];
+                put_run<G::S1I, R4>(buf, js[h], acc[h]);
             }
         }
         // ---- A <- X_b . H_1 (Y_b is in LDS; X_b dies here)
@@ -536,8 +606,8 @@ k_fir4_hpart(const PresetRt* __restrict__ rt, const int2* __restrict__ jobs, con
 #pragma unroll
         for (int k = 0; k < R4; ++k) {
             const int kA = t + k * NB4;
-            H[(uint32_t)kA] = v[0][k];
-            H[(uint32_t)(M - kA)] = v[1][R4 - 1 - k];
+            at32(H, kA) = v[0][k];
+            at32(H, M - kA) = v[1][R4 - 1 - k];
         }
     } else {   // thread 0's slot layout (fir4s_forward): (X[0], X[M]) packed, X[M/2]
 #pragma unroll
@@ -567,8 +637,8 @@ inline void fir4_tables(std::vector<float>& out) {
         for (int k = 0; k < G::R1; ++k) put(G::OFF_TA + r * G::R1 + k, (long double)k * r, (long double)G::R1 * G::R2);
     for (int r = 0; r < G::R3; ++r)
         for (int k = 0; k < G::R4; ++k) put(G::OFF_TB + r * G::R4 + k, (long double)k * r, (long double)G::R4 * G::R3);
-    for (int x = 0; x < 128; ++x) put(G::OFF_MLO + x, x, M);
+    for (int x = 0; x < 128; ++x) put(G::OFF_MLO + fir4_lo(x), x, M);
     for (int x = 0; x < M / 128; ++x) put(G::OFF_MHI + x, 128.0L * x, M);
-    for (int x = 0; x < 128; ++x) put(G::OFF_PLO + x, x, 2.0L * M);
+    for (int x = 0; x < 128; ++x) put(G::OFF_PLO + fir4_lo(x), x, 2.0L * M);
     for (int x = 0; x <= G::NB4 / 128; ++x) put(G::OFF_PHI + x, 128.0L * x, 2.0L * M);
 }

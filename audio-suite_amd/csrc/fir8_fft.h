@@ -60,9 +60,7 @@ MSG_DEV void fwd_half(float2* buf, const float2* tab, float2 (&in)[R1], float2 (
     const int t = otid();
     Dft<R1, false>::run(in);
     {
-        const int base = pads<G::S1>(t * R1);
-#pragma unroll
-        for (int r = 0; r < R1; ++r) buf[base + r] = in[r];
+        put_run<G::S1, R1>(buf, t, in);
     }
     __syncthreads();
     fir4_pass_lds<MH, R2, R1, G::BP2, G::S1, G::S2, true, G::OFF_TA>(buf, tab, t);
@@ -93,9 +91,7 @@ MSG_DEV void inv_half(float2* buf, const float2* tab, float2 (&acc)[2][R4], floa
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
         Dft<R4, false>::run(acc[h]);
-        const int base = pads<G::S1I>(js[h] * R4);
-#pragma unroll
-        for (int r = 0; r < R4; ++r) buf[base + r] = acc[h][r];
+        put_run<G::S1I, R4>(buf, js[h], acc[h]);
     }
     __syncthreads();
     fir4_pass_lds<MH, R3, R4, G::BP3, G::S1I, G::S2I, true, G::OFF_TB>(buf, tab, t);
@@ -119,12 +115,12 @@ MSG_DEV void even_mac_pre(const float2* tab, const float2 (&v)[2][R4], const flo
 #pragma unroll
         for (int r = 0; r < R4; ++r) acc[h][r] = make_float2(0.f, 0.f);
     if (t != 0) {
-        const float2 wA = fir_wM(tab, G::OFF_PLO, G::OFF_PHI, t);
+        const float2 wA = fir4_wM(tab, G::OFF_PLO, G::OFF_PHI, t);
 #pragma unroll
         for (int r = 0; r < R4; ++r) {
             const int kA = t + r * NB4;
             const float2 wk = cmul_k(wA, fir_cr<R4>(r));
-            fir_pair_mac(v[0][r], v[1][R4 - 1 - r], wk, He[(uint32_t)kA], He[(uint32_t)(MH - kA)], acc[0][r],
+            fir_pair_mac(v[0][r], v[1][R4 - 1 - r], wk, at32(He, kA), at32(He, MH - kA), acc[0][r],
                          acc[1][R4 - 1 - r]);
             fir_pair_pre(acc[0][r], acc[1][R4 - 1 - r], wk);
         }
@@ -155,15 +151,15 @@ MSG_DEV void even_mac_pre(const float2* tab, const float2 (&v)[2][R4], const flo
 MSG_DEV void odd_mac_pre(const float2* tab, const float2 (&v)[2][R4], const float2* __restrict__ Ho,
                          float2 (&acc)[2][R4]) {
     const int t = otid();
-    const float2 wA = cmul_k(fir_wM(tab, G::OFF_PLO, G::OFF_PHI, t), wN1());   // W_N^(2t+1)
+    const float2 wA = cmul_k(fir4_wM(tab, G::OFF_PLO, G::OFF_PHI, t), wN1());   // W_N^(2t+1)
 #pragma unroll
     for (int r = 0; r < R4; ++r) {
         const int kA = t + r * NB4;
         const float2 wk = cmul_k(wA, fir_cr<R4>(r));
         float2 xk, xm;
         fir_split(v[0][r], v[1][R4 - 1 - r], wk, xk, xm);
-        acc[0][r] = cmul(xk, Ho[(uint32_t)kA]);
-        acc[1][R4 - 1 - r] = cmul(xm, Ho[(uint32_t)(MH - 1 - kA)]);
+        acc[0][r] = cmul(xk, at32(Ho, kA));
+        acc[1][R4 - 1 - r] = cmul(xm, at32(Ho, MH - 1 - kA));
         fir_pair_pre(acc[0][r], acc[1][R4 - 1 - r], wk);
     }
 }
@@ -172,22 +168,27 @@ MSG_DEV void odd_mac_pre(const float2* tab, const float2 (&v)[2][R4], const floa
 // outside [0, n)) into a and (z0 - z1) into b (twiddled after the tables are in LDS).
 MSG_DEV void load_halves(const float* __restrict__ x, int64_t n, int64_t s0, float2 (&a)[R1], float2 (&b)[R1]) {
     const int t = otid();
-    const bool fast = s0 >= 0 && s0 + N <= n && (((uintptr_t)(x + s0)) & 7) == 0;
-    if (fast) {
-        const float2* z = reinterpret_cast<const float2*>(x + s0);
+    // segment samples u in [ulo, ulo + cnt) lie inside [0, n); 32-bit offsets from
+    // xs = x + s0 (uniform), so every load takes its base in SGPRs
+    const int64_t hi = n - s0 < (int64_t)N ? n - s0 : (int64_t)N;
+    const uint32_t ulo = s0 < 0 ? (uint32_t)(-s0) : 0u;
+    const uint32_t cnt = hi > (int64_t)ulo ? (uint32_t)(hi - ulo) : 0u;
+    const float* xs = x + s0;
+    if (ulo == 0 && cnt == (uint32_t)N && (((uintptr_t)xs) & 7) == 0) {
+        const float2* z = reinterpret_cast<const float2*>(xs);
 #pragma unroll
         for (int r = 0; r < R1; ++r) {
-            a[r] = z[(uint32_t)(t + r * NB1)];
-            b[r] = z[(uint32_t)(t + r * NB1 + MH)];
+            a[r] = at32(z, t + r * NB1);
+            b[r] = at32(z, t + r * NB1 + MH);
         }
-    } else {
+    } else {                                          // the first and last blocks of a signal
 #pragma unroll
         for (int r = 0; r < R1; ++r) {
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
-                const int64_t i = s0 + 2 * (int64_t)(t + r * NB1 + h * MH);
-                const bool in0 = i >= 0 && i < n, in1 = i + 1 >= 0 && i + 1 < n;
-                const float x0 = x[(uint32_t)(in0 ? i : 0)], x1 = x[(uint32_t)(in1 ? i + 1 : 0)];
+                const uint32_t u = 2u * (uint32_t)(t + r * NB1 + h * MH);
+                const bool in0 = u - ulo < cnt, in1 = u + 1 - ulo < cnt;
+                const float x0 = at32(xs, in0 ? u : ulo), x1 = at32(xs, in1 ? u + 1 : ulo);
                 (h ? b : a)[r] = make_float2(in0 ? x0 : 0.f, in1 ? x1 : 0.f);
             }
         }
@@ -196,7 +197,7 @@ MSG_DEV void load_halves(const float* __restrict__ x, int64_t n, int64_t s0, flo
 
 // (a, b) <- (a + b, (a - b) W_M^(t + r NB1))
 MSG_DEV void dif_split(const float2* tab, float2 (&a)[R1], float2 (&b)[R1]) {
-    const float2 wt = fir_wM(tab, G::OFF_PLO, G::OFF_PHI, otid());   // W_M^t (PLO/PHI: W_{2 MH} = W_M)
+    const float2 wt = fir4_wM(tab, G::OFF_PLO, G::OFF_PHI, otid());   // W_M^t (PLO/PHI: W_{2 MH} = W_M)
 #pragma unroll
     for (int r = 0; r < R1; ++r) {
         const float2 z0 = a[r], z1 = b[r];
@@ -237,20 +238,17 @@ k_fir8(const PresetRt* __restrict__ rt, const int2* __restrict__ jobs, const flo
     inv_half<true>(buf, tab, acc, B);
     // F[m] = A + W_M^m B, F[m + MH] = A - W_M^m B; z'[m] = conj(F[m]) / M
     const int t = otid();
-    const float2 wt = fir_wM(tab, G::OFF_PLO, G::OFF_PHI, t);
-    float* y = y_out + pr.y_off;
+    const float2 wt = fir4_wM(tab, G::OFF_PLO, G::OFF_PHI, t);
+    const SegOut so = seg_out(y_out, pr.y_off, t0, n, N - P + 1, P);
+    const int d0 = 2 * t - (P - 1);
     const float s = 1.0f / (float)M;
 #pragma unroll
     for (int r = 0; r < R1; ++r) {
         const float2 wb = r == 0 ? cmul(B[r], wt) : cmul(B[r], cmul_k(wt, w32<R1>(r)));
         const float2 f[2] = {ff(vv(A[r]) + vv(wb)), ff(vv(A[r]) - vv(wb))};
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            const int u = 2 * (t + r * NB1 + h * MH);        // segment sample of z'[u/2]
-            const int64_t o = t0 + u - (P - 1);
-            if (u >= P - 1 && o < n) y[(uint32_t)o] = f[h].x * s;
-            if (u + 1 >= P - 1 && o + 1 < n) y[(uint32_t)(o + 1)] = -f[h].y * s;
-        }
+        for (int h = 0; h < 2; ++h)                   // segment sample u = 2 (t + r NB1 + h MH)
+            so.put((uint32_t)(d0 + 2 * (r * NB1 + h * MH)), make_float2(f[h].x * s, -f[h].y * s));
     }
 }
 
@@ -277,7 +275,7 @@ MSG_DEV void store_half(const float2* tab, const float2 (&v)[2][R4], const float
     const int t = otid();
     auto put = [&](int k, float2 x) { Hh[(uint32_t)k] = S ? cmul(x, S[(uint32_t)k]) : x; };
     if (ODD) {
-        const float2 wA = cmul_k(fir_wM(tab, G::OFF_PLO, G::OFF_PHI, t), wN1());
+        const float2 wA = cmul_k(fir4_wM(tab, G::OFF_PLO, G::OFF_PHI, t), wN1());
 #pragma unroll
         for (int q = 0; q < R4; ++q) {
             const int kA = t + q * NB4;
@@ -287,7 +285,7 @@ MSG_DEV void store_half(const float2* tab, const float2 (&v)[2][R4], const float
             put(MH - 1 - kA, xm);
         }
     } else if (t != 0) {
-        const float2 wA = fir_wM(tab, G::OFF_PLO, G::OFF_PHI, t);
+        const float2 wA = fir4_wM(tab, G::OFF_PLO, G::OFF_PHI, t);
 #pragma unroll
         for (int q = 0; q < R4; ++q) {
             const int kA = t + q * NB4;
@@ -329,7 +327,7 @@ MSG_DEV void load_half(const float2* tab, const T* __restrict__ x, int64_t n, fl
         in[r] = ODD ? ff(vv(z[0]) - vv(z[1])) : ff(vv(z[0]) + vv(z[1]));
     }
     if (ODD) {
-        const float2 wt = fir_wM(tab, G::OFF_PLO, G::OFF_PHI, t);
+        const float2 wt = fir4_wM(tab, G::OFF_PLO, G::OFF_PHI, t);
 #pragma unroll
         for (int r = 0; r < R1; ++r) in[r] = r == 0 ? cmul(in[r], wt) : cmul(in[r], cmul_k(wt, w32<R1>(r)));
     }
@@ -392,7 +390,7 @@ k_fir8_hconv(const PresetRt* __restrict__ rt, const int32_t* __restrict__ list, 
 #pragma unroll
     for (int q = 0; q < R1; ++q) in[q] = buf[t + q * NB1];
     if (odd) {
-        const float2 wt = fir_wM(tab, G::OFF_PLO, G::OFF_PHI, t);
+        const float2 wt = fir4_wM(tab, G::OFF_PLO, G::OFF_PHI, t);
 #pragma unroll
         for (int q = 0; q < R1; ++q) in[q] = q == 0 ? cmul(in[q], wt) : cmul(in[q], cmul_k(wt, w32<R1>(q)));
     }
