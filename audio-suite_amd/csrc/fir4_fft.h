@@ -125,6 +125,16 @@ MSG_DEV void fir_twiddle(float2 (&v)[R], const float2* tab, int lo, int hi, int 
     }
 }
 
+// v[r] *= w_M^(t r), r = 1 .. R-1, t = 64 a + b < T, from the split tables at
+// (oa, ob): w_M^(64 a r) at oa + r (T/64) + a, w_M^(b r) at ob + r 64 + b.
+template <int R, int T>
+MSG_DEV void fir_twiddle_t(float2 (&v)[R], const float2* tab, int oa, int ob, int t) {
+    const float2* ta = tab + oa + (t >> 6);
+    const float2* tb = tab + ob + (t & 63);
+#pragma unroll
+    for (int r = 1; r < R; ++r) v[r] = cmul(v[r], cmul(ta[r * (T / 64)], tb[r * 64]));
+}
+
 template <int M> struct Fir4Geo {
     static constexpr int R1 = Fir4Cfg<M>::R1, R2 = Fir4Cfg<M>::R2, R3 = Fir4Cfg<M>::R3, R4 = Fir4Cfg<M>::R4;
     static_assert(R1 * R2 * R3 * R4 == M, "four passes");
@@ -148,7 +158,12 @@ template <int M> struct Fir4Geo {
     static constexpr int OFF_MHI = OFF_MLO + FIR4_LO;   // w_M^(128 x), x < M / 128
     static constexpr int OFF_PLO = OFF_MHI + M / 128;   // w_2M^x, x < 128 (at fir4_lo(x))
     static constexpr int OFF_PHI = OFF_PLO + FIR4_LO;   // w_2M^(128 x), 128 x <= NB4
-    static constexpr int TAB_USED = OFF_PHI + NB4 / 128 + 1;
+    static constexpr int OFF_TC = OFF_PHI + NB4 / 128 + 1;   // inverse pass 3': radix R2, NS = R4 R3, [R2][R4 R3]
+    // inverse pass 4' (radix R1, twiddle w_M^(t r), t < T): w_M^(64 a r) [R1][T/64] times w_M^(b r) [R1][64],
+    // t = 64 a + b -- one product of two table entries at fixed offsets, no index arithmetic
+    static constexpr int OFF_T4A = OFF_TC + R2 * R4 * R3;
+    static constexpr int OFF_T4B = OFF_T4A + R1 * (T / 64);
+    static constexpr int TAB_USED = OFF_T4B + R1 * 64;
     static constexpr int TAB = (TAB_USED + 15) & ~15;
     static constexpr int BUF = M + ((S1 > 0 || S2 > 0 || S3 > 0 || S1I > 0 || S2I > 0 || S3I > 0) ? M / 8 : 0);
     static constexpr int LDS_BYTES = (TAB + BUF) * 8;
@@ -319,7 +334,7 @@ k_fir4(const PresetRt* __restrict__ rt, const int2* __restrict__ jobs, const flo
     // ---- passes 2', 3': LDS -> LDS (E1' -> E2' -> E3')
     fir4_pass_lds<M, R3, R4, G::BP3, G::S1I, G::S2I, true, G::OFF_TB>(buf, tab, t);
     __syncthreads();
-    fir4_pass_lds<M, R2, R4 * R3, G::BP2, G::S2I, G::S3I, false, 0>(buf, tab, t);
+    fir4_pass_lds<M, R2, R4 * R3, G::BP2, G::S2I, G::S3I, true, G::OFF_TC>(buf, tab, t);
     __syncthreads();
     // ---- pass 4': LDS (E3') -> DFT_R1 -> output block (samples u >= P-1 of the segment)
     const float s = 1.0f / (float)M;
@@ -327,7 +342,7 @@ k_fir4(const PresetRt* __restrict__ rt, const int2* __restrict__ jobs, const flo
         float2 v[R1];
 #pragma unroll
         for (int r = 0; r < R1; ++r) v[r] = buf[pads<G::S3I>(t + r * NB1)];
-        fir_twiddle<M, R1>(v, tab, G::OFF_MLO, G::OFF_MHI, t);
+        fir_twiddle_t<R1, T>(v, tab, G::OFF_T4A, G::OFF_T4B, t);
         Dft<R1, false>::run(v);
         const SegOut so = seg_out(y_out, pr.y_off, t0, n, 2 * M - P + 1, P);
 #pragma unroll
@@ -554,7 +569,7 @@ k_fir4s(const PresetRt* __restrict__ rt, const int2* __restrict__ jobs, const fl
         const int t = otid();
         fir4_pass_lds<M, G::R3, R4, G::BP3, G::S1I, G::S2I, true, G::OFF_TB>(buf, tab, t);
         __syncthreads();
-        fir4_pass_lds<M, G::R2, R4 * G::R3, G::BP2, G::S2I, G::S3I, false, 0>(buf, tab, t);
+        fir4_pass_lds<M, G::R2, R4 * G::R3, G::BP2, G::S2I, G::S3I, true, G::OFF_TC>(buf, tab, t);
         __syncthreads();
         // ---- pass 4': LDS (E3') -> DFT_R1 -> outputs [t0, t0 + P) (segment samples u >= P-1)
         {
@@ -562,7 +577,7 @@ k_fir4s(const PresetRt* __restrict__ rt, const int2* __restrict__ jobs, const fl
             float2 u[R1];
 #pragma unroll
             for (int r = 0; r < R1; ++r) u[r] = buf[pads<G::S3I>(t + r * NB1)];
-            fir_twiddle<M, R1>(u, tab, G::OFF_MLO, G::OFF_MHI, t);
+            fir_twiddle_t<R1, T>(u, tab, G::OFF_T4A, G::OFF_T4B, t);
             Dft<R1, false>::run(u);
 #pragma unroll
             for (int r = 0; r < R1; ++r) {
@@ -641,4 +656,11 @@ inline void fir4_tables(std::vector<float>& out) {
     for (int x = 0; x < M / 128; ++x) put(G::OFF_MHI + x, 128.0L * x, M);
     for (int x = 0; x < 128; ++x) put(G::OFF_PLO + fir4_lo(x), x, 2.0L * M);
     for (int x = 0; x <= G::NB4 / 128; ++x) put(G::OFF_PHI + x, 128.0L * x, 2.0L * M);
+    for (int r = 0; r < G::R2; ++r)
+        for (int k = 0; k < G::R4 * G::R3; ++k)
+            put(G::OFF_TC + r * G::R4 * G::R3 + k, (long double)k * r, (long double)G::R4 * G::R3 * G::R2);
+    for (int r = 0; r < G::R1; ++r) {
+        for (int a = 0; a < G::T / 64; ++a) put(G::OFF_T4A + r * (G::T / 64) + a, (long double)((64 * a * r) % M), M);
+        for (int b = 0; b < 64; ++b) put(G::OFF_T4B + r * 64 + b, (long double)b * r, M);
+    }
 }

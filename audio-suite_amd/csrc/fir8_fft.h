@@ -96,12 +96,12 @@ MSG_DEV void inv_half(float2* buf, const float2* tab, float2 (&acc)[2][R4], floa
     __syncthreads();
     fir4_pass_lds<MH, R3, R4, G::BP3, G::S1I, G::S2I, true, G::OFF_TB>(buf, tab, t);
     __syncthreads();
-    fir4_pass_lds<MH, R2, R4 * R3, G::BP2, G::S2I, G::S3I, false, 0>(buf, tab, t);
+    fir4_pass_lds<MH, R2, R4 * R3, G::BP2, G::S2I, G::S3I, true, G::OFF_TC>(buf, tab, t);
     __syncthreads();
 #pragma unroll
     for (int r = 0; r < R1; ++r) u[r] = buf[pads<G::S3I>(t + r * NB1)];
     __syncthreads();   // LDS free for the next half
-    fir_twiddle<MH, R1>(u, tab, G::OFF_MLO, G::OFF_MHI, t);
+    fir_twiddle_t<R1, T>(u, tab, G::OFF_T4A, G::OFF_T4B, t);
     Dft<R1, false>::run(u);
 }
 
