@@ -125,15 +125,22 @@ MSG_DEV void fir_twiddle(float2 (&v)[R], const float2* tab, int lo, int hi, int 
     }
 }
 
-// v[r] *= w_M^(t r), r = 1 .. R-1, t = 64 a + b < T, from the split tables at
-// (oa, ob): w_M^(64 a r) at oa + r (T/64) + a, w_M^(b r) at ob + r 64 + b.
-template <int R, int T>
-MSG_DEV void fir_twiddle_t(float2 (&v)[R], const float2* tab, int oa, int ob, int t) {
-    const float2* ta = tab + oa + (t >> 6);
-    const float2* tb = tab + ob + (t & 63);
+// v[r] *= w_M^(e r), r = 1 .. R-1, e = 64 a + b < 64 NA, from the split tables at
+// (oa, ob): w_M^(64 a r) at oa + r NA + a, w_M^(b r) at ob + r 64 + b.
+template <int R, int NA>
+MSG_DEV void fir_twiddle_t(float2 (&v)[R], const float2* tab, int oa, int ob, int e) {
+    const float2* ta = tab + oa + (e >> 6);
+    const float2* tb = tab + ob + (e & 63);
 #pragma unroll
-    for (int r = 1; r < R; ++r) v[r] = cmul(v[r], cmul(ta[r * (T / 64)], tb[r * 64]));
+    for (int r = 1; r < R; ++r) v[r] = cmul(v[r], cmul(ta[r * NA], tb[r * 64]));
 }
+
+// Forward pass 4's twiddles (radix R4, exponent j < NB4): split tables (1, one
+// product of two correctly rounded entries) or powers of two two-level table
+// values (0, twiddle_pow_ab: up to ~3 roundings at R = 8).  Tuning macro.
+#ifndef MSG_FIR_P4TAB
+#define MSG_FIR_P4TAB 1
+#endif
 
 template <int M> struct Fir4Geo {
     static constexpr int R1 = Fir4Cfg<M>::R1, R2 = Fir4Cfg<M>::R2, R3 = Fir4Cfg<M>::R3, R4 = Fir4Cfg<M>::R4;
@@ -163,12 +170,25 @@ template <int M> struct Fir4Geo {
     // t = 64 a + b -- one product of two table entries at fixed offsets, no index arithmetic
     static constexpr int OFF_T4A = OFF_TC + R2 * R4 * R3;
     static constexpr int OFF_T4B = OFF_T4A + R1 * (T / 64);
-    static constexpr int TAB_USED = OFF_T4B + R1 * 64;
+    // forward pass 4 (radix R4, w_M^(j r), j < NB4): the same split, [R4][NB4/64] and [R4][64]
+    static constexpr int OFF_T5A = OFF_T4B + R1 * 64;
+    static constexpr int OFF_T5B = OFF_T5A + R4 * (NB4 / 64);
+    static constexpr int TAB_USED = OFF_T5B + R4 * 64;
     static constexpr int TAB = (TAB_USED + 15) & ~15;
     static constexpr int BUF = M + ((S1 > 0 || S2 > 0 || S3 > 0 || S1I > 0 || S2I > 0 || S3I > 0) ? M / 8 : 0);
     static constexpr int LDS_BYTES = (TAB + BUF) * 8;
     static_assert(LDS_BYTES <= 163840, "FIR4 LDS budget");
 };
+
+template <int M, int R4>
+MSG_DEV void fir_twiddle_p4(float2 (&v)[R4], const float2* tab, int j) {
+    using G = Fir4Geo<M>;
+#if MSG_FIR_P4TAB
+    fir_twiddle_t<R4, G::NB4 / 64>(v, tab, G::OFF_T5A, G::OFF_T5B, j);
+#else
+    fir_twiddle<M, R4>(v, tab, G::OFF_MLO, G::OFF_MHI, j);
+#endif
+}
 
 // One radix-R Stockham pass LDS -> LDS on the 1024-thread grid.  TW: the
 // twiddles w_{NS R}^{k r} from the exact [r][k] table at OFF_T (TAB = true) or
@@ -274,7 +294,7 @@ k_fir4(const PresetRt* __restrict__ rt, const int2* __restrict__ jobs, const flo
         __syncthreads();   // LDS free for the next segment / the inverse
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
-            fir_twiddle<M, R4>(v[h], tab, G::OFF_MLO, G::OFF_MHI, js[h]);
+            fir_twiddle_p4<M, R4>(v[h], tab, js[h]);
             Dft<R4, false>::run(v[h]);
         }
         // ---- real split, X . H_q accumulated in registers (k_fir2's pairing)
@@ -342,7 +362,7 @@ k_fir4(const PresetRt* __restrict__ rt, const int2* __restrict__ jobs, const flo
         float2 v[R1];
 #pragma unroll
         for (int r = 0; r < R1; ++r) v[r] = buf[pads<G::S3I>(t + r * NB1)];
-        fir_twiddle_t<R1, T>(v, tab, G::OFF_T4A, G::OFF_T4B, t);
+        fir_twiddle_t<R1, T / 64>(v, tab, G::OFF_T4A, G::OFF_T4B, t);
         Dft<R1, false>::run(v);
         const SegOut so = seg_out(y_out, pr.y_off, t0, n, 2 * M - P + 1, P);
 #pragma unroll
@@ -454,7 +474,7 @@ MSG_DEV void fir4s_forward(float2* buf, const float2* tab, const float* x, int64
     __syncthreads();   // LDS free for the inverse
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-        fir_twiddle<M, R4>(v[h], tab, G::OFF_MLO, G::OFF_MHI, js[h]);
+        fir_twiddle_p4<M, R4>(v[h], tab, js[h]);
         Dft<R4, false>::run(v[h]);
     }
     if (!t0z) {
@@ -577,7 +597,7 @@ k_fir4s(const PresetRt* __restrict__ rt, const int2* __restrict__ jobs, const fl
             float2 u[R1];
 #pragma unroll
             for (int r = 0; r < R1; ++r) u[r] = buf[pads<G::S3I>(t + r * NB1)];
-            fir_twiddle_t<R1, T>(u, tab, G::OFF_T4A, G::OFF_T4B, t);
+            fir_twiddle_t<R1, T / 64>(u, tab, G::OFF_T4A, G::OFF_T4B, t);
             Dft<R1, false>::run(u);
 #pragma unroll
             for (int r = 0; r < R1; ++r) {
@@ -662,5 +682,9 @@ inline void fir4_tables(std::vector<float>& out) {
     for (int r = 0; r < G::R1; ++r) {
         for (int a = 0; a < G::T / 64; ++a) put(G::OFF_T4A + r * (G::T / 64) + a, (long double)((64 * a * r) % M), M);
         for (int b = 0; b < 64; ++b) put(G::OFF_T4B + r * 64 + b, (long double)b * r, M);
+    }
+    for (int r = 0; r < G::R4; ++r) {
+        for (int a = 0; a < G::NB4 / 64; ++a) put(G::OFF_T5A + r * (G::NB4 / 64) + a, (long double)((64 * a * r) % M), M);
+        for (int b = 0; b < 64; ++b) put(G::OFF_T5B + r * 64 + b, (long double)b * r, M);
     }
 }

@@ -76,7 +76,7 @@ MSG_DEV void fwd_half(float2* buf, const float2* tab, float2 (&in)[R1], float2 (
     __syncthreads();   // LDS free for the inverse
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-        fir_twiddle<MH, R4>(v[h], tab, G::OFF_MLO, G::OFF_MHI, js[h]);
+        fir_twiddle_p4<MH, R4>(v[h], tab, js[h]);
         Dft<R4, false>::run(v[h]);
     }
 }
@@ -101,7 +101,7 @@ MSG_DEV void inv_half(float2* buf, const float2* tab, float2 (&acc)[2][R4], floa
 #pragma unroll
     for (int r = 0; r < R1; ++r) u[r] = buf[pads<G::S3I>(t + r * NB1)];
     __syncthreads();   // LDS free for the next half
-    fir_twiddle_t<R1, T>(u, tab, G::OFF_T4A, G::OFF_T4B, t);
+    fir_twiddle_t<R1, T / 64>(u, tab, G::OFF_T4A, G::OFF_T4B, t);
     Dft<R1, false>::run(u);
 }
 
