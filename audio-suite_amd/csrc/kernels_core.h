@@ -230,7 +230,6 @@ k_gen_normal(const msg_preset* __restrict__ presets, const msg_event* __restrict
     // emitted, r = the lane's rank) from the chunk's uniform sin/cos and decay
     // at j0 and the per-rank rotation/decay table (angle addition, one ds_read
     // per sample instead of the phase reduction, a sine and two exponentials).
-    float4 rot = make_float4(0.f, 0.f, 0.f, 0.f);
 #if MSG_GEN_EMIT == 2
     // Two-level form: the value at j = B + t (B = a group's chunk base, |t| < 64
     // or t in [-64, 0) after slow draws shifted the chunk) is the rotation of the
@@ -246,6 +245,7 @@ k_gen_normal(const msg_preset* __restrict__ presets, const msg_event* __restrict
         }
     }
 #else
+    float4 rot = make_float4(0.f, 0.f, 0.f, 0.f);
     if (!RAW64 && c.mode == MSG_GEN_RESONANT) {
         const float rf = (float)lane;
         const float ph = ring_phase(rf, c.fa, c.fb);

@@ -539,16 +539,20 @@ static int g64_ops(const msg_preset& p, const msg_event& e) {
 }
 
 static void stage_mark(msg_ctx* ctx, int i, hipStream_t s) {
-    if (ctx->profiling) hipEventRecord(ctx->ev[ctx->ev_cur][i], s);
-    if (ctx->gate_wait < 0 && ctx->gate_rec < 0) return;
-    std::lock_guard<std::mutex> lk(g_gate_mu);   // the peer may be unlinked by msg_destroy
-    if (ctx->gate_peer) {
-        if (i == ctx->gate_wait && ctx->gate_peer->gate_armed.load()) hipStreamWaitEvent(s, ctx->gate_peer->gate_ev, 0);
-        if (i == ctx->gate_rec) {
-            hipEventRecord(ctx->gate_ev, s);
-            ctx->gate_armed.store(true);
+    if (ctx->gate_wait >= 0 || ctx->gate_rec >= 0) {
+        std::lock_guard<std::mutex> lk(g_gate_mu);   // the peer may be unlinked by msg_destroy
+        if (ctx->gate_peer) {
+            // the gate's wait comes before the stage's profiling event, so a stage's
+            // time is its kernels' span on the stream, not the time it was held
+            if (i == ctx->gate_wait && ctx->gate_peer->gate_armed.load())
+                hipStreamWaitEvent(s, ctx->gate_peer->gate_ev, 0);
+            if (i == ctx->gate_rec) {
+                hipEventRecord(ctx->gate_ev, s);
+                ctx->gate_armed.store(true);
+            }
         }
     }
+    if (ctx->profiling) hipEventRecord(ctx->ev[ctx->ev_cur][i], s);
 }
 
 // A batch on a different stream than the context's last one waits for that
