@@ -71,3 +71,27 @@ def test_fir_errors():
         eng.fir(x, np.ones(10), out=x)
     with pytest.raises(NotImplementedError):
         eng.fir(x, np.ones(64 * 32768))
+
+
+@pytest.mark.parametrize("M", [16383, 16384, 25473, 40000])
+def test_fir8_block_edges_and_alignment(M):
+    """k_fir8's block epilogue and edge-block loads: odd and even tap counts (the
+    output pairs are written as 8-byte stores only for odd P and an 8-byte-aligned
+    row), an odd signal length so that every other row of the batch starts at an
+    odd float offset (misaligned loads and single stores), and a length that is
+    not a multiple of the block."""
+    import torch
+    from msgpu.engine import default_engine
+    from oracle import msound_oracle as O
+    n, S = 100001, 3
+    h = O.synthetic_fir_taps(M)
+    x = np.stack([np.random.default_rng(7 + b).standard_normal(n).astype(np.float32) for b in range(S)])
+    y, (N, P, Q) = default_engine(0).fir(torch.from_numpy(x).cuda(), h)
+    torch.cuda.synchronize()
+    assert (N, Q) == (65536, 1) and P == M        # one partition on k_fir8
+    y = y.cpu().numpy()
+    for b in range(S):
+        e = _rel_rms(y[b], _ref(x[b], h))
+        print(f"M={M} row {b}: rel rms {e:.3e}")
+        assert e <= REL, (M, b)
+        assert np.all(np.isfinite(y[b]))
