@@ -168,41 +168,15 @@ template <class P> MSG_HD constexpr bool s3_band_fits(int kz, int ky) {
     return ((kz + 15) & ~15) + 2 * ((ky + 15) & ~15) + 16 <= P::BUF && 2 * ((kz + 15) & ~15) <= P::BUF;
 }
 
+// Everything of one event after forward pass 1 (exchange A written, barrier
+// passed): pass 2, the band, the inverse and the grain store.
 template <class P>
-__global__ void __launch_bounds__(P::T)
-k_spec3(const msg_event* __restrict__ events, const EventRt* __restrict__ ert, const PresetRt* __restrict__ rt,
-        const float2* __restrict__ tables, const int32_t* __restrict__ ev_list, int n_list,
-        const float* __restrict__ micro_pool, float* __restrict__ grain_pool) {
+MSG_DEV void s3_rest(float2* buf, const float2* tab, const EventRt* __restrict__ ert, int ei, int64_t off,
+                     float* __restrict__ grain_pool) {
     constexpr int M = P::M, T = P::T, K = P::K;
-    extern __shared__ __attribute__((aligned(16))) float2 lds[];
-    float2* tab = lds;
-    float2* buf = lds + P::TAB;
-    const int li = blockIdx.x;
-    if (li >= n_list) return;
-    const int ei = ev_list[li];
-    const msg_event& e = events[ei];
-    const PresetRt& pr = rt[e.preset];
-    const int64_t off = pr.pool_base + e.pool_off;   // even (n even, 16-B aligned preset regions)
+    (void)K;
     SPEC_STAMP_INIT;
     int j = otid();
-
-    // ---- forward pass 1: the packed grain z[i] = x[2i] + i x[2i+1] from HBM
-    // (the grain's loads are issued before the twiddle tables' so both share
-    // one memory latency)
-    {
-        const float2* z = reinterpret_cast<const float2*>(micro_pool + off);
-        float2 v[P::R1];
-        if (j < P::NB1) {
-#pragma unroll
-            for (int r = 0; r < P::R1; ++r) v[r] = z[j + r * P::NB1];
-        }
-        for (int i = threadIdx.x; i < P::TAB_USED; i += T) tab[i] = tables[i];
-        if (j < P::NB1) {
-            Dft<P::R1, false>::run(v);
-            s3_store_a<P>(buf, v, j);
-        }
-    }
-    __syncthreads();
     SPEC_STAMP(0);
     s3_pass2<P>(buf, tab);
     SPEC_STAMP(1);
@@ -318,6 +292,72 @@ k_spec3(const msg_event* __restrict__ events, const EventRt* __restrict__ ert, c
         for (int r = 0; r < P::R3; ++r) g[j + r * P::NB3] = make_float2(v[r].x * s, -v[r].y * s);
     }
     SPEC_STAMP(6);
+}
+
+// Forward pass 1 of an event from its packed grain in registers (exchange A).
+template <class P> MSG_DEV void s3_first(float2* buf, float2 (&v)[P::R1]) {
+    const int j = otid();
+    if (j < P::NB1) {
+        Dft<P::R1, false>::run(v);
+        s3_store_a<P>(buf, v, j);
+    }
+}
+template <class P>
+MSG_DEV void s3_load(const msg_event* __restrict__ events, const PresetRt* __restrict__ rt, const int32_t* __restrict__ ev_list,
+                     int li, const float* __restrict__ micro_pool, float2 (&v)[P::R1]) {
+    const msg_event& e = events[ev_list[li]];
+    const float2* z = reinterpret_cast<const float2*>(micro_pool + rt[e.preset].pool_base + e.pool_off);
+    const int j = otid();
+    if (j < P::NB1) {
+#pragma unroll
+        for (int r = 0; r < P::R1; ++r) v[r] = z[j + r * P::NB1];
+    }
+}
+
+// One workgroup takes events li and li + gridDim.x (MSG_S3_PAIR = 1): the
+// second event's grain is loaded into registers right after the first one's
+// pass 1, so its HBM latency hides behind the first event (one 158 KB
+// workgroup per CU leaves nothing else to cover it), and the twiddle tables
+// are staged once for both.  Written out twice rather than as a loop: an event
+// loop lets LLVM hoist every DFT and band constant out of the loop (100 VGPRs of
+// spills).  MSG_S3_PAIR = 0: one event per workgroup.
+#ifndef MSG_S3_PAIR
+#define MSG_S3_PAIR 1
+#endif
+template <class P>
+__global__ void __launch_bounds__(P::T)
+k_spec3(const msg_event* __restrict__ events, const EventRt* __restrict__ ert, const PresetRt* __restrict__ rt,
+        const float2* __restrict__ tables, const int32_t* __restrict__ ev_list, int n_list,
+        const float* __restrict__ micro_pool, float* __restrict__ grain_pool) {
+    constexpr int T = P::T;
+    extern __shared__ __attribute__((aligned(16))) float2 lds[];
+    float2* tab = lds;
+    float2* buf = lds + P::TAB;
+    const int li = blockIdx.x;
+    if (li >= n_list) return;
+    auto off_of = [&](int l) {
+        const msg_event& e = events[ev_list[l]];
+        return rt[e.preset].pool_base + e.pool_off;   // even (n even, 16-B aligned preset regions)
+    };
+    float2 v[P::R1];
+    // (the grain's loads are issued before the twiddle tables' so both share one memory latency)
+    s3_load<P>(events, rt, ev_list, li, micro_pool, v);
+    for (int i = threadIdx.x; i < P::TAB_USED; i += T) tab[i] = tables[i];
+    s3_first<P>(buf, v);
+    __syncthreads();
+#if MSG_S3_PAIR
+    const int l2 = li + (int)gridDim.x;
+    float2 pre[P::R1];
+    if (l2 < n_list) s3_load<P>(events, rt, ev_list, l2, micro_pool, pre);   // in flight through event li
+    s3_rest<P>(buf, tab, ert, ev_list[li], off_of(li), grain_pool);
+    if (l2 >= n_list) return;
+    __syncthreads();                                // exchange B read before the second pass 1 writes
+    s3_first<P>(buf, pre);
+    __syncthreads();
+    s3_rest<P>(buf, tab, ert, ev_list[l2], off_of(l2), grain_pool);
+#else
+    s3_rest<P>(buf, tab, ert, ev_list[li], off_of(li), grain_pool);
+#endif
 }
 
 // Host: twiddle tables (float64-built, rounded once).
