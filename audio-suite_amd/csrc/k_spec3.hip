@@ -30,9 +30,7 @@ hipError_t launch_spec3(unsigned grid, hipStream_t s, const msg_event* events, c
                         const float2* tables, const int32_t* ev_list, int n_list, const float* micro_pool,
                         float* grain_pool) {
     using P = Spec3P18750;
-#if MSG_S3_PAIR
-    grid = (unsigned)((n_list + 1) / 2);        // two events per workgroup (spec3.h)
-#endif
+    grid = (unsigned)((n_list + MSG_S3_EVENTS - 1) / MSG_S3_EVENTS);   // MSG_S3_EVENTS per workgroup (spec3.h)
     hipLaunchKernelGGL((k_spec3<P>), dim3(grid), dim3(P::T), P::LDS_BYTES, s, events, ert, rt, tables, ev_list,
                        n_list, micro_pool, grain_pool);
     return hipGetLastError();

@@ -314,16 +314,37 @@ MSG_DEV void s3_load(const msg_event* __restrict__ events, const PresetRt* __res
     }
 }
 
-// One workgroup takes events li and li + gridDim.x (MSG_S3_PAIR = 1): the
-// second event's grain is loaded into registers right after the first one's
-// pass 1, so its HBM latency hides behind the first event (one 158 KB
-// workgroup per CU leaves nothing else to cover it), and the twiddle tables
-// are staged once for both.  Written out twice rather than as a loop: an event
-// loop lets LLVM hoist every DFT and band constant out of the loop (100 VGPRs of
-// spills).  MSG_S3_PAIR = 0: one event per workgroup.
-#ifndef MSG_S3_PAIR
-#define MSG_S3_PAIR 1
+// Events li, li + G, li + 2G, ... (G = gridDim.x), MSG_S3_EVENTS of them, run
+// one after another in one workgroup: each next event's grain is loaded into
+// registers right after the current one's pass 1, so its HBM latency hides
+// behind the current event (one 158 KB workgroup per CU leaves nothing else to
+// cover it), and the twiddle tables are staged once.  Written as an inlined
+// template chain rather than a loop: an event loop lets LLVM hoist every DFT
+// and band constant out of the loop (100 VGPRs of spills).
+#ifndef MSG_S3_EVENTS
+#define MSG_S3_EVENTS 2
 #endif
+template <class P, int KE>
+MSG_DEV void s3_chain(float2* buf, const float2* tab, const msg_event* __restrict__ events,
+                      const EventRt* __restrict__ ert, const PresetRt* __restrict__ rt,
+                      const int32_t* __restrict__ ev_list, int n_list, const float* __restrict__ micro_pool,
+                      float* __restrict__ grain_pool, int li, float2 (&cur)[P::R1]) {
+    s3_first<P>(buf, cur);
+    __syncthreads();
+    const msg_event& e = events[ev_list[li]];
+    const int64_t off = rt[e.preset].pool_base + e.pool_off;   // even (n even, 16-B aligned preset regions)
+    if constexpr (KE > 1) {
+        const int l2 = li + (int)gridDim.x;
+        float2 pre[P::R1];
+        if (l2 < n_list) s3_load<P>(events, rt, ev_list, l2, micro_pool, pre);   // in flight through event li
+        s3_rest<P>(buf, tab, ert, ev_list[li], off, grain_pool);
+        if (l2 >= n_list) return;
+        __syncthreads();                            // exchange B read before the next pass 1 writes
+        s3_chain<P, KE - 1>(buf, tab, events, ert, rt, ev_list, n_list, micro_pool, grain_pool, l2, pre);
+    } else {
+        s3_rest<P>(buf, tab, ert, ev_list[li], off, grain_pool);
+    }
+}
 template <class P>
 __global__ void __launch_bounds__(P::T)
 k_spec3(const msg_event* __restrict__ events, const EventRt* __restrict__ ert, const PresetRt* __restrict__ rt,
@@ -335,29 +356,11 @@ k_spec3(const msg_event* __restrict__ events, const EventRt* __restrict__ ert, c
     float2* buf = lds + P::TAB;
     const int li = blockIdx.x;
     if (li >= n_list) return;
-    auto off_of = [&](int l) {
-        const msg_event& e = events[ev_list[l]];
-        return rt[e.preset].pool_base + e.pool_off;   // even (n even, 16-B aligned preset regions)
-    };
     float2 v[P::R1];
     // (the grain's loads are issued before the twiddle tables' so both share one memory latency)
     s3_load<P>(events, rt, ev_list, li, micro_pool, v);
     for (int i = threadIdx.x; i < P::TAB_USED; i += T) tab[i] = tables[i];
-    s3_first<P>(buf, v);
-    __syncthreads();
-#if MSG_S3_PAIR
-    const int l2 = li + (int)gridDim.x;
-    float2 pre[P::R1];
-    if (l2 < n_list) s3_load<P>(events, rt, ev_list, l2, micro_pool, pre);   // in flight through event li
-    s3_rest<P>(buf, tab, ert, ev_list[li], off_of(li), grain_pool);
-    if (l2 >= n_list) return;
-    __syncthreads();                                // exchange B read before the second pass 1 writes
-    s3_first<P>(buf, pre);
-    __syncthreads();
-    s3_rest<P>(buf, tab, ert, ev_list[l2], off_of(l2), grain_pool);
-#else
-    s3_rest<P>(buf, tab, ert, ev_list[li], off_of(li), grain_pool);
-#endif
+    s3_chain<P, MSG_S3_EVENTS>(buf, tab, events, ert, rt, ev_list, n_list, micro_pool, grain_pool, li, v);
 }
 
 // Host: twiddle tables (float64-built, rounded once).
