@@ -43,15 +43,6 @@ template <int S> MSG_HD constexpr int pads(int x) {
     else if constexpr (S == -1) return x ^ (((x >> 6) & 1) << 3);
     else return x;
 }
-// x[i] of a uniform base with the byte offset formed in 32 bits, so the load or
-// store takes the base in SGPRs (a 64-bit index costs two VALU per access).
-template <class T> MSG_DEV T& at32(T* base, uint32_t i) {
-    return *reinterpret_cast<T*>(reinterpret_cast<char*>(base) + i * (uint32_t)sizeof(T));
-}
-template <class T> MSG_DEV const T& at32(const T* base, uint32_t i) {
-    return *reinterpret_cast<const T*>(reinterpret_cast<const char*>(base) + i * (uint32_t)sizeof(T));
-}
-
 // Block epilogue of the overlap-save kernels: segment samples (u, u + 1) go to
 // frames t0 + d, d = u - (P - 1), kept for d in [0, span), span = min(n - t0,
 // B).  32-bit offsets from the block's (uniform) first frame, one unsigned

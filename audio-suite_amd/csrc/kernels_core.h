@@ -605,13 +605,27 @@ MSG_DEV int mod_n(int64_t i, int64_t n) {
 // store waits on them.
 template <int PER>
 MSG_DEV void stereo_load(const float* __restrict__ y, int n, int b0, int len, float (&v)[PER]) {
+    if (b0 + len <= n) {                       // no wrap (nearly every tile): one base, 32-bit offsets
+        const float* yb = y + b0;
 #pragma unroll
-    for (int i = 0; i < PER; ++i) {
-        const int u = threadIdx.x + i * ST_T;
-        int j = b0 + u;
-        if (n >= len) { if (j >= n) j -= n; }   // one wrap at most
-        else j %= n;
-        v[i] = u < len ? y[j] : 0.f;
+        for (int i = 0; i < PER; ++i) {
+            const int u = threadIdx.x + i * ST_T;
+            v[i] = u < len ? at32(yb, (uint32_t)u) : 0.f;
+        }
+    } else if (n >= len) {                     // one wrap at most
+#pragma unroll
+        for (int i = 0; i < PER; ++i) {
+            const int u = threadIdx.x + i * ST_T;
+            int j = b0 + u;
+            if (j >= n) j -= n;
+            v[i] = u < len ? at32(y, (uint32_t)j) : 0.f;
+        }
+    } else {
+#pragma unroll
+        for (int i = 0; i < PER; ++i) {
+            const int u = threadIdx.x + i * ST_T;
+            v[i] = u < len ? y[(b0 + u) % n] : 0.f;
+        }
     }
 }
 template <int PER>
@@ -726,12 +740,19 @@ k_stereo_max(const PresetRt* __restrict__ rt, const int32_t* __restrict__ st_beg
 // library tanhf's ~30 instructions; k_stereo_out runs two per frame):
 // 1 - 2 / (e^{2|x|} + 1), |error| <= ~2 float32 ulp of 1, and an odd Taylor
 // polynomial below |x| = 0.05 where the subtraction would lose relative digits.
+// MSG_TANH_TAYLOR = 0 drops the polynomial: below |x| = 0.05 the subtraction's
+// absolute error stays ~1e-7 of the unit peak, far inside the 1e-5 RMS bar.
+#ifndef MSG_TANH_TAYLOR
+#define MSG_TANH_TAYLOR 1
+#endif
 MSG_DEV float tanh_fast(float x) {
     const float ax = fabsf(x);
     const float e = __builtin_amdgcn_exp2f(fminf(2.8853900817779268f * ax, 126.f));   // e^{2|x|}
     float t = 1.0f - 2.0f * __builtin_amdgcn_rcpf(e + 1.0f);
+#if MSG_TANH_TAYLOR
     const float x2 = ax * ax;
     if (ax < 0.05f) t = ax * fmaf(x2, fmaf(x2, 0.13333333f, -0.33333333f), 1.0f);
+#endif
     return copysignf(t, x);
 }
 MSG_DEV float sat(float v, float d, float inv_td) { return d > 0.f ? tanh_fast(v * d) * inv_td : v; }
@@ -745,12 +766,14 @@ MSG_DEV f2p tanh_fast2(f2p x) {
     const f2p e1 = f2p{__builtin_amdgcn_exp2f(a.x), __builtin_amdgcn_exp2f(a.y)} + 1.0f;
     const f2p r = f2p{__builtin_amdgcn_rcpf(e1.x), __builtin_amdgcn_rcpf(e1.y)};
     f2p t = 1.0f - 2.0f * r;
+#if MSG_TANH_TAYLOR
     const f2p x2 = ax * ax;
     const f2p tp = ax * __builtin_elementwise_fma(x2, __builtin_elementwise_fma(x2, f2p{0.13333333f, 0.13333333f},
                                                                                 f2p{-0.33333333f, -0.33333333f}),
                                                   f2p{1.0f, 1.0f});
     t.x = ax.x < 0.05f ? tp.x : t.x;
     t.y = ax.y < 0.05f ? tp.y : t.y;
+#endif
     return __builtin_elementwise_copysign(t, x);
 }
 
@@ -808,13 +831,13 @@ k_stereo_out(const PresetRt* __restrict__ rt, const int32_t* __restrict__ st_beg
             for (int k = 0; k < 4; ++k) v[k] = make_float2(L[k] * scale, R[k] * scale);
         }
         if (o16 && u + 4 <= st.cnt) {
-            float4* o4 = reinterpret_cast<float4*>(o + u);
+            float4* o4 = reinterpret_cast<float4*>(reinterpret_cast<char*>(o) + (uint32_t)u * 8u);   // 32-bit offset
             o4[0] = make_float4(v[0].x, v[0].y, v[1].x, v[1].y);
             o4[1] = make_float4(v[2].x, v[2].y, v[3].x, v[3].y);
         } else {
 #pragma unroll
             for (int k = 0; k < 4; ++k)
-                if (u + k < st.cnt) o[u + k] = v[k];
+                if (u + k < st.cnt) at32(o, (uint32_t)(u + k)) = v[k];
         }
     }
 }

@@ -13,6 +13,17 @@
 #include "plan.h"
 #include "fft_lds.h"
 
+#if defined(__HIPCC__)
+// x[i] of a uniform base with the byte offset formed in 32 bits, so the load or
+// store takes the base in SGPRs (a 64-bit index costs two VALU per access).
+template <class T> MSG_DEV T& at32(T* base, uint32_t i) {
+    return *reinterpret_cast<T*>(reinterpret_cast<char*>(base) + i * (uint32_t)sizeof(T));
+}
+template <class T> MSG_DEV const T& at32(const T* base, uint32_t i) {
+    return *reinterpret_cast<const T*>(reinterpret_cast<const char*>(base) + i * (uint32_t)sizeof(T));
+}
+#endif
+
 // Per-preset runtime record, built on the host after planning.
 struct PresetRt {
     int64_t out_n;
