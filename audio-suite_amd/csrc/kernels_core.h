@@ -45,6 +45,17 @@ __global__ void k_plan_events(const msg_preset* __restrict__ presets, int n_pres
 #define MSG_GEN_G 8
 #endif
 constexpr int GEN_G = MSG_GEN_G;   // chunks of 64 draws classified per pass
+// Waves per event (MSG_GEN_K): wave w of an event's workgroup takes groups
+// w, w + K, w + 2K, ... of its draw stream.  Classification (the fast test and
+// the slow normals) does not depend on where the parse stands, only the walk
+// does; each wave walks its group as if no earlier slow normal reached into it,
+// and after one barrier per round every wave scans the K (count, overhang)
+// pairs; a group whose predecessor's last slow normal does reach into it walks
+// again from that overhang (rare: the last draws of a group must be slow).
+#ifndef MSG_GEN_K
+#define MSG_GEN_K 1
+#endif
+constexpr int GEN_K = MSG_GEN_K;
 // MSG_GEN_LDS=0 (tuning builds): the ziggurat tables are read through L1 and the
 // resonant rotation by cross-lane reads, so k_gen_normal allocates no LDS and its
 // waves can sit beside k_spec3's 162 KB workgroups.
@@ -66,7 +77,43 @@ constexpr int GEN_G = MSG_GEN_G;   // chunks of 64 draws classified per pass
 #endif
 // Jump-ahead constants and the ziggurat fast-path table (ki >> 20, wi * 2^20 as
 // float32 bits).
-struct JumpTab { nprng::u128 a[GEN_T]; nprng::u128 s[GEN_T]; nprng::u128 a64, s64, aG, sG; uint2 kw[256]; float fif[256]; };
+struct JumpTab {
+    nprng::u128 a[GEN_T]; nprng::u128 s[GEN_T]; nprng::u128 a64, s64, aG, sG;
+    nprng::u128 aW[GEN_K], sW[GEN_K];   // jump by w groups (wave w's first group)
+    nprng::u128 aR, sR;                 // jump by K groups (one round)
+    uint2 kw[256]; float fif[256];
+};
+
+// The walk over one group's G chunks: from the first lane not consumed by an
+// earlier slow normal (local, >= 64 skips whole chunks), mark the draws each
+// slow normal consumed; bit g of a lane's vb = the lane's draw of chunk g starts
+// a normal (a VGPR, not 2 G SGPRs of masks), cnt = their number.  Returns the
+// overhang into the next group.  Wave-uniform apart from vb.
+template <int G>
+MSG_DEV int gen_walk(const uint64_t (&F)[G], const int (&consumed)[G], int local, uint32_t& vb, int& cnt) {
+    cnt = 0;
+    vb = 0;
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+        if (local >= 64) { local -= 64; continue; }   // chunk consumed by an earlier slow normal
+        uint64_t valid = ~0ULL << local;
+        uint64_t S = ~F[g] & valid;
+        int pos = 64;
+        while (S) {
+            const int q = __builtin_ctzll(S);
+            const int end = q + __builtin_amdgcn_readlane(consumed[g], q);
+            const uint64_t after_q = ~((2ULL << q) - 1);                  // lanes q+1..63
+            const uint64_t before_end = end >= 64 ? ~0ULL : ((1ULL << end) - 1);
+            valid &= ~(after_q & before_end);
+            if (end >= 64) { pos = end; break; }
+            S &= ~0ULL << end;
+        }
+        if (__builtin_amdgcn_inverse_ballot_w64(valid)) vb |= 1u << g;
+        cnt += __popcll(valid);
+        local = pos - 64;
+    }
+    return local;
+}
 
 // The slow part of NumPy's ziggurat normal (legacy_gauss / random_standard_normal,
 // the same walk as nprng::standard_normal) from a draw that missed the fast test.
@@ -171,7 +218,7 @@ MSG_DEV float gen_fade(const GenBasicConst& c, int j, float x) {
 #define MSG_GEN_WAVES 1
 #endif
 template <bool RAW64>
-__global__ void __launch_bounds__(GEN_T, MSG_GEN_WAVES)
+__global__ void __launch_bounds__(GEN_T * GEN_K, MSG_GEN_WAVES)
 k_gen_normal(const msg_preset* __restrict__ presets, const msg_event* __restrict__ events,
              const PresetRt* __restrict__ rt, const int32_t* __restrict__ ev_list, int n_list,
              nprng::Zig z, const JumpTab* __restrict__ jt, float* __restrict__ pool,
@@ -183,7 +230,7 @@ k_gen_normal(const msg_preset* __restrict__ presets, const msg_event* __restrict
     __shared__ float s_fif[256];         // fi as float32: the slow path's wedge test
 #if MSG_GEN_EMIT == 2
     __shared__ float4 s_rot[128];        // resonant: (cos, sin)(2 pi r f/sr), 0.9 * 2^(r k_ring), 0.25 * 2^(r k_exc), r = i - 64
-    __shared__ float4 s_grp[GEN_G];      // resonant: (sin, cos, 2^(j k_ring), 2^(j k_exc)) at j = group start + 64 g
+    __shared__ float4 s_grp[GEN_K][GEN_G];   // resonant, per wave: (sin, cos, 2^(j k_ring), 2^(j k_exc)) at j = group start + 64 g
 #else
     __shared__ float4 s_rot[64];         // resonant: (cos, sin)(2 pi r f/sr), 2^(r k_ring), 2^(r k_exc), r < 64
 #endif
@@ -195,9 +242,11 @@ k_gen_normal(const msg_preset* __restrict__ presets, const msg_event* __restrict
 #endif
     const int li = blockIdx.x;
     if (li >= n_list) return;
-    const int lane = threadIdx.x;
+    const int lane = (int)(threadIdx.x & (GEN_T - 1));
+    const int wv = GEN_K == 1 ? 0 : __builtin_amdgcn_readfirstlane((int)(threadIdx.x / GEN_T));
+    __shared__ int2 s_carry[2][GEN_K];   // GEN_K > 1, per round (parity) and wave: (normals, overhang)
 #if MSG_GEN_LDS
-    for (int i = lane; i < 256; i += GEN_T) {
+    for (int i = (int)threadIdx.x; i < 256; i += GEN_T * GEN_K) {
         s_ki[i] = z.ki[i];
         s_wi[i] = z.wi[i];
         s_kw[i] = jt->kw[i];
@@ -236,7 +285,7 @@ k_gen_normal(const msg_preset* __restrict__ presets, const msg_event* __restrict
     // base's (sin, cos, decays) by the offset table entry t, with the 0.9 and
     // 0.25 gains folded into the table.
     if (!RAW64 && c.mode == MSG_GEN_RESONANT) {
-        for (int i = lane; i < 128; i += GEN_T) {
+        for (int i = (int)threadIdx.x; i < 128; i += GEN_T * GEN_K) {
             const float rf = (float)(i - 64);
             const float ph = ring_phase(rf, c.fa, c.fb);
             s_rot[i] = make_float4(__builtin_amdgcn_cosf(ph), __builtin_amdgcn_sinf(ph),
@@ -272,16 +321,19 @@ k_gen_normal(const msg_preset* __restrict__ presets, const msg_event* __restrict
     constexpr int G = GEN_G;
     nprng::u128 st[G];
     st[0] = jt->a[lane] * g0.state + inc * jt->s[lane];   // state after lane+1 steps
+    if (GEN_K > 1) st[0] = jt->aW[wv] * st[0] + inc * jt->sW[wv];   // + wv groups
 #pragma unroll
     for (int g = 1; g < G; ++g) st[g] = a64 * st[g - 1] + c64;
-    const nprng::u128 aG = jt->aG;
-    const nprng::u128 cG = inc * jt->sG;
+    const nprng::u128 aG = GEN_K > 1 ? jt->aR : jt->aG;   // the next group of this wave
+    const nprng::u128 cG = inc * (GEN_K > 1 ? jt->sR : jt->sG);
 #if MSG_GEN_LDS
     __syncthreads();
 #endif
 
-    int produced = 0;
-    int local = 0;   // first lane of the current chunk not consumed by an earlier slow normal
+    int produced = 0;   // normals of all groups walked so far (workgroup-uniform)
+    int local = 0;      // first lane of the next group not consumed by an earlier slow normal
+    int rpar = 0;       // s_carry buffer of this round
+    (void)rpar;
     while (produced < n) {
         using XT = typename std::conditional<RAW64, double, float>::type;
         uint64_t rabs[G], F[G];
@@ -345,41 +397,61 @@ k_gen_normal(const msg_preset* __restrict__ presets, const msg_event* __restrict
             for (int g = 0; g < G; ++g)
                 if (gs == g) { x[g] = (XT)v; consumed[g] = cn; }
         }
+        // the walk: which lanes of each chunk start a normal (vb), and this wave's
+        // first output index pw
+        uint32_t vb;
+        int cnt, pw;
+        if constexpr (GEN_K == 1) {
+            local = gen_walk<G>(F, consumed, local, vb, cnt);
+            pw = produced;
+            produced += cnt;
+        } else {
+            int lout = gen_walk<G>(F, consumed, 0, vb, cnt);   // as if nothing reaches into the group
+            if (lane == 0) s_carry[rpar][wv] = make_int2(cnt, lout);
+            __syncthreads();
+            pw = produced;
+            int lin = local;
+#pragma unroll 1
+            for (int j = 0; j < GEN_K; ++j) {
+                if (lin != 0) {                   // workgroup-uniform: group j starts inside a slow normal
+                    if (wv == j) {
+                        lout = gen_walk<G>(F, consumed, lin, vb, cnt);
+                        if (lane == 0) s_carry[rpar][j] = make_int2(cnt, lout);
+                    }
+                    __syncthreads();
+                }
+                const int2 cj = s_carry[rpar][j];
+                if (wv == j) pw = produced;
+                produced += cj.x;
+                lin = cj.y;
+            }
+            local = lin;
+            rpar ^= 1;
+        }
 #if MSG_GEN_EMIT == 2
         // resonant: lanes g < G evaluate the group's chunk bases p0 + 64 g (one set
         // of transcendentals per group instead of per chunk)
         const bool reson = !RAW64 && c.mode == MSG_GEN_RESONANT;
-        const int p0 = produced;
+        const int p0 = pw;
         if (reson) {
             if (lane < G) {
                 const float jb = (float)(p0 + 64 * lane);
                 const float ph = ring_phase(jb, c.fa, c.fb);
-                s_grp[lane] = make_float4(__builtin_amdgcn_sinf(ph), __builtin_amdgcn_cosf(ph),
-                                          __builtin_amdgcn_exp2f(fmaxf(jb * c.k_ring, -126.f)),
-                                          __builtin_amdgcn_exp2f(fmaxf(jb * c.k_exc, -126.f)));
+                s_grp[wv][lane] = make_float4(__builtin_amdgcn_sinf(ph), __builtin_amdgcn_cosf(ph),
+                                              __builtin_amdgcn_exp2f(fmaxf(jb * c.k_ring, -126.f)),
+                                              __builtin_amdgcn_exp2f(fmaxf(jb * c.k_exc, -126.f)));
             }
-            __syncthreads();                      // one wave: orders the LDS writes before the reads
+            __syncthreads();                      // orders the LDS writes before the reads
         }
 #endif
+        int pc = pw;                              // output index of the chunk's first normal
 #pragma unroll
         for (int g = 0; g < G; ++g) {
-            if (local >= 64) { local -= 64; continue; }   // chunk consumed by an earlier slow normal
-            if (produced >= n) continue;
-            uint64_t valid = ~0ULL << local;
-            uint64_t S = ~F[g] & valid;
-            int pos = 64;
-            while (S) {                               // wave-uniform
-                const int q = __builtin_ctzll(S);
-                const int end = q + __builtin_amdgcn_readlane(consumed[g], q);
-                const uint64_t after_q = ~((2ULL << q) - 1);                  // lanes q+1..63
-                const uint64_t before_end = end >= 64 ? ~0ULL : ((1ULL << end) - 1);
-                valid &= ~(after_q & before_end);
-                if (end >= 64) { pos = end; break; }
-                S &= ~0ULL << end;
-            }
+            const uint64_t valid = __ballot((vb >> g) & 1u);
+            if (pc >= n || !valid) continue;
             if constexpr (RAW64) {
                 if ((valid >> lane) & 1) {
-                    const int j = produced + __popcll(valid & ((1ULL << lane) - 1));
+                    const int j = pc + __popcll(valid & ((1ULL << lane) - 1));
                     if (j < n) out64[j] = x[g];
                 }
             }
@@ -389,50 +461,50 @@ k_gen_normal(const msg_preset* __restrict__ presets, const msg_event* __restrict
                 const int rk = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(valid >> 32),
                                                               __builtin_amdgcn_mbcnt_lo((uint32_t)valid, 0u));
                 const bool vl = __builtin_amdgcn_inverse_ballot_w64(valid);
-                const int room = n - produced;    // uniform
-                float* __restrict__ ob = out + produced;
+                const int room = n - pc;          // uniform
+                float* __restrict__ ob = out + pc;
                 if (reson) {
-                    // j = produced + rk = B_g + (d + rk), d = produced - B_g in [-64, 0]
-                    const int d = produced - (p0 + 64 * g);
+                    // j = pc + rk = B_g + (d + rk), d = pc - B_g in [-64, 0]
+                    const int d = pc - (p0 + 64 * g);
                     float4 u;
                     int off;
                     if (d >= -64) {
-                        u = s_grp[g];
+                        u = s_grp[wv][g];
                         off = d + 64;
                     } else {                          // a slow normal spanned > 64 draws: exact base
-                        const float j0 = (float)produced;
+                        const float j0 = (float)pc;
                         const float ph0 = ring_phase(j0, c.fa, c.fb);
                         u = make_float4(__builtin_amdgcn_sinf(ph0), __builtin_amdgcn_cosf(ph0),
                                         __builtin_amdgcn_exp2f(fmaxf(j0 * c.k_ring, -126.f)),
                                         __builtin_amdgcn_exp2f(fmaxf(j0 * c.k_exc, -126.f)));
                         off = 64;
                     }
-                    const bool edge = produced < c.fade || produced + 64 > c.n - c.fade;
+                    const bool edge = pc < c.fade || pc + 64 > c.n - c.fade;
                     if (vl && rk < room) {
                         const float4 tb = s_rot[rk + off];
                         float v = fmaf(u.x, tb.x, u.y * tb.y) * (u.z * tb.z) + x[g] * (u.w * tb.w);
-                        if (edge) v = gen_fade(c, produced + rk, v);
+                        if (edge) v = gen_fade(c, pc + rk, v);
                         ob[rk] = v;
                     }
                 } else if (vl && rk < room) {
-                    ob[rk] = gen_basic_sample(c, produced + rk, (float)x[g]);
+                    ob[rk] = gen_basic_sample(c, pc + rk, (float)x[g]);
                 }
             }
 #elif MSG_GEN_EMIT == 0
             else {                                // cost experiment only: raw normals, no generator formula
                 const int rk = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(valid >> 32),
                                                               __builtin_amdgcn_mbcnt_lo((uint32_t)valid, 0u));
-                if (__builtin_amdgcn_inverse_ballot_w64(valid) && rk < n - produced) out[produced + rk] = (float)x[g];
+                if (__builtin_amdgcn_inverse_ballot_w64(valid) && rk < n - pc) out[pc + rk] = (float)x[g];
             }
 #else
             else if (c.mode == MSG_GEN_RESONANT) {
-                // chunk-uniform phase and decays at j0 = produced
-                const float j0 = (float)produced;
+                // chunk-uniform phase and decays at j0 = pc
+                const float j0 = (float)pc;
                 const float ph0 = ring_phase(j0, c.fa, c.fb);
                 const float s0 = __builtin_amdgcn_sinf(ph0), c0 = __builtin_amdgcn_cosf(ph0);
                 const float dA = __builtin_amdgcn_exp2f(fmaxf(j0 * c.k_ring, -126.f));
                 const float dE = __builtin_amdgcn_exp2f(fmaxf(j0 * c.k_exc, -126.f));
-                const bool edge = produced < c.fade || produced + 64 > c.n - c.fade;
+                const bool edge = pc < c.fade || pc + 64 > c.n - c.fade;
                 const int rk = __popcll(valid & ((1ULL << lane) - 1));
 #if MSG_GEN_LDS
                 const float4 tb = s_rot[rk];
@@ -441,7 +513,7 @@ k_gen_normal(const msg_preset* __restrict__ presets, const msg_event* __restrict
                                               __shfl(rot.w, rk));   // every lane: lane rk holds rank rk's rotation
 #endif
                 if ((valid >> lane) & 1) {
-                    const int j = produced + rk;
+                    const int j = pc + rk;
                     if (j < n) {
                         float v = 0.9f * fmaf(s0, tb.x, c0 * tb.y) * (dA * tb.z) + 0.25f * x[g] * (dE * tb.w);
                         if (edge) v = gen_fade(c, j, v);
@@ -450,13 +522,12 @@ k_gen_normal(const msg_preset* __restrict__ presets, const msg_event* __restrict
                 }
             } else {
                 if ((valid >> lane) & 1) {
-                    const int j = produced + __popcll(valid & ((1ULL << lane) - 1));
+                    const int j = pc + __popcll(valid & ((1ULL << lane) - 1));
                     if (j < n) out[j] = gen_basic_sample(c, j, (float)x[g]);
                 }
             }
 #endif
-            produced += __popcll(valid);
-            local = pos - 64;
+            pc += __popcll(valid);
         }
 #pragma unroll
         for (int g = 0; g < G; ++g) st[g] = aG * st[g] + cG;   // next group of G chunks

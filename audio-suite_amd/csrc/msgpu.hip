@@ -620,6 +620,12 @@ msg_ctx* msg_create(int device_ordinal) {
     jt.a64 = j64.a; jt.s64 = j64.s;
     const nprng::Jump jG = nprng::jump_of((uint64_t)GEN_T * GEN_G);
     jt.aG = jG.a; jt.sG = jG.s;
+    for (int w = 0; w < GEN_K; ++w) {
+        const nprng::Jump jw = nprng::jump_of((uint64_t)GEN_T * GEN_G * w);
+        jt.aW[w] = jw.a; jt.sW[w] = jw.s;
+    }
+    const nprng::Jump jR = nprng::jump_of((uint64_t)GEN_T * GEN_G * GEN_K);
+    jt.aR = jR.a; jt.sR = jR.s;
     for (int i = 0; i < 256; ++i) {
         const float w = (float)(zig_wi_double[i] * 1048576.0);
         uint32_t wb;
@@ -1731,12 +1737,12 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
     // ---- generate ----
     stage_mark(ctx, 2, s);
     if (!gen_list.empty())
-        hipLaunchKernelGGL(k_gen_normal<false>, dim3((unsigned)gen_list.size()), dim3(GEN_T), 0, s,
+        hipLaunchKernelGGL(k_gen_normal<false>, dim3((unsigned)gen_list.size()), dim3(GEN_T * GEN_K), 0, s,
                            ctx->presets.p, ctx->events.p, ctx->prt.p, ctx->gen_list.p, (int)gen_list.size(),
                            ctx->dzig, ctx->d_jump, ctx->micro.p, (double*)nullptr, (const int64_t*)nullptr);
     HIPCHK(ctx, hipGetLastError());
     if (!gen64_list.empty())   // raw normals of the float64 chain's normal-driven generators
-        hipLaunchKernelGGL(k_gen_normal<true>, dim3((unsigned)gen64_list.size()), dim3(GEN_T), 0, s,
+        hipLaunchKernelGGL(k_gen_normal<true>, dim3((unsigned)gen64_list.size()), dim3(GEN_T * GEN_K), 0, s,
                            ctx->presets.p, ctx->events.p, ctx->prt.p, ctx->gen64_list.p, (int)gen64_list.size(),
                            ctx->dzig, ctx->d_jump, ctx->micro.p, ctx->micro64.p, (const int64_t*)ctx->gen64_off.p);
     HIPCHK(ctx, hipGetLastError());
