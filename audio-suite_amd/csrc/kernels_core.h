@@ -811,8 +811,10 @@ k_stereo_max(const PresetRt* __restrict__ rt, const int32_t* __restrict__ st_beg
 // library tanhf's ~30 instructions; k_stereo_out runs two per frame):
 // 1 - 2 / (e^{2|x|} + 1), |error| <= ~2 float32 ulp of 1, and an odd Taylor
 // polynomial below |x| = 0.05 where the subtraction would lose relative digits.
-// MSG_TANH_TAYLOR = 0 drops the polynomial: below |x| = 0.05 the subtraction's
-// absolute error stays ~1e-7 of the unit peak, far inside the 1e-5 RMS bar.
+// MSG_TANH_TAYLOR = 0 (tuning only) drops the polynomial: the subtraction's
+// ~1e-7 absolute error becomes a large relative one once the peak normalisation
+// scales a quiet render (drive x peak << 1) back up, and test_feedback_imprint_chain
+// fails (profiles/r03ab_stereo_ab.json).
 #ifndef MSG_TANH_TAYLOR
 #define MSG_TANH_TAYLOR 1
 #endif
