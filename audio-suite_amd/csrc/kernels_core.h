@@ -874,6 +874,7 @@ k_stereo_out(const PresetRt* __restrict__ rt, const int32_t* __restrict__ st_beg
     const float M = __uint_as_float(maxbits[p]);
     const float mc = sat(M, d, inv_td);
     const float scale = mc > 0.f ? r.peak / mc : 1.f;
+    const float k_out = inv_td * scale;                     // one multiply per channel after the tanh
     float2* o = reinterpret_cast<float2*>(out) + r.out_off + st.t0;
     const bool o16 = ((r.out_off + st.t0) & 1) == 0;      // float4 stores of two frames
     __syncthreads();
@@ -896,7 +897,7 @@ k_stereo_out(const PresetRt* __restrict__ rt, const int32_t* __restrict__ st_beg
         if (d > 0.f) {
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
-                const f2p t = tanh_fast2(f2p{L[k], R[k]} * d) * inv_td * scale;
+                const f2p t = tanh_fast2(f2p{L[k], R[k]} * d) * k_out;
                 v[k] = make_float2(t.x, t.y);
             }
         } else {

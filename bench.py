@@ -106,7 +106,12 @@ def measured_traffic(prefixes, cfg, batch):
     committed PMC summary of this workload, or None when there is none (bench
     cannot read PMC itself)."""
     import glob
-    newest = sorted(glob.glob(os.path.join(PROFILES, f"r*_traffic_{cfg}.json")), reverse=True)
+    import re
+
+    def tag_order(path):                # r03z < r03aa < r03ae: round, then tag length, then tag
+        m = re.match(r"r(\d+)([a-z]*)_", os.path.basename(path))
+        return (int(m.group(1)), len(m.group(2)), m.group(2)) if m else (-1, 0, "")
+    newest = sorted(glob.glob(os.path.join(PROFILES, f"r*_traffic_{cfg}.json")), key=tag_order, reverse=True)
     for path in (os.path.join(PROFILES, f"traffic_{cfg}.json"), *newest, os.path.join(PROFILES, "traffic.json")):
         try:
             with open(path) as f:
