@@ -1,7 +1,7 @@
 #!/bin/bash
 # A/B of stage stream priorities (MSGPU_PRIO_HI / MSGPU_PRIO_LO stage masks:
 # (The MSGPU_PRIO_HI / MSGPU_PRIO_LO knob lived in a tuning build only and was
-# removed after this A/B: profiles/r03ad_prio_ab.json.)
+# removed after this A/B: profiles/r03ad_prio_ab.json, r03af_queues_prio_ab.json.)
 # 0x4 generate, 0x8 spectral, 0x10 overlap-add, 0x20 h build, 0x100 FIR, 0x40 stereo).
 #   usage (on the box): bash tools/prio_ab.sh base HI:LO [HI:LO ...]
 set -e
