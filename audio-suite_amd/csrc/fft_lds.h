@@ -418,6 +418,46 @@ MSG_DEV void stockham_fwd(float2* buf, int size, const int32_t* rad, int nrad, c
     }
 }
 
+// A fixed-size float2 table copied from global memory into LDS with every load
+// of the block issued before the first LDS store: fetch() puts the thread's
+// entries in registers, put() stores them.  The plain `for (i = tid; i < N;
+// i += T) dst[i] = src[i]` loop compiles to load / s_waitcnt vmcnt(0) /
+// ds_write per iteration -- one full memory latency per iteration, before the
+// kernel's data loads even issue (k_fir8: 4 iterations, k_spec3: 2).  Kernels
+// issue their data loads between fetch() and put(); put() then waits for the
+// table loads only (vmcnt counts in order), and the data loads' latency runs
+// under the stores and the barrier.  MSG_TAB_PRELOAD=0 (tuning A/B): the loop.
+#ifndef MSG_TAB_PRELOAD
+#define MSG_TAB_PRELOAD 1
+#endif
+template <int N, int T>
+struct TabCopy {
+    static constexpr int PER = (N + T - 1) / T;
+#if MSG_TAB_PRELOAD
+    float2 v[PER];
+    MSG_DEV void fetch(const float2* __restrict__ src) {
+#pragma unroll
+        for (int i = 0; i < PER; ++i) {
+            const int k = (int)threadIdx.x + i * T;
+            if (i < PER - 1 || k < N) v[i] = src[k];
+        }
+    }
+    MSG_DEV void put(float2* dst) const {
+#pragma unroll
+        for (int i = 0; i < PER; ++i) {
+            const int k = (int)threadIdx.x + i * T;
+            if (i < PER - 1 || k < N) dst[k] = v[i];
+        }
+    }
+#else
+    const float2* s = nullptr;
+    MSG_DEV void fetch(const float2* __restrict__ src) { s = src; }
+    MSG_DEV void put(float2* dst) const {
+        for (int k = threadIdx.x; k < N; k += T) dst[k] = s[k];
+    }
+#endif
+};
+
 // Copy the plan's twiddle tables into LDS at `dst` (after the data region).
 template <int T>
 MSG_DEV TwLds stage_twiddles(float2* dst, const RealPlan& rp) {

@@ -236,7 +236,7 @@ k_fir4(const PresetRt* __restrict__ rt, const int2* __restrict__ jobs, const flo
     const int64_t n = pr.out_n;
     const int64_t t0 = (int64_t)job.y * pr.fir_B;
     const float* x = x_in + pr.y_off;
-    for (int i = threadIdx.x; i < G::TAB_USED; i += T) tab[i] = tables[i];   // visible after the first exchange
+    { TabCopy<G::TAB_USED, T> tc; tc.fetch(tables); tc.put(tab); }   // one memory latency, not one per T entries
 
     float2 acc[2][R4];
 #pragma unroll
@@ -535,7 +535,7 @@ k_fir4s(const PresetRt* __restrict__ rt, const int2* __restrict__ jobs, const fl
     float* y = y_out + pr.y_off;
     const float2* H0 = hspec + pr.h_off;
     const float2* H1 = H0 + (M + 1);
-    for (int i = threadIdx.x; i < G::TAB_USED; i += T) tab[i] = tables[i];   // visible after the first exchange
+    { TabCopy<G::TAB_USED, T> tc; tc.fetch(tables); tc.put(tab); }   // one memory latency, not one per T entries
 
     float2 acc[2][R4];
 #pragma unroll
@@ -621,7 +621,7 @@ k_fir4_hpart(const PresetRt* __restrict__ rt, const int2* __restrict__ jobs, con
     const int2 job = jobs[blockIdx.x];
     const PresetRt& r = rt[job.x];
     const int q = job.y, P = r.fir_P;
-    for (int i = threadIdx.x; i < G::TAB_USED; i += T) tab[i] = tables[i];   // visible after the first exchange
+    { TabCopy<G::TAB_USED, T> tc; tc.fetch(tables); tc.put(tab); }   // one memory latency, not one per T entries
     const int64_t s0 = (int64_t)q * P;
     const int64_t len = P < r.h_len - s0 ? P : r.h_len - s0;               // h[qP, qP + P), zero-padded to N
     float2 v[2][R4];

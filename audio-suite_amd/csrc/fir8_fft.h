@@ -221,9 +221,11 @@ k_fir8(const PresetRt* __restrict__ rt, const int2* __restrict__ jobs, const flo
     const int P = pr.fir_P;                       // Q == 1
     const int64_t n = pr.out_n;
     const int64_t t0 = (int64_t)job.y * pr.fir_B;
-    for (int i = threadIdx.x; i < G::TAB_USED; i += T) tab[i] = tables[i];
+    TabCopy<G::TAB_USED, T> tc;
+    tc.fetch(tables);                             // table loads, then the segment's, all in flight
     float2 a[R1], b[R1];
     load_halves(x_in + pr.y_off, n, t0 - (P - 1), a, b);
+    tc.put(tab);
     __syncthreads();                              // tables visible
     dif_split(tab, a, b);
     const float2* He = hspec + pr.h_off;
@@ -345,7 +347,7 @@ k_fir8_spec(const int64_t* __restrict__ jobs, const float2* __restrict__ tables,
     float2* buf = lds + G::TAB;
     const int64_t* j = jobs + 4 * (blockIdx.x >> 1);
     const bool odd = blockIdx.x & 1;
-    for (int i = threadIdx.x; i < G::TAB_USED; i += T) tab[i] = tables[i];
+    { TabCopy<G::TAB_USED, T> tc; tc.fetch(tables); tc.put(tab); }   // one memory latency, not one per T entries
     __syncthreads();
     float2 in[R1], v[2][R4];
     float2* He = hspec + j[2];
@@ -370,7 +372,7 @@ k_fir8_hconv(const PresetRt* __restrict__ rt, const int32_t* __restrict__ list, 
     float2* buf = lds + G::TAB;
     const PresetRt& r = rt[list[blockIdx.x >> 1]];
     const bool odd = blockIdx.x & 1;
-    for (int i = threadIdx.x; i < G::TAB_USED; i += T) tab[i] = tables[i];
+    { TabCopy<G::TAB_USED, T> tc; tc.fetch(tables); tc.put(tab); }   // one memory latency, not one per T entries
     for (int m = threadIdx.x; m < MH; m += T) buf[m] = make_float2(0.f, 0.f);
     __syncthreads();
     // e = delta + taps as the half's input: slot m & (MH-1), minus for m >= MH in the odd half

@@ -32,6 +32,10 @@
 #include "kernels_core.h"
 #include "launch.h"
 #include "host_pool.h"
+#include "tap_sort.h"
+#ifndef MSG_TAP_RADIX
+#define MSG_TAP_RADIX 1   // tuning A/B: 0 = std::sort of the tap keys
+#endif
 #include "../../include/msgpu.h"
 
 namespace {
@@ -1166,16 +1170,26 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
             const int nt = std::max(1, presets[p].er_taps);
             int32_t* off = ctx->h_er_off.data() + tap_base[p];
             double* g = ctx->h_er_gain.data() + tap_base[p];
-            // (offset, tap index) packed in one key: a plain sort is the stable sort by offset
-            thread_local std::vector<uint64_t> key;
+            // (offset, tap index) packed in one key, sorted stably by offset (tap_sort.h)
+            thread_local std::vector<uint64_t> keybuf, tmpbuf;
             thread_local std::vector<double> g0;
-            key.resize(nt);
+            keybuf.resize(nt);
+            tmpbuf.resize(nt);
             g0.assign(g, g + nt);
             const int64_t n = info[p].out_n;
             int m = 0;
+            uint32_t omax = 0;
             for (int k = 0; k < nt; ++k)
-                if (off[k] > 0 && off[k] < n) key[m++] = ((uint64_t)(uint32_t)off[k] << 32) | (uint32_t)k;
-            std::sort(key.begin(), key.begin() + m);
+                if (off[k] > 0 && off[k] < n) {
+                    keybuf[m++] = ((uint64_t)(uint32_t)off[k] << 32) | (uint32_t)k;
+                    omax = std::max(omax, (uint32_t)off[k]);
+                }
+#if MSG_TAP_RADIX
+            const uint64_t* key = sort_taps_by_offset(keybuf.data(), tmpbuf.data(), m, omax);
+#else                                                    // tuning A/B: the comparison sort
+            std::sort(keybuf.begin(), keybuf.begin() + m);
+            const uint64_t* key = keybuf.data();
+#endif
             int live = 0;
             for (int i = 0; i < m;) {
                 const uint32_t o = (uint32_t)(key[i] >> 32);

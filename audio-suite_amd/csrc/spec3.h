@@ -357,9 +357,11 @@ k_spec3(const msg_event* __restrict__ events, const EventRt* __restrict__ ert, c
     const int li = blockIdx.x;
     if (li >= n_list) return;
     float2 v[P::R1];
-    // (the grain's loads are issued before the twiddle tables' so both share one memory latency)
+    // table loads, then the grain's, all in flight; the table stores wait for the tables only
+    TabCopy<P::TAB_USED, T> tc;
+    tc.fetch(tables);
     s3_load<P>(events, rt, ev_list, li, micro_pool, v);
-    for (int i = threadIdx.x; i < P::TAB_USED; i += T) tab[i] = tables[i];
+    tc.put(tab);
     s3_chain<P, MSG_S3_EVENTS>(buf, tab, events, ert, rt, ev_list, n_list, micro_pool, grain_pool, li, v);
 }
 

@@ -149,7 +149,7 @@ k_spectral_ct(const msg_event* __restrict__ events, const EventRt* __restrict__ 
     const int n = 2 * P::M;
     float* micro = micro_pool + r.pool_base + e.pool_off;
     float* grain = grain_pool + r.pool_base + e.pool_off;
-    for (int i = threadIdx.x; i < P::TAB_USED; i += T) tab[i] = tables[i];
+    { TabCopy<P::TAB_USED, T> tc; tc.fetch(tables); tc.put(tab); }   // one memory latency, not one per T entries
     load_real_segment<LayId, T, P::Q4>(buf, true, micro_pool + r.pool_base, e.pool_off, n, threadIdx.x);
     __syncthreads();
     SPEC_STAMP(0);

@@ -62,3 +62,17 @@ def test_host_pool_under_tsan(tmp_path):
     assert r.returncode == 0, out[-4000:]
     assert "WARNING: ThreadSanitizer" not in out, out[-4000:]
     assert "bad 0" in out
+
+
+@pytest.mark.skipif(shutil.which("g++") is None, reason="needs g++")
+def test_tap_sort_matches_std_sort(tmp_path):
+    """The ER merge's stable radix sort of the taps by offset (csrc/tap_sort.h)
+    gives std::sort's order of the packed (offset, tap index) keys -- equal
+    offsets in tap order, as MS:416-420 adds them -- under ASan + UBSan."""
+    exe = str(tmp_path / "tap_sort_check")
+    subprocess.run(["g++", "-std=c++17", "-O1", "-g", "-fsanitize=address,undefined", "-fno-sanitize-recover=undefined",
+                    "-Wall", "-Werror", "-I", CSRC, "-o", exe, os.path.join(REPO, "tests", "tap_sort_check.cpp")],
+                   check=True)
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=300)
+    out = r.stdout + r.stderr
+    assert r.returncode == 0 and "bad 0" in out, out[-4000:]
