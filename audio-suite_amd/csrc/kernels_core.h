@@ -217,8 +217,14 @@ MSG_DEV float gen_fade(const GenBasicConst& c, int j, float x) {
 #ifndef MSG_GEN_WAVES
 #define MSG_GEN_WAVES 1
 #endif
+#ifndef MSG_GEN_VGPRS
+#define MSG_GEN_VGPRS 0
+#endif
 template <bool RAW64>
 __global__ void __launch_bounds__(GEN_T * GEN_K, MSG_GEN_WAVES)
+#if MSG_GEN_VGPRS
+__attribute__((amdgpu_num_vgpr(MSG_GEN_VGPRS)))
+#endif
 k_gen_normal(const msg_preset* __restrict__ presets, const msg_event* __restrict__ events,
              const PresetRt* __restrict__ rt, const int32_t* __restrict__ ev_list, int n_list,
              nprng::Zig z, const JumpTab* __restrict__ jt, float* __restrict__ pool,
