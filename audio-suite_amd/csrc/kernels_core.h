@@ -577,11 +577,27 @@ MSG_DEV int events_starting_by(const msg_event* __restrict__ ev, int n, int64_t 
     return lo;
 }
 
+// Traversal order against the Infinity Cache (tuning A/B): MSG_OLA_REV /
+// MSG_STMAX_REV = 1 walk each XCD's job range backwards, so a consumer starts
+// on the most recently written end of its producer's output (spectral grains
+// -> overlap-add, FIR output -> stereo max) and leaves its own first jobs most
+// recent for the next, forward kernel.
+#ifndef MSG_OLA_REV
+#define MSG_OLA_REV 0
+#endif
+#ifndef MSG_STMAX_REV
+#define MSG_STMAX_REV 0
+#endif
+MSG_DEV int job_order(int rev) {
+    const int b = xcd_block(blockIdx.x, gridDim.x);
+    return rev ? (int)gridDim.x - 1 - b : b;
+}
+
 __global__ void __launch_bounds__(OLA_T)
 k_ola_env(const msg_event* __restrict__ events, const PresetRt* __restrict__ rt,
           const int32_t* __restrict__ tile_begin, int n_presets,
           const float* __restrict__ grain_pool, float* __restrict__ mono) {
-    const int b = xcd_block(blockIdx.x, gridDim.x);
+    const int b = job_order(MSG_OLA_REV);
     const int p = find_preset(tile_begin, n_presets, b);
     const PresetRt& r = rt[p];
     const int64_t t0 = (int64_t)(b - r.tile_begin) * OLA_TILE;
@@ -750,7 +766,7 @@ k_stereo_max(const PresetRt* __restrict__ rt, const int32_t* __restrict__ st_beg
              const float* __restrict__ ybuf, const float* __restrict__ rbuf, unsigned* __restrict__ maxbits) {
     __shared__ __attribute__((aligned(16))) float w[ST_WIN];
     __shared__ float wm[ST_T / 64];
-    const int b = xcd_block(blockIdx.x, gridDim.x);
+    const int b = job_order(MSG_STMAX_REV);
     const int p = find_preset(st_begin, n_presets, b);
     const PresetRt& r = rt[p];
     const float* y = ybuf + r.y_off;
