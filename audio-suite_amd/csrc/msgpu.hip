@@ -1045,11 +1045,13 @@ int msg_last_grain64(msg_ctx* ctx, int32_t preset, int32_t k, double* grain, int
     const int32_t ne = ctx->h_info[preset].n_events;
     if (l64 < 0) return fail(ctx, MSG_E_ARG, "preset is not on the float64 chain");
     if (k < 0 || k >= ne) return fail(ctx, MSG_E_ARG, "bad event index");
-    const Ev64& v = ctx->h_ev64[l64 - (ne - 1) + k];
+    const int64_t at = (int64_t)l64 - (ne - 1) + k;   // the preset's events end at its last float64 record
+    if (at < 0 || at >= (int64_t)ctx->h_ev64.size()) return fail(ctx, MSG_E_ARG, "event not on the float64 chain");
+    const Ev64& v = ctx->h_ev64[at];
     *n = v.n;
     if (!grain) return MSG_OK;
     if (v.n > cap) return fail(ctx, MSG_E_ARG, "grain buffer too small");
-    hipSetDevice(ctx->device);
+    HIPCHK(ctx, hipSetDevice(ctx->device));
     HIPCHK(ctx, hipDeviceSynchronize());
     HIPCHK(ctx, hipMemcpy(grain, ctx->grain64.p + v.off64, v.n * sizeof(double), hipMemcpyDeviceToHost));
     return MSG_OK;
