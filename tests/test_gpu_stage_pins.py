@@ -126,3 +126,25 @@ def test_imprint_input_every_event(pins_all, golden_info, irs, full_renders):
     print(f"{name}: SpectralImprint.apply inputs of {len(errs)} events, rel rms err max {max(errs):.3e}: "
           + " ".join(f"{e:.1e}" for e in errs))
     assert max(errs) <= TOL
+
+
+def test_grain64_readback_bounds(golden_info, irs, full_renders):
+    """msg_last_grain64 refuses event indices outside the preset's events and
+    presets that are not on the float64 chain (RuntimeError), instead of reading
+    another preset's record."""
+    import torch
+    import msgpu
+    from msgpu.engine import default_engine
+    from msgpu.pack import PackedBatch
+    eng = default_engine(0)
+    eng.render_packed(PackedBatch([_preset("ghost_formants", golden_info, irs, full_renders)]))
+    torch.cuda.synchronize(0)
+    ne = len(eng.last_events(0))
+    assert eng.last_grain64(0, ne - 1).size > 0
+    for k in (-1, ne):
+        with pytest.raises(RuntimeError):
+            eng.last_grain64(0, k)
+    eng.render_packed(PackedBatch([msgpu.config_params("C2", seed=1000, irs=irs, out_dur_s=0.25)]))
+    torch.cuda.synchronize(0)
+    with pytest.raises(RuntimeError):
+        eng.last_grain64(0, 0)
