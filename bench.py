@@ -65,6 +65,9 @@ CORES_PER_GPU = 16
 # (~35 GB of working buffers per context, three contexts, all outputs resident).
 CONFIG_BATCH = {"C1": 1, "C2": 1, "C3": 1024, "C4": 512, "C5": 1024, "H48": 1024}
 CONFIG_SUB = {"C5": 171}   # six sub-batches, two per stream (C5 ungated: 126.8 ms vs 130.6-132.2 at 128)
+# host-bound short-step points: at ~2 ms per step, 10 steps (20 ms) swung by +-40 % between
+# back-to-back runs on a shared-host box (profiles/r03an_h48_sweep.txt); time at least 50
+POINT_STEPS_MIN = {"H48": 50}
 GATE_OFF = {"C5"}   # configs whose points run ungated (measured slower with --gate 2,4)
 WORKLOAD = {
     "C1": "C1: 48 kHz out, no band limit, unfold x1, stretch x1, Single event, 1 s, ER 320 taps, stereo",
@@ -680,8 +683,8 @@ def main():
             pb = default_batch(pc, args)
             # C5's 8 sub-batches of 128 ran 3 % slower gated (135.2 vs 139.5 ms per step)
             runner.set_gate(None if pc in GATE_OFF else gate)
-            points[pc] = measure(runner, pc, rank_seeds(rank, pb), default_sub(pc, args, pb), args.point_steps,
-                                 1, comm, irs, golden)
+            points[pc] = measure(runner, pc, rank_seeds(rank, pb), default_sub(pc, args, pb),
+                                 max(args.point_steps, POINT_STEPS_MIN.get(pc, 0)), 3, comm, irs, golden)
         lat = dropin_latency(cpu) if (rank == 0 and world == 1 and not args.no_cpu) else None
         ranks = comm.gather({"rank": rank, "pid": os.getpid(), "device": local,
                              "cpus": [cpus[0], cpus[-1], len(cpus)], "host_threads": host_threads(),
