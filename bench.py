@@ -67,7 +67,7 @@ CONFIG_BATCH = {"C1": 1, "C2": 1, "C3": 1024, "C4": 512, "C5": 1024, "H48": 1024
 CONFIG_SUB = {"C5": 171}   # six sub-batches, two per stream (C5 ungated: 126.8 ms vs 130.6-132.2 at 128)
 # host-bound short-step points: at ~2 ms per step, 10 steps (20 ms) swung by +-40 % between
 # back-to-back runs on a shared-host box (profiles/r03an_h48_sweep.txt); time at least 50
-POINT_STEPS_MIN = {"H48": 50}
+POINT_STEPS_MIN = {"H48": 50, "C4": 30}
 GATE_OFF = {"C5"}   # configs whose points run ungated (measured slower with --gate 2,4)
 WORKLOAD = {
     "C1": "C1: 48 kHz out, no band limit, unfold x1, stretch x1, Single event, 1 s, ER 320 taps, stereo",
