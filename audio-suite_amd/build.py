@@ -99,6 +99,22 @@ def _compile(tu, variant=""):
     return obj
 
 
+def build_pack() -> str:
+    """The native params-dict packer msgpu/_mspack (csrc/mspack.c, CPython C API,
+    host only): rebuilt when the source or include/msgpu.h is newer."""
+    import sysconfig
+    src = os.path.join(CSRC, "mspack.c")
+    out = os.path.join(HERE, "msgpu", "_mspack" + sysconfig.get_config_var("EXT_SUFFIX"))
+    newest = max(os.path.getmtime(src), os.path.getmtime(os.path.join(os.path.dirname(HERE), "include", "msgpu.h")))
+    if not os.path.exists(out) or os.path.getmtime(out) < newest:
+        cmd = [os.environ.get("CC", "gcc"), "-O2", "-shared", "-fPIC", "-Wall", "-Werror",
+               "-I" + sysconfig.get_paths()["include"], "-o", out + ".tmp", src]
+        print("[msgpu build]", " ".join(cmd), flush=True)
+        subprocess.check_call(cmd)
+        os.replace(out + ".tmp", out)
+    return out
+
+
 def build(force: bool = False, variant: str = "") -> str:
     _, objdir, libname = VARIANTS[variant]
     out = os.path.join(HERE, "msgpu", libname)
@@ -109,6 +125,7 @@ def build(force: bool = False, variant: str = "") -> str:
             if os.path.exists(o):
                 os.remove(o)
     _defs_stamp(variant)
+    build_pack()
     with cf.ThreadPoolExecutor(max_workers=len(TUS)) as ex:
         objs = list(ex.map(lambda tu: _compile(tu, variant), TUS))
     OUT = out

@@ -43,7 +43,8 @@ int64_t msg_sizeof(int32_t which) {
 const char* msg_last_error(msg_ctx*) { return g_err.c_str(); }
 msg_ctx* msg_create(int) { no_device(); return nullptr; }
 void msg_destroy(msg_ctx*) {}
-int msg_render_batch(msg_ctx*, const msg_preset*, int32_t, const double* const*, const int64_t*, int32_t,
+int msg_render_batch(msg_ctx*, const msg_preset*, int32_t, const double*, int64_t, const double* const*,
+                     const int64_t*, int32_t,
                      const uint8_t* const*, const int32_t*, const int32_t*, int32_t, float*, const int64_t*, void*) {
     return no_device();
 }

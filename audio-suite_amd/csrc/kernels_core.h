@@ -7,17 +7,17 @@
 // Planner (one thread per preset).
 // ---------------------------------------------------------------------------
 __global__ void k_plan_sizes(const msg_preset* __restrict__ presets, int n_presets,
-                             const int64_t* __restrict__ frag_len, nprng::Zig z,
+                             const double* __restrict__ bp, const int64_t* __restrict__ frag_len, nprng::Zig z,
                              msg_plan_info* __restrict__ info) {
     const int p = blockIdx.x * blockDim.x + threadIdx.x;
     if (p >= n_presets) return;
     msg_plan_info inf;
-    msgplan::plan_sizes(presets[p], z, frag_len[p], inf);
+    msgplan::plan_sizes(presets[p], bp, z, frag_len[p], inf);
     info[p] = inf;
 }
 
 __global__ void k_plan_events(const msg_preset* __restrict__ presets, int n_presets,
-                              const int64_t* __restrict__ frag_len, nprng::Zig z,
+                              const double* __restrict__ bp, const int64_t* __restrict__ frag_len, nprng::Zig z,
                               const int32_t* __restrict__ slot_base, const int32_t* __restrict__ tap_base,
                               msg_event* __restrict__ events, int32_t* __restrict__ er_off,
                               double* __restrict__ er_gain, msg_plan_info* __restrict__ info) {
@@ -26,7 +26,7 @@ __global__ void k_plan_events(const msg_preset* __restrict__ presets, int n_pres
     msg_plan_info inf;
     const msg_preset& pr = presets[p];
     const bool er = (pr.flags & MSG_F_ER_CLOUD) != 0;
-    msgplan::plan_events(pr, z, frag_len[p], p, inf, events + slot_base[p],
+    msgplan::plan_events(pr, bp, z, frag_len[p], p, inf, events + slot_base[p],
                          er ? er_off + tap_base[p] : nullptr, er ? er_gain + tap_base[p] : nullptr);
     info[p] = inf;
 }

@@ -273,37 +273,45 @@ MSG_DEV void gen64(const msg_preset& pr, const PresetRt& r, const Ev64& ev, cons
         return;
     }
     case MSG_GEN_WAVELET: {
+        // any atom count: the atoms' parameters are drawn G64_MAXPAR at a time by
+        // lane 0 from the one stream (MS:322-327), and every sample's sum runs on
+        // in d[j] across the chunks, in the reference's k order (MS:329)
         const int cnt = pr.wav_count > 1 ? pr.wav_count : 1;
         const double dur = pr.micro_ms;
-        if (tid == 0) {
-            nprng::Pcg64 g = nprng::default_rng(seed);
-            const int64_t lo = -(int64_t)((n + 7) / 8);   // Python -n//8 (floor)
-            const int64_t hi = n / 8;
-            for (int k = 0; k < cnt; ++k) {
-                const double f0 = pr.wav_base_hz * pow(2.0, nprng::uniform(g, -pr.wav_spread, pr.wav_spread));
-                const double sig_ms = fmax(0.03, dur * nprng::uniform(g, 0.04, 0.18));
-                const double ph = nprng::uniform(g, 0.0, 2.0 * G64_PI);
-                const int64_t sh_ = nprng::integers(g, lo, hi);
-                sh.par[0][k] = f0;
-                sh.par[1][k] = fmax(1e-9, sig_ms / 1000.0);
-                sh.par[2][k] = ph;
-                sh.ipar[k] = (int)sh_;
-            }
-        }
-        __syncthreads();
         const double half = (double)n / 2.0;
-        for (int j = tid; j < n; j += G64_T) {
-            double x = 0.0;
-            for (int k = 0; k < cnt; ++k) {
-                int i = (j - sh.ipar[k]) % n;
-                if (i < 0) i += n;
-                const double t = ((double)i - half) / sr;
-                const double u = t / sh.par[1][k];
-                const double a = exp(-0.5 * (u * u)) * cos(2.0 * G64_PI * sh.par[0][k] * t + sh.par[2][k]);
-                x += (1.0 / (1.0 + (double)k * 0.6)) * a;
+        nprng::Pcg64 g = nprng::default_rng(seed);
+        const int64_t lo = -(int64_t)((n + 7) / 8);       // Python -n//8 (floor)
+        const int64_t hi = n / 8;
+        for (int k0 = 0; k0 < cnt; k0 += G64_MAXPAR) {
+            const int kn = cnt - k0 < G64_MAXPAR ? cnt - k0 : G64_MAXPAR;
+            if (tid == 0) {
+                for (int k = 0; k < kn; ++k) {
+                    const double f0 = pr.wav_base_hz * pow(2.0, nprng::uniform(g, -pr.wav_spread, pr.wav_spread));
+                    const double sig_ms = fmax(0.03, dur * nprng::uniform(g, 0.04, 0.18));
+                    const double ph = nprng::uniform(g, 0.0, 2.0 * G64_PI);
+                    const int64_t sh_ = nprng::integers(g, lo, hi);
+                    sh.par[0][k] = f0;
+                    sh.par[1][k] = fmax(1e-9, sig_ms / 1000.0);
+                    sh.par[2][k] = ph;
+                    sh.ipar[k] = (int)sh_;
+                }
             }
-            d[j] = x * hann64(j, n);
+            __syncthreads();
+            for (int j = tid; j < n; j += G64_T) {
+                double x = k0 == 0 ? 0.0 : d[j];
+                for (int k = 0; k < kn; ++k) {
+                    int i = (j - sh.ipar[k]) % n;
+                    if (i < 0) i += n;
+                    const double t = ((double)i - half) / sr;
+                    const double u = t / sh.par[1][k];
+                    const double a = exp(-0.5 * (u * u)) * cos(2.0 * G64_PI * sh.par[0][k] * t + sh.par[2][k]);
+                    x += (1.0 / (1.0 + (double)(k0 + k) * 0.6)) * a;
+                }
+                d[j] = x;
+            }
+            __syncthreads();                              // the chunk's parameters are read up
         }
+        for (int j = tid; j < n; j += G64_T) d[j] *= hann64(j, n);
         __syncthreads();
         return;
     }
@@ -468,61 +476,95 @@ MSG_DEV void gather64(C* buf, int K, bool ascending, Src src) {
         __syncthreads();
     }
 }
-// partial_lock_stretch (MS:130-148) on the resident spectrum
+// partial_lock_stretch (MS:130-148) on the resident spectrum.  Peaks are taken by
+// repeated block arg-max (descending |X|, ties to the larger bin) and applied in
+// argsort order (ascending: selection p is entry cnt-1-p).  Up to G64_MAXPAR
+// peaks are held at once; beyond that the entries are applied G64_MAXPAR at a
+// time in argsort order, each chunk re-running the selection down to its own
+// entries, with every bin's sum carried across the chunks (registers in the LDS
+// engine, where K <= G64_T * G64_MAXE; acc_g, the FFT scratch, in the global one).
 MSG_DEV void partial_lock64(double2* buf, int K, double factor, int top_n, int neigh, G64Shared& sh,
-                            uint32_t* mask) {
+                            uint32_t* mask, double2* acc_g) {
     const int nb = K - 1;                   // candidates: bins 1..K-1
     int cnt;
     if (top_n > 0) cnt = top_n < nb ? top_n : nb;
     else if (top_n == 0) cnt = nb;          // a[-0:] is the whole array
     else cnt = nb + top_n > 0 ? nb + top_n : 0;
-    for (int i = threadIdx.x; i < (K + 31) / 32 + 1; i += G64_T) mask[i] = 0u;
-    __syncthreads();
-    // descending selection: pick the largest |X| not yet taken, cnt times
-    for (int p = 0; p < cnt; ++p) {
-        double bv = -1.0;
-        int bk = -1;
-        for (int k = 1 + threadIdx.x; k < K; k += G64_T) {
-            if ((mask[k >> 5] >> (k & 31)) & 1u) continue;
-            const double m = hypot(buf[k].x, buf[k].y);
-            if (m > bv || (m == bv && k > bk)) { bv = m; bk = k; }
-        }
-        for (int off = 32; off > 0; off >>= 1) {
-            const double ov = __shfl_xor(bv, off);
-            const int ok = __shfl_xor(bk, off);
-            if (ov > bv || (ov == bv && ok > bk)) { bv = ov; bk = ok; }
-        }
-        if ((threadIdx.x & 63) == 0) { sh.red[threadIdx.x >> 6] = bv; sh.ired[threadIdx.x >> 6] = bk; }
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            double v = sh.red[0];
-            int kk = sh.ired[0];
-            for (int w = 1; w < G64_T / 64; ++w)
-                if (sh.red[w] > v || (sh.red[w] == v && sh.ired[w] > kk)) { v = sh.red[w]; kk = sh.ired[w]; }
-            // argsort order is ascending: peak p of the selection is entry cnt-1-p
-            const int slot = cnt - 1 - p;
-            sh.peak_x[slot] = buf[kk];
-            sh.peak_k2[slot] = (int)rint((double)kk * factor);
-            mask[kk >> 5] |= 1u << (kk & 31);
-        }
-        __syncthreads();
-    }
-    // Y[kk] = sum over peaks (argsort order) of X[k] w(d), then + 0.12 X
     const double inv = 1.0 / (double)(neigh + 1);
-    for (int k = threadIdx.x; k < K; k += G64_T) {
-        double2 acc = d2(0.0, 0.0);
-        if (k >= 1) {
-            for (int p = 0; p < cnt; ++p) {
-                const int k2 = sh.peak_k2[p];
-                if (k2 < 1 || k2 >= K) continue;
-                const int dd = k - k2;
-                if (dd < -neigh || dd > neigh) continue;
-                const double w = 1.0 - ((double)(dd < 0 ? -dd : dd) * inv);
-                acc = dadd(acc, dscale(sh.peak_x[p], w));
+    double2 accr[G64_MAXE];
+#pragma unroll
+    for (int b = 0; b < G64_MAXE; ++b) accr[b] = d2(0.0, 0.0);
+    if (acc_g)
+        for (int k = threadIdx.x; k < K; k += G64_T) acc_g[k] = d2(0.0, 0.0);
+    for (int c0 = 0; c0 < cnt || c0 == 0; c0 += G64_MAXPAR) {
+        const int c1 = cnt - c0 < G64_MAXPAR ? cnt : c0 + G64_MAXPAR;   // entries [c0, c1) of the argsort
+        for (int i = threadIdx.x; i < (K + 31) / 32 + 1; i += G64_T) mask[i] = 0u;
+        __syncthreads();
+        // descending selection: pick the largest |X| not yet taken, down to entry c0
+        for (int p = 0; p < cnt - c0; ++p) {
+            double bv = -1.0;
+            int bk = -1;
+            for (int k = 1 + threadIdx.x; k < K; k += G64_T) {
+                if ((mask[k >> 5] >> (k & 31)) & 1u) continue;
+                const double m = hypot(buf[k].x, buf[k].y);
+                if (m > bv || (m == bv && k > bk)) { bv = m; bk = k; }
+            }
+            for (int off = 32; off > 0; off >>= 1) {
+                const double ov = __shfl_xor(bv, off);
+                const int ok = __shfl_xor(bk, off);
+                if (ov > bv || (ov == bv && ok > bk)) { bv = ov; bk = ok; }
+            }
+            if ((threadIdx.x & 63) == 0) { sh.red[threadIdx.x >> 6] = bv; sh.ired[threadIdx.x >> 6] = bk; }
+            __syncthreads();
+            if (threadIdx.x == 0) {
+                double v = sh.red[0];
+                int kk = sh.ired[0];
+                for (int w = 1; w < G64_T / 64; ++w)
+                    if (sh.red[w] > v || (sh.red[w] == v && sh.ired[w] > kk)) { v = sh.red[w]; kk = sh.ired[w]; }
+                const int slot = cnt - 1 - p;
+                if (slot < c1) {
+                    sh.peak_x[slot - c0] = buf[kk];
+                    sh.peak_k2[slot - c0] = (int)rint((double)kk * factor);
+                }
+                mask[kk >> 5] |= 1u << (kk & 31);
+            }
+            __syncthreads();
+        }
+        // Y[kk] += X[k] w(d) over this chunk's peaks, in argsort order
+        const int np = c1 - c0;
+        auto add = [&](int k, double2 acc) -> double2 {
+            if (k >= 1) {
+                for (int q = 0; q < np; ++q) {
+                    const int k2 = sh.peak_k2[q];
+                    if (k2 < 1 || k2 >= K) continue;
+                    const int dd = k - k2;
+                    if (dd < -neigh || dd > neigh) continue;
+                    const double w = 1.0 - ((double)(dd < 0 ? -dd : dd) * inv);
+                    acc = dadd(acc, dscale(sh.peak_x[q], w));
+                }
+            }
+            return acc;
+        };
+        if (acc_g) {
+            for (int k = threadIdx.x; k < K; k += G64_T) acc_g[k] = add(k, acc_g[k]);
+        } else {
+#pragma unroll
+            for (int b = 0; b < G64_MAXE; ++b) {
+                const int k = threadIdx.x + b * G64_T;
+                if (k < K) accr[b] = add(k, accr[b]);
             }
         }
-        const double2 x = buf[k];
-        buf[k] = dadd(acc, dscale(x, 0.12));
+        __syncthreads();                      // the chunk's peaks are read up
+    }
+    // then + 0.12 X (MS:147)
+    if (acc_g) {
+        for (int k = threadIdx.x; k < K; k += G64_T) buf[k] = dadd(acc_g[k], dscale(buf[k], 0.12));
+    } else {
+#pragma unroll
+        for (int b = 0; b < G64_MAXE; ++b) {
+            const int k = threadIdx.x + b * G64_T;
+            if (k < K) buf[k] = dadd(accr[b], dscale(buf[k], 0.12));
+        }
     }
     __syncthreads();
 }
@@ -556,72 +598,84 @@ MSG_DEV void cepstral64(double2* buf, const Real64Plan& rp, double factor, doubl
 // ---------------------------------------------------------------------------
 // Physics (MS:369-402) on d[0..n).
 // ---------------------------------------------------------------------------
+// Any mode / line count: lane 0 draws the parameters G64_MAXPAR at a time from
+// the one stream (MS:377-380, 391-396); the per-sample mode sum runs on in s[j]
+// across the chunks in the reference's k order (MS:382), the lines stay
+// sequential (MS:391-401).
 MSG_DEV void resonator64(double* d, int n, double sr, const msg_preset& pr, uint64_t seed, const nprng::Zig& z,
                          G64Shared& sh) {
     (void)z;
     const int modes = pr.res_modes > 1 ? pr.res_modes : 1;
     double* s = d + n;
-    if (threadIdx.x == 0) {
-        nprng::Pcg64 g = nprng::default_rng(seed + 321);
-        const double ratio = pr.res_fmax / fmax(1.0, pr.res_fmin);
-        const int den = pr.res_modes - 1 > 1 ? pr.res_modes - 1 : 1;
-        for (int k = 0; k < modes; ++k) {
-            double f = pr.res_fmin * pow(ratio, (double)k / (double)den);
-            f *= pow(2.0, nprng::uniform(g, -0.02, 0.02));
-            sh.par[0][k] = f;
-            sh.par[1][k] = nprng::uniform(g, 0.0, 2.0 * G64_PI);
-        }
-    }
-    __syncthreads();
+    nprng::Pcg64 g = nprng::default_rng(seed + 321);
+    const double ratio = pr.res_fmax / fmax(1.0, pr.res_fmin);
+    const int den = pr.res_modes - 1 > 1 ? pr.res_modes - 1 : 1;
     const double tau = fmax(1e-6, pr.res_decay_ms / 1000.0);
     double m = 0.0;
-    for (int j = threadIdx.x; j < n; j += G64_T) {
-        const double t = (double)j / sr;
-        const double env = exp(-t / tau);
-        double acc = 0.0;
-        for (int k = 0; k < modes; ++k) {
-            const double carrier = sin(2.0 * G64_PI * sh.par[0][k] * t + sh.par[1][k]);
-            acc += (1.0 / (1.0 + (double)k * 0.35)) * carrier * env;
+    for (int k0 = 0; k0 < modes; k0 += G64_MAXPAR) {
+        const int kn = modes - k0 < G64_MAXPAR ? modes - k0 : G64_MAXPAR;
+        if (threadIdx.x == 0) {
+            for (int k = 0; k < kn; ++k) {
+                double f = pr.res_fmin * pow(ratio, (double)(k0 + k) / (double)den);
+                f *= pow(2.0, nprng::uniform(g, -0.02, 0.02));
+                sh.par[0][k] = f;
+                sh.par[1][k] = nprng::uniform(g, 0.0, 2.0 * G64_PI);
+            }
         }
-        s[j] = acc;
-        m = fmax(m, fabs(acc));
+        __syncthreads();
+        const bool last = k0 + kn >= modes;
+        for (int j = threadIdx.x; j < n; j += G64_T) {
+            const double t = (double)j / sr;
+            const double env = exp(-t / tau);
+            double acc = k0 == 0 ? 0.0 : s[j];
+            for (int k = 0; k < kn; ++k) {
+                const double carrier = sin(2.0 * G64_PI * sh.par[0][k] * t + sh.par[1][k]);
+                acc += (1.0 / (1.0 + (double)(k0 + k) * 0.35)) * carrier * env;
+            }
+            s[j] = acc;
+            if (last) m = fmax(m, fabs(acc));
+        }
+        __syncthreads();
     }
     m = block_max(m, sh);
-    const double den = fmax(1e-12, m);
+    const double dn = fmax(1e-12, m);
     for (int j = threadIdx.x; j < n; j += G64_T) {
         const double x = d[j];
         const double sg = x > 0.0 ? 1.0 : (x < 0.0 ? -1.0 : 0.0);
-        d[j] = 0.55 * x + 0.45 * (s[j] / den) * sg;
+        d[j] = 0.55 * x + 0.45 * (s[j] / dn) * sg;
     }
     __syncthreads();
 }
 
 MSG_DEV void waveguide64(double* d, int n, double sr, const msg_preset& pr, uint64_t seed, G64Shared& sh) {
     const int lines = pr.wg_lines > 1 ? pr.wg_lines : 1;
-    if (threadIdx.x == 0) {
-        nprng::Pcg64 g = nprng::default_rng(seed + 777);
-        for (int l = 0; l < lines; ++l) {
-            const double dl = rint((nprng::uniform(g, 0.4, pr.wg_max_ms) / 1000.0) * sr);
-            sh.ipar[l] = dl > 1.0 ? (int)fmin(dl, 2.0e9) : 1;
-            sh.par[0][l] = pr.wg_fb * nprng::uniform(g, 0.6, 0.98);
-            sh.par[1][l] = nprng::uniform(g, 0.15, 0.45);
-        }
-    }
-    __syncthreads();
-    for (int l = 0; l < lines; ++l) {
-        const int dly = sh.ipar[l];
-        const double gn = sh.par[0][l], mix = sh.par[1][l];
-        const int lanes = dly < n ? dly : n;
-        // v[t] = y[t] + g v[t - d]: independent recursions per residue t mod d
-        for (int r0 = threadIdx.x; r0 < lanes; r0 += G64_T) {
-            double v = 0.0;
-            for (int t = r0; t < n; t += dly) {
-                const double yt = d[t];
-                v = yt + gn * v;
-                d[t] = (1.0 - mix) * yt + mix * v;
+    nprng::Pcg64 g = nprng::default_rng(seed + 777);
+    for (int l0 = 0; l0 < lines; l0 += G64_MAXPAR) {
+        const int ln = lines - l0 < G64_MAXPAR ? lines - l0 : G64_MAXPAR;
+        if (threadIdx.x == 0) {
+            for (int l = 0; l < ln; ++l) {
+                const double dl = rint((nprng::uniform(g, 0.4, pr.wg_max_ms) / 1000.0) * sr);
+                sh.ipar[l] = dl > 1.0 ? (int)fmin(dl, 2.0e9) : 1;
+                sh.par[0][l] = pr.wg_fb * nprng::uniform(g, 0.6, 0.98);
+                sh.par[1][l] = nprng::uniform(g, 0.15, 0.45);
             }
         }
         __syncthreads();
+        for (int l = 0; l < ln; ++l) {
+            const int dly = sh.ipar[l];
+            const double gn = sh.par[0][l], mix = sh.par[1][l];
+            const int lanes = dly < n ? dly : n;
+            // v[t] = y[t] + g v[t - d]: independent recursions per residue t mod d
+            for (int r0 = threadIdx.x; r0 < lanes; r0 += G64_T) {
+                double v = 0.0;
+                for (int t = r0; t < n; t += dly) {
+                    const double yt = d[t];
+                    v = yt + gn * v;
+                    d[t] = (1.0 - mix) * yt + mix * v;
+                }
+            }
+            __syncthreads();
+        }
     }
 }
 
@@ -702,7 +756,7 @@ k_grain64(const msg_preset* __restrict__ presets, const Ev64* __restrict__ ev64,
         }
         if (ops & G64_LOCK) {                                   // MS:699-700
             boundary();
-            partial_lock64(buf, K, ev.stretch, pr.pl_top_n, pr.pl_neigh, sh, mask);
+            partial_lock64(buf, K, ev.stretch, pr.pl_top_n, pr.pl_neigh, sh, mask, GLOBAL ? scr : nullptr);
         } else if (ops & G64_STRETCH) {                         // MS:701-702
             boundary();
             const double inv_f = 1.0 / fmax(1e-12, ev.stretch);

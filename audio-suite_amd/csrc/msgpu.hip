@@ -216,6 +216,7 @@ struct msg_ctx {
     // per-batch buffers
     // device planner (MSGPU_DEVICE_PLAN=1)
     DevBuf<msg_preset> dp_presets;
+    DevBuf<double> dp_bp;                                 // breakpoint bank (device planner)
     DevBuf<int64_t> frag_len;
     DevBuf<msg_plan_info> info;
     DevBuf<int32_t> slot_base, tap_base;
@@ -259,7 +260,9 @@ struct msg_ctx {
     DevBuf<float2> sf_hspec, sf_xspec;
     DevBuf<float> sf_hf;                        // float taps of a k_fir8 filter
     // odd-length stereo rotation (kernels_stereo_odd.h)
-    std::map<int64_t, DevBuf<double2>> so_bp;  // chirp kernel spectra by n (float64)
+    std::map<int64_t, DevBuf<double2>> so_bp;  // chirp kernel spectra by n (float64), LRU-bounded
+    std::map<int64_t, uint64_t> so_bp_use;     // batch serial of each entry's last use
+    uint64_t batch_serial = 0;
     int so_row = 0, so_col = 0;                // transform-split limits (MSGPU_SO_ROW / _COL, tests; 0 = default)
     DevBuf<double2> so_A;
     DevBuf<float> so_r2;
@@ -452,8 +455,12 @@ static double bessel_j(int m, double x) {
 // stream: when non-null, also consider k_fir4s (N = 32768, P = B = 16384, Q <= 2:
 // one forward and one inverse transform per block plus, for Q = 2, one forward
 // per workgroup of kblk blocks) and report whether it won.
+// M8: the length of the filter k_fir8 would apply (its spectrum holds every
+// in-range ER tap and the whole IR, so it can be longer than an M capped at
+// out_n); the 65536-point candidate needs M8 + B - 1 <= N or it wraps.
 static void choose_fir(int64_t M, int64_t n, int& N, int& P, int& Q, bool fir8, bool* stream = nullptr,
-                       int kblk = 1) {
+                       int kblk = 1, int64_t M8 = -1) {
+    if (M8 < M) M8 = M;
     double best = 1e300;
     N = FIR_NMAX; P = (int)std::min<int64_t>(M, FIR_NMAX / 2); Q = (int)((M + P - 1) / P);
     for (int lg = 11; lg <= 15; ++lg) {   // k_fir2 / k_fir4 sizes: M = N/2 in 1024..16384
@@ -467,11 +474,11 @@ static void choose_fir(int64_t M, int64_t n, int& N, int& P, int& Q, bool fir8, 
             if (cost < best) { best = cost; N = NN; P = (int)pp; Q = q; }
         }
     }
-    if (fir8 && M < FIR8_N / 2 + FIR8_N / 4) {   // B >= N/4
-        const int64_t B = FIR8_N - M + 1;
+    if (fir8 && M8 < FIR8_N / 2 + FIR8_N / 4) {   // B >= N/4
+        const int64_t B = FIR8_N - M8 + 1;
         const int64_t blocks = (n + B - 1) / B;
         const double cost = (double)blocks * 2 * FIR8_N * 16 + (double)blocks * FIR8_N * 4.0;
-        if (cost < best) { best = cost; N = FIR8_N; P = (int)M; Q = 1; }
+        if (cost < best) { best = cost; N = FIR8_N; P = (int)M8; Q = 1; }
     }
     if (stream) {
         *stream = false;
@@ -511,14 +518,6 @@ static bool is_precise(const msg_preset& p) {
 static bool normal_driven(int gen_mode) {
     return gen_mode == MSG_GEN_GAUSSIAN_CLICK || gen_mode == MSG_GEN_NOISE_BURST || gen_mode == MSG_GEN_SKEWED ||
            gen_mode == MSG_GEN_RESONANT || gen_mode == MSG_GEN_FALLBACK;
-}
-
-static bool supported(const msg_preset& p, std::string& why) {
-    if (!is_precise(p)) return true;
-    if (p.res_modes > G64_MAXPAR_HOST && (p.flags & MSG_F_RES_BANK)) { why = "res_modes above 256"; return false; }
-    if (p.wav_count > G64_MAXPAR_HOST && p.gen_mode == MSG_GEN_WAVELET) { why = "wav_count above 256"; return false; }
-    if (p.wg_lines > G64_MAXPAR_HOST && (p.flags & MSG_F_WAVEGUIDE)) { why = "wg_lines above 256"; return false; }
-    return true;
 }
 
 // Stages of the float64 chain one event runs, with the reference's own
@@ -573,6 +572,24 @@ static hipError_t stream_done(msg_ctx* ctx, hipStream_t s) {
     ctx->last_stream = s;
     ctx->done_armed = true;
     return hipEventRecord(ctx->done_ev, s);
+}
+
+// Records done_ev on every exit of a call that may have enqueued work, the
+// early fail() returns included: a later batch on another stream
+// then still waits for this one before it reuses the staging arena and buffers.
+struct DoneGuard {
+    msg_ctx* ctx;
+    hipStream_t s;
+    bool armed = true;
+    DoneGuard(msg_ctx* c, hipStream_t st) : ctx(c), s(st) {}
+    hipError_t finish() { armed = false; return stream_done(ctx, s); }
+    ~DoneGuard() { if (armed) stream_done(ctx, s); }
+};
+
+// Wait for the context's last batch (not the whole device: other contexts'
+// streams keep running).
+static hipError_t wait_last(msg_ctx* ctx) {
+    return ctx->done_armed ? hipEventSynchronize(ctx->done_ev) : hipSuccess;
 }
 
 // ---------------------------------------------------------------------------
@@ -717,7 +734,7 @@ void msg_destroy(msg_ctx* ctx) {
     if (ctx->gate_ev) hipEventDestroy(ctx->gate_ev);
     if (ctx->done_ev) hipEventDestroy(ctx->done_ev);
     ctx->staging.release();
-    ctx->dp_presets.release(); ctx->frag_len.release(); ctx->info.release(); ctx->slot_base.release();
+    ctx->dp_presets.release(); ctx->dp_bp.release(); ctx->frag_len.release(); ctx->info.release(); ctx->slot_base.release();
     ctx->tap_base.release(); ctx->dp_events.release(); ctx->dp_er_off.release(); ctx->dp_er_gain.release();
     ctx->micro.release(); ctx->grain.release();
     ctx->mono_a.release(); ctx->mono_y.release(); ctx->hspec.release();
@@ -886,6 +903,7 @@ int msg_fir(msg_ctx* ctx, const float* x_dev, float* y_dev, int64_t n, int32_t n
     HIPCHK(ctx, hipSetDevice(ctx->device));
     hipStream_t s = (hipStream_t)stream;
     HIPCHK(ctx, stream_handover(ctx, s));
+    DoneGuard done(ctx, s);
     int N = 0, Pp = 0, Q = 0;
     choose_fir(M, n, N, Pp, Q, ctx->fir8);
     // Many partitions: a frequency-domain delay line (fir_fft.h) computes each
@@ -932,7 +950,7 @@ int msg_fir(msg_ctx* ctx, const float* x_dev, float* y_dev, int64_t n, int32_t n
         HIPCHK(ctx, launch_fir8_spec32(1, s, ctx->sf_irjobs.p, ctx->d_fir4tab, ctx->sf_hf.p, ctx->sf_hspec.p));
         HIPCHK(ctx, launch_fir8((unsigned)fj.size(), s, ctx->sf_prt.p, ctx->sf_jobs.p, ctx->d_fir4tab, ctx->sf_hspec.p,
                                 x_dev, y_dev));
-        HIPCHK(ctx, stream_done(ctx, s));
+        HIPCHK(ctx, done.finish());
         return MSG_OK;
     }
     std::string why;
@@ -984,7 +1002,7 @@ int msg_fir(msg_ctx* ctx, const float* x_dev, float* y_dev, int64_t n, int32_t n
                                 ctx->sf_hspec.p, x_dev, y_dev));
     // pageable-host H2D copies are staged before hipMemcpyAsync returns (as in
     // msg_render_batch), so the host vectors may go; the FIR runs asynchronously.
-    HIPCHK(ctx, stream_done(ctx, s));
+    HIPCHK(ctx, done.finish());
     return MSG_OK;
 }
 
@@ -1017,7 +1035,7 @@ int msg_last_meta(msg_ctx* ctx, int32_t preset, double* micro, double* grain, in
     if (e.n > cap) return fail(ctx, MSG_E_ARG, "meta buffer too small");
     std::vector<float> tmp(e.n);
     const int64_t off = ctx->h_prt[preset].pool_base + e.pool_off;
-    HIPCHK(ctx, hipDeviceSynchronize());
+    HIPCHK(ctx, wait_last(ctx));
     const int32_t l64 = ctx->h_last64.empty() ? -1 : ctx->h_last64[preset];
     if (l64 >= 0) {   // float64 chain: micro_last / grain_last kept in float64
         const int64_t o64 = ctx->h_ev64[l64].off64;
@@ -1052,26 +1070,27 @@ int msg_last_grain64(msg_ctx* ctx, int32_t preset, int32_t k, double* grain, int
     if (!grain) return MSG_OK;
     if (v.n > cap) return fail(ctx, MSG_E_ARG, "grain buffer too small");
     HIPCHK(ctx, hipSetDevice(ctx->device));
-    HIPCHK(ctx, hipDeviceSynchronize());
+    HIPCHK(ctx, wait_last(ctx));
     HIPCHK(ctx, hipMemcpy(grain, ctx->grain64.p + v.off64, v.n * sizeof(double), hipMemcpyDeviceToHost));
     return MSG_OK;
 }
 
 int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
-                     const double* const* irs, const int64_t* ir_lens, int32_t n_irs,
+                     const double* bp_bank, int64_t bp_pairs, const double* const* irs, const int64_t* ir_lens, int32_t n_irs,
                      const uint8_t* const* images, const int32_t* img_h, const int32_t* img_w,
                      int32_t n_images, float* out_dev, const int64_t* out_offsets, void* stream) {
     if (!ctx || !presets || P <= 0 || !out_dev || !out_offsets) return fail(ctx, MSG_E_ARG, "bad arguments");
     hipStream_t s = (hipStream_t)stream;
     HIPCHK(ctx, hipSetDevice(ctx->device));
     HIPCHK(ctx, stream_handover(ctx, s));
+    DoneGuard done(ctx, s);
     collect_stage_set(ctx, ctx->ev_cur);   // this batch's event set: from two batches back
     for (int p = 0; p < P; ++p) {
-        std::string why;
-        if (!supported(presets[p], why)) return fail(ctx, MSG_E_UNSUPPORTED, "preset " + std::to_string(p) + ": " + why);
-        if (presets[p].n_bp[0] > MSG_MAX_BP || presets[p].n_bp[1] > MSG_MAX_BP ||
-            presets[p].n_bp[2] > MSG_MAX_BP || presets[p].n_bp[3] > MSG_MAX_BP)
-            return fail(ctx, MSG_E_ARG, "too many breakpoints");
+        for (int l = 0; l < 4; ++l) {   // lanes inside the breakpoint bank
+            const int32_t nb = presets[p].n_bp[l], ob = presets[p].bp_off[l];
+            if (nb < 0 || (nb > 0 && (!bp_bank || ob < 0 || (int64_t)ob + nb > bp_pairs)))
+                return fail(ctx, MSG_E_ARG, "preset " + std::to_string(p) + ": breakpoint lane outside the bank");
+        }
         const int ic = presets[p].ir_conv;
         if (ic >= n_irs || (ic >= 0 && !irs)) return fail(ctx, MSG_E_ARG, "bad IR index");
     }
@@ -1105,7 +1124,7 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
         // ---- host plan (plan.h, the device planner's code) on the host pool:
         // no device round trip, so the call returns once the batch is enqueued
         HostPool& pool = HostPool::get();
-        pool.run(P, [&](int p) { msgplan::plan_sizes(presets[p], kHostZig, flen[p], info[p]); });
+        pool.run(P, [&](int p) { msgplan::plan_sizes(presets[p], bp_bank, kHostZig, flen[p], info[p]); });
         hA = hclock::now();
         if (int st = bases()) return st;
         ctx->h_events.resize(nslots);
@@ -1113,7 +1132,7 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
         ctx->h_er_gain.resize(ntaps);
         pool.run(P, [&](int p) {
             const bool er = (presets[p].flags & MSG_F_ER_CLOUD) != 0;
-            msgplan::plan_events(presets[p], kHostZig, flen[p], p, info[p], ctx->h_events.data() + slot_base[p],
+            msgplan::plan_events(presets[p], bp_bank, kHostZig, flen[p], p, info[p], ctx->h_events.data() + slot_base[p],
                                  er ? ctx->h_er_off.data() + tap_base[p] : nullptr,
                                  er ? ctx->h_er_gain.data() + tap_base[p] : nullptr, true);
         });
@@ -1125,9 +1144,12 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
         HIPCHK(ctx, ctx->dp_presets.ensure(P));
         HIPCHK(ctx, hipMemcpyAsync(ctx->dp_presets.p, presets, sizeof(msg_preset) * P, hipMemcpyHostToDevice, s));
         HIPCHK(ctx, hipMemcpyAsync(ctx->frag_len.p, flen.data(), sizeof(int64_t) * P, hipMemcpyHostToDevice, s));
+        HIPCHK(ctx, ctx->dp_bp.ensure((size_t)std::max<int64_t>(1, 2 * bp_pairs)));
+        if (bp_pairs > 0)
+            HIPCHK(ctx, hipMemcpyAsync(ctx->dp_bp.p, bp_bank, sizeof(double) * 2 * bp_pairs, hipMemcpyHostToDevice, s));
         const int pb = 64;
         hipLaunchKernelGGL(k_plan_sizes, dim3((P + pb - 1) / pb), dim3(pb), 0, s,
-                           ctx->dp_presets.p, P, ctx->frag_len.p, ctx->dzig, ctx->info.p);
+                           ctx->dp_presets.p, P, ctx->dp_bp.p, ctx->frag_len.p, ctx->dzig, ctx->info.p);
         HIPCHK(ctx, hipGetLastError());
         HIPCHK(ctx, hipMemcpyAsync(info.data(), ctx->info.p, sizeof(msg_plan_info) * P, hipMemcpyDeviceToHost, s));
         HIPCHK(ctx, hipStreamSynchronize(s));
@@ -1141,7 +1163,8 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
         HIPCHK(ctx, hipMemcpyAsync(ctx->slot_base.p, slot_base.data(), sizeof(int32_t) * P, hipMemcpyHostToDevice, s));
         HIPCHK(ctx, hipMemcpyAsync(ctx->tap_base.p, tap_base.data(), sizeof(int32_t) * P, hipMemcpyHostToDevice, s));
         hipLaunchKernelGGL(k_plan_events, dim3((P + pb - 1) / pb), dim3(pb), 0, s,
-                           ctx->dp_presets.p, P, ctx->frag_len.p, ctx->dzig, ctx->slot_base.p, ctx->tap_base.p,
+                           ctx->dp_presets.p, P, ctx->dp_bp.p, ctx->frag_len.p, ctx->dzig, ctx->slot_base.p,
+                           ctx->tap_base.p,
                            ctx->dp_events.p, ctx->dp_er_off.p, ctx->dp_er_gain.p, ctx->info.p);
         HIPCHK(ctx, hipGetLastError());
         ctx->h_events.resize(nslots);
@@ -1288,7 +1311,9 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
     // Taps of the space filter h = (delta + ER) * IR of preset p (MS:409-445), 0
     // without a FIR: the largest ER offset (planned span or actual) plus the IR
     // length, at most out_n (later taps never reach y[:out_n]).
-    auto h_taps = [&](int p) -> int64_t {
+    // full8: instead the length of the filter k_fir8's spectrum holds (every
+    // in-range tap, offset < out_n, and the whole IR), not capped at out_n.
+    auto h_taps = [&](int p, bool full8 = false) -> int64_t {
         const msg_preset& pr = presets[p];
         const bool er = (pr.flags & MSG_F_ER_CLOUD) != 0;
         const int ic = pr.ir_conv;
@@ -1297,6 +1322,7 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
         const int64_t irl = ir ? std::min<int64_t>(ir_lens[ic], 8192) : 1;
         const int64_t span = er ? std::max<int64_t>((int64_t)std::nearbyint(pr.er_max_ms / 1000.0 * (double)pr.base_sr),
                                                     tap_max[p]) : 0;
+        if (full8) return std::min<int64_t>(span, std::max<int64_t>(0, info[p].out_n - 1)) + irl;
         return std::max<int64_t>(1, std::min<int64_t>(span + irl, info[p].out_n));
     };
     // k_fir4s pays one extra forward transform per workgroup: it is offered only
@@ -1322,7 +1348,9 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
         f.M = h_taps(p);
         f.N = f.P = f.Q = 0;
         f.stream = false;
-        if (f.M > 0) choose_fir(f.M, info[p].out_n, f.N, f.P, f.Q, ctx->fir8, fir4s_ok ? &f.stream : nullptr, fir4s_k);
+        if (f.M > 0)
+            choose_fir(f.M, info[p].out_n, f.N, f.P, f.Q, ctx->fir8, fir4s_ok ? &f.stream : nullptr, fir4s_k,
+                       h_taps(p, true));
         const double w = std::min(std::max(presets[p].stereo_width, 0.0), 1.0);
         for (int m = -12; m <= 12; ++m) {
             const double j = bessel_j(std::abs(m), w * 0.9);
@@ -1538,13 +1566,6 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
                 v.cutoff_gen = e.cutoff_out * e.ufac;
                 v.stretch = e.stretch;
                 if (v.ops & G64_CEP) { v.save_off = save_sum; save_sum += e.n / 2 + 1; }
-                if (v.ops & G64_LOCK) {
-                    const int nb = e.n / 2;               // candidate bins 1..n/2
-                    const int cnt = pr.pl_top_n > 0 ? std::min(pr.pl_top_n, nb)
-                                                    : (pr.pl_top_n == 0 ? nb : std::max(0, nb + pr.pl_top_n));
-                    if (cnt > G64_MAXPAR_HOST)
-                        return fail(ctx, MSG_E_UNSUPPORTED, "partial lock of more than 256 peaks");
-                }
                 if (pr.gen_mode == MSG_GEN_WAVELET) {
                     // morlet_atom is max(16, round(..)) long, the grain max(128, ..): shorter
                     // atoms do not broadcast into the grain (MS:319, 166, 329)
@@ -1849,14 +1870,34 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
     }
     // ---- stereo, tanh, normalise ----
     stage_mark(ctx, 6, s);
+    ++ctx->batch_serial;
     for (int p : odd_presets) {           // odd out_n: R = irfft(rfft(roll(y, -dr)) . rot) (MS:432-435)
         const int64_t n = info[p].out_n;
         auto it = ctx->so_bp.find(n);
         if (it == ctx->so_bp.end()) {
+            // bound the cache (one entry per distinct odd length, for the
+            // life of the process): drop least-recently-used spectra of earlier
+            // batches while the cache holds more than 1 GiB (hipFree waits for them)
+            auto bytes = [&]() {
+                size_t b = 0;
+                for (auto& kv : ctx->so_bp) b += kv.second.cap * sizeof(double2);
+                return b;
+            };
+            while (bytes() > ((size_t)1 << 30)) {
+                int64_t victim = -1;
+                uint64_t oldest = ctx->batch_serial;
+                for (auto& kv : ctx->so_bp_use)
+                    if (kv.second < oldest) { oldest = kv.second; victim = kv.first; }
+                if (victim < 0) break;
+                ctx->so_bp[victim].release();
+                ctx->so_bp.erase(victim);
+                ctx->so_bp_use.erase(victim);
+            }
             it = ctx->so_bp.emplace(n, DevBuf<double2>()).first;
             HIPCHK(ctx, it->second.ensure(stereo_odd_len(n, ctx->so_row, ctx->so_col)));
             HIPCHK(ctx, launch_stereo_odd_kernel(n, ctx->so_row, ctx->so_col, it->second.p, ctx->so_A.p, s));
         }
+        ctx->so_bp_use[n] = ctx->batch_serial;
         const double w = std::min(std::max(presets[p].stereo_width, 0.0), 1.0);
         HIPCHK(ctx, launch_stereo_odd(n, ctx->so_row, ctx->so_col, prt[p].dr, w, yb + prt[p].y_off, it->second.p, ctx->so_A.p,
                                       ctx->so_r2.p + prt[p].r2_off, s));
@@ -1868,7 +1909,7 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
                        yb, ctx->so_r2.p, ctx->maxbits.p, out_dev);
     HIPCHK(ctx, hipGetLastError());
     stage_mark(ctx, 7, s);
-    HIPCHK(ctx, stream_done(ctx, s));
+    HIPCHK(ctx, done.finish());
     ctx->h_info = info;
     ctx->h_prt = prt;
     ctx->h_slot_base = slot_base;

@@ -18,17 +18,20 @@ using nprng::Zig;
 
 constexpr int32_t GEN_SR_CAP = 30000000;
 
-MSG_HD double eval_bp(const msg_preset& p, int lane, double t, double def) {
+// eval_breakpoints (MS:469-482): piecewise linear, held at the ends.  The lane's
+// points are (t, v) pairs in the batch's breakpoint bank, sorted by t on the host
+// exactly as parse_breakpoints sorts them (MS:452-467); any number of points.
+MSG_HD double eval_bp(const msg_preset& p, const double* bank, int lane, double t, double def) {
     const int n = p.n_bp[lane];
     if (n <= 0) return def;
-    const double* T = p.bp_t[lane];
-    const double* V = p.bp_v[lane];
-    if (t <= T[0]) return V[0];
-    if (t >= T[n - 1]) return V[n - 1];
+    const double* B = bank + 2 * (int64_t)p.bp_off[lane];   // B[2i] = t_i, B[2i + 1] = v_i
+    if (t <= B[0]) return B[1];
+    if (t >= B[2 * (n - 1)]) return B[2 * (n - 1) + 1];
     for (int i = 0; i + 1 < n; ++i) {
-        if (T[i] <= t && t <= T[i + 1]) {
-            const double a = (t - T[i]) / fmax(1e-12, (T[i + 1] - T[i]));
-            return (1 - a) * V[i] + a * V[i + 1];
+        const double t0 = B[2 * i], t1 = B[2 * i + 2];
+        if (t0 <= t && t <= t1) {
+            const double a = (t - t0) / fmax(1e-12, (t1 - t0));
+            return (1 - a) * B[2 * i + 1] + a * B[2 * i + 3];
         }
     }
     return def;
@@ -145,7 +148,8 @@ MSG_HD bool time_order_is_generation_order(const msg_preset& p) {
 // Phase 1: sizes only.  n_slots counts the events that must be materialised
 // before truncation (all children for Clustered); pool_len/max_n are bounds
 // over those slots.
-MSG_HD void plan_sizes(const msg_preset& p, const Zig& z, int64_t ir_frag_len, msg_plan_info& info) {
+MSG_HD void plan_sizes(const msg_preset& p, const double* bp, const Zig& z, int64_t ir_frag_len,
+                       msg_plan_info& info) {
     info.out_n = out_frames(p);
     const double unfold0 = fmax(1.0, p.time_unfold);
     info.design_sr = design_sr(p.base_sr, unfold0);
@@ -155,7 +159,7 @@ MSG_HD void plan_sizes(const msg_preset& p, const Zig& z, int64_t ir_frag_len, m
     const int32_t cap = p.max_grains;
     event_times(p, z, [&](double t) -> bool {
         if (ordered && slots >= cap) return false;
-        double uf = eval_bp(p, 1, t, unfold0);
+        double uf = eval_bp(p, bp, 1, t, unfold0);
         uf = fmax(1.0, uf);
         const int32_t n = event_grain_len(p, design_sr(p.base_sr, uf), ir_frag_len);
         ++slots;
@@ -183,10 +187,10 @@ MSG_HD void sort_by_time(msg_event* ev, int32_t n) {
 // n_events), exact pool offsets, and the ER taps.  sizes_known: info already
 // holds this preset's plan_sizes (the host batch path runs phase 1 for every
 // preset first); otherwise phase 1 runs here.
-MSG_HD void plan_events(const msg_preset& p, const Zig& z, int64_t ir_frag_len, int32_t preset_index,
+MSG_HD void plan_events(const msg_preset& p, const double* bp, const Zig& z, int64_t ir_frag_len, int32_t preset_index,
                         msg_plan_info& info, msg_event* ev, int32_t* er_off, double* er_gain,
                         bool sizes_known = false) {
-    if (!sizes_known) plan_sizes(p, z, ir_frag_len, info);
+    if (!sizes_known) plan_sizes(p, bp, z, ir_frag_len, info);
     int32_t k = 0;
     const bool ordered = time_order_is_generation_order(p);
     const int32_t cap = p.max_grains;
@@ -211,10 +215,10 @@ MSG_HD void plan_events(const msg_preset& p, const Zig& z, int64_t ir_frag_len, 
     for (int32_t i = 0; i < nev; ++i) {
         msg_event& e = ev[i];
         const double t0 = e.t0;
-        const double dens = eval_bp(p, 0, t0, rate);
-        double uf = eval_bp(p, 1, t0, unfold0);
-        const double cut = eval_bp(p, 2, t0, p.bandlimit_out_hz);
-        const double st = eval_bp(p, 3, t0, p.partial_stretch);
+        const double dens = eval_bp(p, bp, 0, t0, rate);
+        double uf = eval_bp(p, bp, 1, t0, unfold0);
+        const double cut = eval_bp(p, bp, 2, t0, p.bandlimit_out_hz);
+        const double st = eval_bp(p, bp, 3, t0, p.partial_stretch);
         double amp = 1.0;
         if (rate > 0) amp *= fmin(fmax(dens / fmax(1e-6, rate), 0.15), 4.0);
         amp *= nprng::uniform(g, 1.0 - ar, 1.0 + ar);

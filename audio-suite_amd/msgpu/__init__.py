@@ -16,9 +16,22 @@ def render(params, progress=None, device: int = 0):
     return _render(params, progress, device)
 
 
-def render_batch(params_list, device: int = 0):
+def render_batch(params_list, device: int = 0, devices=None):
+    """Render many presets; ``devices`` (e.g. range(8)) shards them across GPUs,
+    one worker process per GPU (multi.py; call before this process touches the GPU)."""
+    if devices is not None and len(list(devices)) > 1:
+        from .multi import pool_for
+        return pool_for(devices).render_batch(params_list)
+    if devices is not None:
+        device = int(list(devices)[0])
     from .dropin import render_batch as _rb
     return _rb(params_list, device)
+
+
+def DevicePool(devices, stub: bool = False):
+    """One render worker per GPU (multi.py); create it before any GPU call."""
+    from .multi import DevicePool as _P
+    return _P(devices, stub)
 
 
 def stft_mag_db(x, sr=None, win=2048, hop=256, max_frames=3000, device: int = 0):
@@ -41,7 +54,8 @@ def fir(x, h, device: int = 0):
     return y.cpu().numpy()
 
 
-def render_variations(base_params, seeds, unfolds, stretches, folder=None, device: int = 0, **kw):
-    """The app's batch render (on_batch, MS:1524-1596); see batch.py."""
+def render_variations(base_params, seeds, unfolds, stretches, folder=None, device: int = 0, devices=None, **kw):
+    """The app's batch render (on_batch, MS:1524-1596); see batch.py.  ``devices``
+    shards the variants across GPUs as render_batch does."""
     from .batch import render_variations as _rv
-    return _rv(base_params, seeds, unfolds, stretches, folder, device, **kw)
+    return _rv(base_params, seeds, unfolds, stretches, folder, device, devices=devices, **kw)

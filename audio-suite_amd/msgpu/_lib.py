@@ -12,8 +12,7 @@ import threading
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("MSGPU_LIB", os.path.join(HERE, "libmsgpu.so"))
-MAX_BP = 32
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 # status codes (msg_status)
 MSG_OK, MSG_E_VALUE, MSG_E_UNSUPPORTED, MSG_E_DEVICE, MSG_E_ARG = 0, 1, 2, 3, 4
@@ -39,7 +38,7 @@ class MsgPreset(C.Structure):
         ("pl_neigh", C.c_int32), ("res_modes", C.c_int32), ("wg_lines", C.c_int32), ("er_taps", C.c_int32),
         ("flags", C.c_uint32),
         ("ir_conv", C.c_int32), ("ir_frag", C.c_int32), ("image", C.c_int32),
-        ("n_bp", C.c_int32 * 4),
+        ("n_bp", C.c_int32 * 4), ("bp_off", C.c_int32 * 4),
         ("out_dur_s", C.c_double), ("time_unfold", C.c_double), ("peak", C.c_double),
         ("sat_drive", C.c_double), ("stereo_width", C.c_double),
         ("micro_ms", C.c_double), ("dust_density", C.c_double), ("noise_tilt", C.c_double),
@@ -62,8 +61,6 @@ class MsgPreset(C.Structure):
         ("er_max_ms", C.c_double),
         ("env_a", C.c_double), ("env_d", C.c_double), ("env_s", C.c_double), ("env_r", C.c_double),
         ("env_curve", C.c_double),
-        ("bp_t", (C.c_double * MAX_BP) * 4),
-        ("bp_v", (C.c_double * MAX_BP) * 4),
     ]
 
 
@@ -87,10 +84,10 @@ _PROTOS = {
     "msg_create": (C.c_void_p, [C.c_int]),
     "msg_destroy": (None, [C.c_void_p]),
     "msg_last_error": (C.c_char_p, [C.c_void_p]),
-    "msg_plan_host": (C.c_int, [C.POINTER(MsgPreset), C.POINTER(C.c_double), C.c_int64,
+    "msg_plan_host": (C.c_int, [C.POINTER(MsgPreset), C.POINTER(C.c_double), C.POINTER(C.c_double), C.c_int64,
                                 C.POINTER(MsgPlanInfo), C.POINTER(MsgEvent), C.c_int32,
                                 C.POINTER(C.c_int32), C.POINTER(C.c_double)]),
-    "msg_render_batch": (C.c_int, [C.c_void_p, C.POINTER(MsgPreset), C.c_int32,
+    "msg_render_batch": (C.c_int, [C.c_void_p, C.POINTER(MsgPreset), C.c_int32, C.POINTER(C.c_double), C.c_int64,
                                    C.POINTER(C.POINTER(C.c_double)), C.POINTER(C.c_int64), C.c_int32,
                                    C.POINTER(C.POINTER(C.c_uint8)), C.POINTER(C.c_int32),
                                    C.POINTER(C.c_int32), C.c_int32,

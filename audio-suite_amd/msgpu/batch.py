@@ -129,34 +129,46 @@ def _chunks(items, frames_of):
 
 
 def render_variations(base_params, seeds, unfolds, stretches, folder=None, device: int = 0,
-                      names="wav", progress=None):
-    """Render every (seed, unfold, stretch) variant of ``base_params`` on the device.
+                      names="wav", progress=None, devices=None):
+    """Render every (seed, unfold, stretch) variant of ``base_params`` on the device
+    (or, with ``devices``, sharded across those GPUs, multi.py).
 
     Returns a list of ``(name, audio, out_sr)`` in the reference's order (audio
     (out_n, 2) float32); with ``folder``, also writes each as a float32 WAV.
     ``progress(percent, text)`` gets the reference's status line per file.
     """
-    from .engine import default_engine
     from .pack import PackedBatch, out_frames
 
-    items = [(key, merged(p)) for key, p in variants(base_params, seeds, unfolds, stretches)]
-    total = max(1, len(items))
-    eng = default_engine(device)
+    base = merged(base_params)
+    pairs = variants(base, seeds, unfolds, stretches)
+    keys = [key for key, _ in pairs]
+    total = max(1, len(keys))
+    out_sr = int(base["base_sr"])                 # every variant has the template's out_n and out_sr
     results = []
-    done = 0
-    for chunk in _chunks(items, lambda it: out_frames(it[1])):
-        packed = PackedBatch([p for _, p in chunk])
+
+    def emit(key, audio):
+        name = variant_name(*key, out_sr, names)
+        if folder is not None:
+            write_wav_float32(os.path.join(folder, name), audio, out_sr)
+        results.append((name, audio, out_sr))
+        if progress:
+            progress(int(100 * len(results) / total), f"Batch: {len(results)}/{total} → {name}")
+
+    if devices is not None and len(list(devices)) > 1:
+        from .multi import pool_for
+        for key, audio in zip(keys, pool_for(devices).render_batch([p for _, p in pairs])):
+            emit(key, audio)
+        return results
+    if devices is not None:
+        device = int(list(devices)[0])
+    from .engine import default_engine
+    eng = default_engine(device)
+    frames = out_frames(base)
+    for chunk in _chunks(keys, lambda k: frames):
+        packed = PackedBatch.variants(base, chunk)   # the template packed once (MS:1578-1584)
         out = eng.render_packed(packed)
         eng.torch.cuda.synchronize(eng.device)
         host = out.cpu().numpy()
-        for ((sd, u, st), p), off, n in zip(chunk, packed.offsets, packed.out_n):
-            out_sr = int(p["base_sr"])
-            audio = host[off:off + n].copy()
-            name = variant_name(sd, u, st, out_sr, names)
-            if folder is not None:
-                write_wav_float32(os.path.join(folder, name), audio, out_sr)
-            results.append((name, audio, out_sr))
-            done += 1
-            if progress:
-                progress(int(100 * done / total), f"Batch: {done}/{total} → {name}")
+        for key, off, n in zip(chunk, packed.offsets, packed.out_n):
+            emit(key, host[off:off + n].copy())
     return results

@@ -77,7 +77,8 @@ class Engine:
             stream = torch.cuda.current_stream(self.device)
         with self._lock:
             st = L.lib().msg_render_batch(
-                self._ctx, packed.presets, packed.n, packed.ir_ptrs, packed.ir_lens, packed.n_irs,
+                self._ctx, packed.presets, packed.n, packed.bp_ptr, packed.bp_pairs,
+                packed.ir_ptrs, packed.ir_lens, packed.n_irs,
                 packed.img_ptrs, packed.img_h, packed.img_w, packed.n_images,
                 C.c_void_p(out.data_ptr()), packed._offsets_c, C.c_void_p(stream.cuda_stream))
             L.check(st, self._ctx)

@@ -251,8 +251,9 @@ def _n_events(params: dict) -> int:
     import ctypes as C
     from . import _lib as L
     from .pack import Banks, pack_preset
-    s = pack_preset(merged(params), Banks())
+    banks = Banks()
+    s = pack_preset(merged(params), banks)
     info = L.MsgPlanInfo()
-    L.check(L.lib().msg_plan_host(C.byref(s), None, 0, C.byref(info), None, 0, None, None), None)
+    L.check(L.lib().msg_plan_host(C.byref(s), banks.bp_array(), None, 0, C.byref(info), None, 0, None, None), None)
     return int(info.n_events)
 

@@ -180,6 +180,9 @@ def cpu_baseline(cfg, budget_s):
         O.render(p2)
         c2.append(time.perf_counter() - t1)
     return {"value": pframes / wall / 1e6, "unit": "Msamples/s", "cores": procs, "kind": "port",
+            "cores_note": f"one process per core of this rank's CPU share: min({CORES_PER_GPU}, affinity "
+                          f"{len(os.sched_getaffinity(0))}); the GPU box gives one GPU a 16-core share of a "
+                          "host whose affinity lists all of its cores (nproc shows the whole machine)",
             "single_core": round(single, 4),
             "per_render_ms_1core": {"C2": round(1e3 * float(np.median(c2)), 2), cfg: round(1e3 * dt / done, 2)},
             "sample": f"{cfg} presets rendered by oracle/msound_oracle.py (NumPy restatement of "
@@ -219,19 +222,10 @@ def dropin_latency(cpu, reps=5):
 
 
 def pin_rank_cpus(local, local_world):
-    """Before the first GPU call: pin this rank to its own contiguous slice of the
-    process's CPU affinity (one host worker pool per GPU; on
-    a node whose GPUs 0..3 / 4..7 hang off NUMA nodes 0 / 1 the contiguous slices
-    follow the NUMA split) and size the library's host pool to the slice
-    (MSGPU_HOST_THREADS, at most CORES_PER_GPU).  Returns the slice."""
-    cpus = sorted(os.sched_getaffinity(0))
-    if local_world > 1 and len(cpus) >= local_world:
-        per = len(cpus) // local_world
-        cpus = cpus[local * per:(local + 1) * per]
-        os.sched_setaffinity(0, cpus)
-    cpus = cpus[:max(1, min(len(cpus), CORES_PER_GPU))] if local_world > 1 else cpus
-    os.environ.setdefault("MSGPU_HOST_THREADS", str(max(1, min(len(cpus), CORES_PER_GPU))))
-    return cpus
+    """Before the first GPU call: this rank's slice of the process affinity and
+    host pool size (msgpu.shard.pin_worker_cpus, shared with msgpu.DevicePool)."""
+    from msgpu.shard import pin_worker_cpus
+    return pin_worker_cpus(local, local_world)
 
 
 def host_threads():
@@ -244,57 +238,7 @@ def rank_seeds(rank, batch):
     return [1000 + rank * batch + b for b in range(batch)]
 
 
-def preset_cost(info, taps=8192):
-    """Predicted device cost of one preset from its plan:
-    sum n log2 n over its grains + out_n (log2 L + taps / L), L the FIR block."""
-    n_ev = max(int(info.n_events), 0)
-    if n_ev == 0:
-        grain = 0.0
-    else:
-        n = max(float(info.pool_len) / n_ev, 2.0)
-        grain = float(info.pool_len) * np.log2(n)
-    L = 16384.0
-    return grain + float(info.out_n) * (np.log2(L) + taps / L)
-
-
-def balance(costs, world):
-    """Contiguous partition of presets into ``world`` chunks of near-equal total
-    cost (greedy on the prefix sum: chunk r ends where the running cost crosses
-    (r + 1) / world of the total).  Returns world + 1 cut indices."""
-    c = np.asarray(costs, dtype=np.float64)
-    n = c.size
-    pref = np.concatenate([[0.0], np.cumsum(c)])
-    total = pref[-1]
-    cuts = [0]
-    for r in range(1, world):
-        target = total * r / world
-        k = int(np.searchsorted(pref, target, side="left"))
-        # pick the closer of the two prefix points around the target
-        if k > 0 and abs(pref[k - 1] - target) <= abs(pref[min(k, n)] - target):
-            k -= 1
-        cuts.append(min(max(k, cuts[-1]), n))
-    cuts.append(n)
-    return cuts
-
-
-def plan_costs(params_list):
-    """Host plans (msg_plan_host, the device planner's code on the CPU) -> costs."""
-    import ctypes as C
-    from msgpu import _lib as L
-    from msgpu.pack import Banks, pack_preset, fragment_source
-    lib = L.lib()
-    out = []
-    for p in params_list:
-        s = pack_preset(p, Banks())
-        info = L.MsgPlanInfo()
-        frag = fragment_source(p) if p.get("gen_mode") == "IR fragment" else None
-        fp = frag.ctypes.data_as(C.POINTER(C.c_double)) if frag is not None else None
-        L.check(lib.msg_plan_host(C.byref(s), fp, 0 if frag is None else frag.size, C.byref(info),
-                                  None, 0, None, None), None)
-        taps = len(p["_ir_audio"][:int(p["space_ir_max_samps"])][:8192]) if p.get("space_ir_on") and \
-            p.get("_ir_audio") is not None else 0
-        out.append(preset_cost(info, taps))
-    return out
+from msgpu.shard import balance, plan_costs, preset_cost  # noqa: E402,F401  (the library's sharding)
 
 
 class Comm:
@@ -402,16 +346,24 @@ class GpuRunner:
         S = len(self.engs)
         w.outs = [self.engs[i % S].alloc_output(p) for i, p in enumerate(w.subs)]
 
-    def step(self, w: Workload):
+    def step(self, w: Workload, from_dicts: bool = False):
+        """One render of the workload; from_dicts: each sub-batch's param dicts are
+        packed again inside the step (what msgpu.render_batch's caller pays)."""
         S = len(self.engs)
+
+        def sub(i):
+            if not from_dicts:
+                return w.subs[i]
+            from msgpu.pack import PackedBatch
+            return PackedBatch(w.params[w.cut[i]:w.cut[i + 1]])
         if self.pool is None:
-            for i, (p, o) in enumerate(zip(w.subs, w.outs)):
-                self.engs[i % S].render_packed(p, o, self.streams[i % S])
+            for i, o in enumerate(w.outs):
+                self.engs[i % S].render_packed(sub(i), o, self.streams[i % S])
             return
 
         def run(e):
             for i in range(e, len(w.subs), S):
-                self.engs[e].render_packed(w.subs[i], w.outs[i], self.streams[e])
+                self.engs[e].render_packed(sub(i), w.outs[i], self.streams[e])
         for f in [self.pool.submit(run, e) for e in range(min(S, len(w.subs)))]:
             f.result()
 
@@ -479,30 +431,30 @@ class DryRunner:
     def prepare(self, w):
         pass
 
-    def step(self, w):
+    def step(self, w, **kw):
         time.sleep(self.delay)
 
     def sync(self):
         pass
 
 
-def timed(runner, w, steps, warmup, comm):
+def timed(runner, w, steps, warmup, comm, **kw):
     """W untimed steps, then K steps bracketed by barrier + device sync; returns
     (this rank's seconds, max over ranks)."""
     for _ in range(warmup):
-        runner.step(w)
+        runner.step(w, **kw)
     runner.sync()
     comm.barrier()
     t0 = time.perf_counter()
     for _ in range(steps):
-        runner.step(w)
+        runner.step(w, **kw)
     runner.sync()
     comm.barrier()
     mine = time.perf_counter() - t0
     return mine, comm.max(mine)
 
 
-def measure(runner, cfg, seeds, sub, steps, warmup, comm, irs, golden, iso_steps=0):
+def measure(runner, cfg, seeds, sub, steps, warmup, comm, irs, golden, iso_steps=0, from_dicts_steps=0):
     """Time one config on this rank; returns the point record (rank 0 fills it)."""
     world = comm.world
     w = Workload(cfg, seeds, sub, irs, len(runner.engs))
@@ -542,18 +494,39 @@ def measure(runner, cfg, seeds, sub, steps, warmup, comm, irs, golden, iso_steps
                                   for k in sb if stages.get(k, 0) > 0},
         "check": check, "_rank_s": mine,
     }
+    if from_dicts_steps > 0:
+        # the same steps with the dict -> msg_preset packing inside each step
+        # (native packer, msgpu/_mspack): what a caller of msgpu.render_batch pays
+        _, el2 = timed(runner, w, from_dicts_steps, 1, comm, from_dicts=True)
+        rec["from_dicts"] = {"value": round(w.frames * world * from_dicts_steps / el2 / 1e6, 3),
+                             "ms_per_step": round(el2 / from_dicts_steps * 1e3, 3), "steps": from_dicts_steps,
+                             "pack_ms_per_step": round(pack_ms(w), 3),
+                             "note": "packing of every sub-batch's param dicts inside the timed step"}
     if iso_steps > 0:
         rec["roofline_isolated"] = isolated(runner, w, iso_steps, sb, cfg)
     runner.free(w)
     return rec
 
 
+def pack_ms(w, reps=5):
+    """Host time to pack the workload's param dicts (all sub-batches), best of reps."""
+    from msgpu.pack import PackedBatch
+    best = 1e9
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        for i in range(len(w.subs)):
+            PackedBatch(w.params[w.cut[i]:w.cut[i + 1]])
+        best = min(best, time.perf_counter() - t0)
+    return best * 1e3
+
+
 def isolated(runner, w, iso_steps, sb, cfg):
     """The whole batch on one stream, kernels not sharing the GPU."""
     from msgpu.pack import PackedBatch
-    if len(w.subs) != len(runner.engs):
-        return None                      # sub-batched configs: one launch is not the whole batch
-    packed = PackedBatch(w.params)
+    whole = len(w.subs) == len(runner.engs)
+    # sub-batched configs (C5): the whole batch does not fit one launch, so the
+    # isolated figure is one sub-batch alone on one stream, with its own bytes
+    packed = PackedBatch(w.params) if whole else w.subs[0]
     e = runner.engs[0]
     o = e.alloc_output(packed)
     e.render_packed(packed, o, runner.streams[0])
@@ -564,13 +537,24 @@ def isolated(runner, w, iso_steps, sb, cfg):
     runner.sync()
     e.set_profiling(False)
     iso = {n: round(float(v), 4) for n, v in zip(STAGE_NAMES, e.stage_times())}
+    if not whole:
+        sb = stage_bytes(e.last_plan())
     dom = max(KERNEL_STAGES, key=lambda k: iso[k])
     ach = sb[dom] / (iso[dom] * 1e-3) / 1e9
+    kern = [k for k in KERNEL_STAGES if iso.get(k, 0) > 0]
+    tot_bytes = sum(sb[k] for k in kern)
+    tot_ms = sum(iso[k] for k in kern)
     del o
     return {"kernel": kernel_label(dom), "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
             "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "algorithmic_bytes": sb[dom],
-            "kernel_ms": iso[dom], "traffic": measured_traffic(STAGE_KERNEL[dom], cfg, len(w.params)),
-            "stage_ms": iso, "note": f"whole batch on one stream, {iso_steps} renders after the timed region"}
+            "kernel_ms": iso[dom], "traffic": measured_traffic(STAGE_KERNEL[dom], cfg, packed.n),
+            "stage_ms": iso,
+            "stage_frac": {k: round(sb[k] / (iso[k] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) for k in kern},
+            "kernels_frac": round(tot_bytes / (tot_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+            "presets": packed.n,
+            "note": (f"whole batch on one stream, {iso_steps} renders after the timed region" if whole else
+                     f"one sub-batch of {packed.n} presets alone on one stream, {iso_steps} renders after the "
+                     "timed region")}
 
 
 # ---------------------------------------------------------------------------
@@ -594,6 +578,8 @@ def parse():
                          "runs beside that sub-batch's FIR and stereo passes rather than its spectral kernel "
                          "(C3: 9.43-9.45 vs 9.52-9.54 ms per step ungated, profiles/r02ze_gate.txt)")
     ap.add_argument("--iso-steps", type=int, default=3, help="single-stream renders for roofline_isolated")
+    ap.add_argument("--from-dicts-steps", type=int, default=20,
+                    help="steps timed again with the param-dict packing inside the step (0 = skip)")
     ap.add_argument("--enqueue", choices=["threads", "serial"], default="threads",
                     help="enqueue the contexts' sub-batches from one host thread each (threads) or in turn")
     ap.add_argument("--points", default="H48,C4,C5",
@@ -677,14 +663,16 @@ def main():
         gate = None if args.gate in ("", "none") else tuple(int(v) for v in args.gate.split(","))
         runner = GpuRunner(local, max(1, args.streams), gate, threaded=args.enqueue == "threads")
         head = measure(runner, cfg, seeds, default_sub(cfg, args, batch), args.steps, args.warmup, comm, irs,
-                       golden, iso_steps=args.iso_steps)
+                       golden, iso_steps=args.iso_steps, from_dicts_steps=args.from_dicts_steps)
         points = {}
         for pc in [c for c in args.points.split(",") if c and c != cfg]:
             pb = default_batch(pc, args)
             # C5's 8 sub-batches of 128 ran 3 % slower gated (135.2 vs 139.5 ms per step)
             runner.set_gate(None if pc in GATE_OFF else gate)
-            points[pc] = measure(runner, pc, rank_seeds(rank, pb), default_sub(pc, args, pb),
-                                 max(args.point_steps, POINT_STEPS_MIN.get(pc, 0)), 3, comm, irs, golden)
+            psteps = max(args.point_steps, POINT_STEPS_MIN.get(pc, 0))
+            points[pc] = measure(runner, pc, rank_seeds(rank, pb), default_sub(pc, args, pb), psteps, 3, comm,
+                                 irs, golden, iso_steps=args.iso_steps,
+                                 from_dicts_steps=psteps if (pc == "H48" and args.from_dicts_steps) else 0)
         lat = dropin_latency(cpu) if (rank == 0 and world == 1 and not args.no_cpu) else None
         ranks = comm.gather({"rank": rank, "pid": os.getpid(), "device": local,
                              "cpus": [cpus[0], cpus[-1], len(cpus)], "host_threads": host_threads(),

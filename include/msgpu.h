@@ -24,8 +24,7 @@
 extern "C" {
 #endif
 
-#define MSG_ABI_VERSION 1
-#define MSG_MAX_BP 32          /* breakpoints per lane (MS:452-467) */
+#define MSG_ABI_VERSION 2
 
 /* gen_mode (MS:919-923) */
 enum msg_gen_mode {
@@ -58,6 +57,7 @@ typedef struct msg_preset {
     int32_t ir_frag;           /* index into the IR bank for the "IR fragment" source   */
     int32_t image;             /* index into the image bank, -1 = none                  */
     int32_t n_bp[4];           /* points in lanes density, unfold, cutoff, stretch      */
+    int32_t bp_off[4];         /* first point of each lane in the breakpoint bank       */
     double out_dur_s, time_unfold, peak, sat_drive, stereo_width;
     double micro_ms, dust_density, noise_tilt, ring_hz, ring_decay_ms;
     double crackle_alpha, crackle_density;
@@ -72,9 +72,13 @@ typedef struct msg_preset {
     double event_feedback_amt, spectral_imprint_amt, spectral_imprint_smooth;
     double er_max_ms;
     double env_a, env_d, env_s, env_r, env_curve;
-    double bp_t[4][MSG_MAX_BP];
-    double bp_v[4][MSG_MAX_BP];
 } msg_preset;
+
+/* Breakpoint lanes (MS:452-482) live outside msg_preset, any number of points:
+ * a breakpoint bank is an array of (t, v) double pairs, bank[2 i] = t_i,
+ * bank[2 i + 1] = v_i; lane l of a preset is the n_bp[l] pairs starting at pair
+ * bp_off[l], sorted by t the way parse_breakpoints sorts them (MS:466).  A
+ * preset without lanes may pass a NULL bank.                                  */
 
 /* One micro event after planning (MS:633-755). */
 typedef struct msg_event {
@@ -115,13 +119,16 @@ void        msg_destroy(msg_ctx* ctx);
 const char* msg_last_error(msg_ctx* ctx);   /* ctx may be NULL (creation errors) */
 
 /* Host-side plan of one preset (the same code the device planner runs).
+ * bp_bank: the breakpoint bank its lanes index (NULL without lanes).
  * events: capacity max_events; *n_events receives the event count.
  * er_off / er_gain: capacity preset->er_taps (MS:410-417).               */
-int msg_plan_host(const msg_preset* preset, const double* ir_frag, int64_t ir_frag_len,
+int msg_plan_host(const msg_preset* preset, const double* bp_bank, const double* ir_frag, int64_t ir_frag_len,
                   msg_plan_info* info, msg_event* events, int32_t max_events,
                   int32_t* er_off, double* er_gain);
 
 /* Render a batch of presets on the context's device.
+ * bp_bank / bp_pairs: the batch's breakpoint bank (host, bp_pairs (t, v) pairs;
+ *      NULL / 0 when no preset has a lane).
  * irs: host pointers to IR bank entries (float64 mono), ir_lens their lengths.
  *      The conv kernel of a preset uses irs[ir_conv] (already cut to
  *      space_ir_max_samps and <= 8192 taps by the caller, MS:443, 773).
@@ -131,6 +138,7 @@ int msg_plan_host(const msg_preset* preset, const double* ir_frag, int64_t ir_fr
  * stream: hipStream_t (NULL = default stream).  The call returns after the
  *      work is enqueued; synchronise the stream before reading out_dev.      */
 int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t n_presets,
+                     const double* bp_bank, int64_t bp_pairs,
                      const double* const* irs, const int64_t* ir_lens, int32_t n_irs,
                      const uint8_t* const* images, const int32_t* img_h, const int32_t* img_w,
                      int32_t n_images,

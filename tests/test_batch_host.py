@@ -48,3 +48,18 @@ def test_chunks_bound_presets_and_frames(monkeypatch):
     assert ch == [[0, 1], [2, 3], [4, 5], [6, 7]]
     ch = list(B._chunks(list(range(7)), lambda i: 1))
     assert ch == [[0, 1, 2], [3, 4, 5], [6]]
+
+
+def test_template_variants_pack_like_each_dict():
+    """PackedBatch.variants (template packed once, three fields patched) equals
+    packing every variant dict of the on_batch loop (MS:1578-1584)."""
+    import ctypes as C
+    from msgpu.pack import PackedBatch
+    from msgpu.params import merged
+    base = merged(gen_mode="Noise burst", event_process="Poisson", bp_unfold="0:5, 1:9", out_dur_s=0.3)
+    v = B.variants(base, "1001, 1002, 99", "15, 2.5", "0.9,1,1.75")
+    a = PackedBatch.variants(base, [k for k, _ in v])
+    b = PackedBatch([p for _, p in v])
+    raw = lambda pk: bytes(C.string_at(C.addressof(pk.presets), C.sizeof(pk.presets)))  # noqa: E731
+    assert a.n == 18 and raw(a) == raw(b)
+    assert np.array_equal(a.out_n, b.out_n) and list(a._bp) == list(b._bp)

@@ -153,7 +153,8 @@ def test_fir8_kernel_agrees(msgpu, irs, full_renders):
     half-size transforms on the k_fir4 engine); MSGPU_FIR8=0 puts them back on
     k_fir4 (N = 32 768, two partitions).  Both match the reference / oracle, and
     each other to float32 rounding: C3 (25 473 taps), the 192 kHz ER + IR case,
-    an IR-only and an ER-only filter."""
+    an IR-only and an ER-only filter, and two ER + IR filters longer than the
+    output (the block must fit the unclipped filter)."""
     import os
     import torch
     from oracle import msound_oracle as O
@@ -166,7 +167,13 @@ def test_fir8_kernel_agrees(msgpu, irs, full_renders):
               msgpu.merged(base, base_sr=384000, out_dur_s=0.2, space_ir_on=True, seed=5, er_cloud_on=True,
                            er_max_ms=90.0, space_ir_max_samps=8192),
               msgpu.merged(base, base_sr=384000, out_dur_s=0.3, space_ir_on=False, seed=6, er_cloud_on=True,
-                           er_max_ms=60.0)]
+                           er_max_ms=60.0),
+              # taps + IR longer than the output (28 800 + 8192 > 32 640 frames): k_fir8's
+              # spectrum holds the whole filter, so its block must leave room for all of it
+              msgpu.merged(base, base_sr=192000, out_dur_s=0.17, space_ir_on=True, seed=8, er_cloud_on=True,
+                           er_max_ms=150.0, er_taps=600, space_ir_max_samps=8192),
+              msgpu.merged(base, base_sr=176400, out_dur_s=0.19, space_ir_on=True, seed=9, er_cloud_on=True,
+                           er_max_ms=140.0, space_ir_max_samps=8192)]
     packed = PackedBatch(params)
     outs = {}
     for flag in ("1", "0"):

@@ -17,16 +17,18 @@ from oracle import msound_oracle as O
 
 def host_plan(p):
     lib = L.lib()
-    s = pack_preset(p, Banks())
+    banks = Banks()
+    s = pack_preset(p, banks)
+    bp = banks.bp_array()
     frag = fragment_source(merged(p)) if merged(p)["gen_mode"] == "IR fragment" else None
     flen = 0 if frag is None else frag.size
     info = L.MsgPlanInfo()
-    assert lib.msg_plan_host(C.byref(s), None, flen, C.byref(info), None, 0, None, None) == 0
+    assert lib.msg_plan_host(C.byref(s), bp, None, flen, C.byref(info), None, 0, None, None) == 0
     ev = (L.MsgEvent * max(1, info.n_slots))()
     ntap = max(1, s.er_taps)
     off = np.zeros(ntap, dtype=np.int32)
     gain = np.zeros(ntap, dtype=np.float64)
-    st = lib.msg_plan_host(C.byref(s), None, flen, C.byref(info), ev, info.n_slots,
+    st = lib.msg_plan_host(C.byref(s), bp, None, flen, C.byref(info), ev, info.n_slots,
                            off.ctypes.data_as(C.POINTER(C.c_int32)), gain.ctypes.data_as(C.POINTER(C.c_double)))
     assert st == 0
     return info, list(ev)[:info.n_events], off, gain
@@ -93,3 +95,25 @@ def test_grain_lengths_by_mode(irs):
             p = merged(gen_mode=mode, event_process="Poisson", out_dur_s=0.7, micro_ms=0.05,
                        _ir_audio=ir)
             check_plan(p)
+
+
+def _lane(n, seed, t_max, v_lo, v_hi, shuffle=True):
+    """A lane string of n 't:v' points (unsorted, with repeated times)."""
+    rng = np.random.default_rng(seed)
+    t = np.round(rng.uniform(0, t_max, n), 3)
+    t[n // 3] = t[n // 2]                      # a repeated time: stable sort keeps input order
+    v = np.round(rng.uniform(v_lo, v_hi, n), 2)
+    order = rng.permutation(n) if shuffle else np.arange(n)
+    return ", ".join(f"{t[i]}:{v[i]}" for i in order)
+
+
+@pytest.mark.parametrize("npts", [33, 40, 200])
+def test_long_breakpoint_lanes(npts):
+    """Lanes beyond the 32 points of the round-3 ABI (the UI's QLineEdits take any
+    number, MS:1070-1073): every lane of every event evaluated as MS:469-482."""
+    for seed in (3, 11):
+        p = merged(event_process="Poisson", seed=seed, out_dur_s=2.0, base_sr=48000, grains_per_sec=40.0,
+                   bp_density=_lane(npts, seed, 2.2, 2, 60), bp_unfold=_lane(npts, seed + 1, 2.2, 1, 60),
+                   bp_cutoff=_lane(npts, seed + 2, 2.2, 500, 20000), bp_stretch=_lane(npts, seed + 3, 2.2, 0.4, 3.5))
+        assert len(O.parse_breakpoints(p["bp_unfold"])) == npts
+        check_plan(p)
