@@ -2,6 +2,7 @@
 // kernel (spec3.h) for the 30 MHz hot length.
 #include "spec3.h"
 #include "launch.h"
+#include <cstdlib>
 
 void spec3_init_attrs() {
     (void)hipFuncSetAttribute((const void*)k_spec3<Spec3P18750>, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -21,7 +22,11 @@ bool spec3_eligible(int n, int ops, int gen_sr, double cutoff_gen, double roll, 
     if (ops & (SPEC_TILT_NOISE | SPEC_TILT_SKEW | SPEC_WARP)) return false;
     if (!(ops & SPEC_LOWPASS)) return false;
     const Spec3Band b = s3_band(n, gen_sr, cutoff_gen, roll, (ops & SPEC_STRETCH) != 0, stretch);
-    if (!(b.ky <= P::M / 2 && b.kz <= b.ky && s3_band_fits<P>(b.kz, b.ky))) return false;
+    if (b.kz > b.ky) return false;
+    if (b.ky <= P::M / 2 ? !s3_band_fits<P>(b.kz, b.ky)                       // narrow: X, Z' halves in LDS
+                         : 2 * ((b.kz + 15) & ~15) > P::BUF) return false;     // wide: Z[k], Z[M-k], then X
+    static const bool wide_on = !(getenv("MSGPU_S3_WIDE") && getenv("MSGPU_S3_WIDE")[0] == '0');   // A/B switch
+    if (b.ky > P::M / 2 && !wide_on) return false;
     *kb = b.kb; *kz = b.kz; *ky = b.ky; *inv_f = b.inv_f;
     return true;
 }

@@ -761,17 +761,15 @@ MSG_DEV void stereo_r4(const PresetRt& r, const float* w, int u, float (&R)[4], 
     R[0] = a01.x; R[1] = a01.y; R[2] = a23.x; R[3] = a23.y;
 }
 
-__global__ void __launch_bounds__(ST_T)
-k_stereo_max(const PresetRt* __restrict__ rt, const int32_t* __restrict__ st_begin, int n_presets,
-             const float* __restrict__ ybuf, const float* __restrict__ rbuf, unsigned* __restrict__ maxbits) {
-    __shared__ __attribute__((aligned(16))) float w[ST_WIN];
-    __shared__ float wm[ST_T / 64];
-    const int b = job_order(MSG_STMAX_REV);
-    const int p = find_preset(st_begin, n_presets, b);
-    const PresetRt& r = rt[p];
+// max|L|, |R| of one tile of preset p into maxbits[p]; with stats, also
+// sum y^2 and sum (1 + (d y)^2)^-2 over the tile's frames into stats[2p ..]
+// (the float64 FIR's error predictor, kernels_fir64.h).
+MSG_DEV void stereo_max_tile(const PresetRt& r, int p, int tile, const float* __restrict__ ybuf,
+                             const float* __restrict__ rbuf, unsigned* __restrict__ maxbits, double* __restrict__ stats,
+                             bool with_r2, float* w, float* wm) {
     const float* y = ybuf + r.y_off;
     const int n = (int)r.out_n;
-    const StereoTile st = stereo_tile(r, (int64_t)(b - st_begin[p]) * ST_TILE);
+    const StereoTile st = stereo_tile(r, (int64_t)tile * ST_TILE);
     // max|L| over all frames equals max|y| (L is a rotation of y).  With the
     // Bessel FIR, the centre tap of output u + k is y[(t0 + u + k + dr) mod n]:
     // over all tiles those cover every sample once, so max|y| comes from the
@@ -798,7 +796,14 @@ k_stereo_max(const PresetRt* __restrict__ rt, const int32_t* __restrict__ st_beg
         }
     }
     __syncthreads();
-    float m = 0.f;
+    const float d = r.drive > 0.f ? r.drive : 0.f;
+    float m = 0.f, s2 = 0.f, sq = 0.f;
+    auto stat = [&](float v) {
+        const float u = d * v;
+        const float q = __builtin_amdgcn_rcpf(fmaf(u, u, 1.f));
+        s2 = fmaf(v, v, s2);
+        sq = fmaf(q, q, sq);
+    };
 #pragma unroll
     for (int i = 0; i < ST_RUNS; ++i) {
         const int u = 4 * (threadIdx.x + i * ST_T);
@@ -808,24 +813,74 @@ k_stereo_max(const PresetRt* __restrict__ rt, const int32_t* __restrict__ st_beg
                 stereo_r4(r, w, u, R, x);
 #pragma unroll
                 for (int k = 0; k < 4; ++k)
-                    if (u + k < st.cnt) m = fmaxf(m, fmaxf(fabsf(R[k]), fabsf(x[k + 24])));
+                    if (u + k < st.cnt) {
+                        m = fmaxf(m, fmaxf(fabsf(R[k]), fabsf(x[k + 24])));
+                        if (stats) stat(x[k + 24]);
+                    }
             }
             continue;
         }
         m = fmaxf(m, fmaxf(fmaxf(fabsf(yv[i].x), fabsf(yv[i].y)), fmaxf(fabsf(yv[i].z), fabsf(yv[i].w))));
-        if (r.stereo_fir == 2) {
+        if (stats) {
+            if (u < st.cnt) stat(yv[i].x);
+            if (u + 1 < st.cnt) stat(yv[i].y);
+            if (u + 2 < st.cnt) stat(yv[i].z);
+            if (u + 3 < st.cnt) stat(yv[i].w);
+        }
+        if (r.stereo_fir == 2 && with_r2) {
 #pragma unroll
             for (int k = 0; k < 4; ++k)
                 if (u + k < st.cnt) m = fmaxf(m, fabsf(rbuf[r.r2_off + st.t0 + u + k]));
         }
     }
     for (int off = 32; off > 0; off >>= 1) m = fmaxf(m, __shfl_xor(m, off));
-    if ((threadIdx.x & 63) == 0) wm[threadIdx.x >> 6] = m;
+    if (stats)
+        for (int off = 32; off > 0; off >>= 1) { s2 += __shfl_xor(s2, off); sq += __shfl_xor(sq, off); }
+    if ((threadIdx.x & 63) == 0) {
+        wm[threadIdx.x >> 6] = m;
+        wm[ST_T / 64 + (threadIdx.x >> 6)] = s2;
+        wm[2 * (ST_T / 64) + (threadIdx.x >> 6)] = sq;
+    }
     __syncthreads();
     if (threadIdx.x == 0) {
         float v = wm[0];
         for (int k = 1; k < ST_T / 64; ++k) v = fmaxf(v, wm[k]);
         atomicMax(maxbits + p, __float_as_uint(v));
+        if (stats) {
+            double a = 0.0, b = 0.0;
+            for (int k = 0; k < ST_T / 64; ++k) { a += (double)wm[ST_T / 64 + k]; b += (double)wm[2 * (ST_T / 64) + k]; }
+            atomicAdd(stats + 2 * p, a);
+            atomicAdd(stats + 2 * p + 1, b);
+        }
+    }
+}
+
+__global__ void __launch_bounds__(ST_T)
+k_stereo_max(const PresetRt* __restrict__ rt, const int32_t* __restrict__ st_begin, int n_presets,
+             const float* __restrict__ ybuf, const float* __restrict__ rbuf, unsigned* __restrict__ maxbits,
+             double* __restrict__ stats, int with_r2) {
+    __shared__ __attribute__((aligned(16))) float w[ST_WIN];
+    __shared__ float wm[3 * (ST_T / 64)];
+    const int b = job_order(MSG_STMAX_REV);
+    const int p = find_preset(st_begin, n_presets, b);
+    stereo_max_tile(rt[p], p, b - st_begin[p], ybuf, rbuf, maxbits, rt[p].fir_on ? stats : nullptr, with_r2 != 0,
+                    w, wm);
+}
+
+// The float64 FIR's presets again (kernels_fir64.h): their peak from the new y.
+__global__ void __launch_bounds__(ST_T)
+k_stereo_remax(const PresetRt* __restrict__ rt, const int32_t* __restrict__ st_count,
+               const int32_t* __restrict__ slot_preset, const int32_t* __restrict__ n_slots, int tmax,
+               const float* __restrict__ ybuf, const float* __restrict__ rbuf, unsigned* __restrict__ maxbits) {
+    __shared__ __attribute__((aligned(16))) float w[ST_WIN];
+    __shared__ float wm[3 * (ST_T / 64)];
+    const int ns = *n_slots;
+    for (int j = blockIdx.x; j < ns * tmax; j += gridDim.x) {
+        const int sl = j / tmax, t = j - sl * tmax;
+        const int p = slot_preset[sl];
+        if (t >= st_count[p]) continue;                          // uniform
+        __syncthreads();
+        stereo_max_tile(rt[p], p, t, ybuf, rbuf, maxbits, nullptr, true, w, wm);
     }
 }
 

@@ -1,6 +1,7 @@
 // kernels_fir.h — space FIR kernels (TU: k_fir.hip).
 #pragma once
 #include "rt.h"
+#include "hbuild.h"
 
 // ---------------------------------------------------------------------------
 // Space FIR (MS:409-445): h = (delta + ER taps) * IR, folded into one kernel
@@ -37,7 +38,6 @@ k_ir_spec(const int64_t* __restrict__ jobs /* [ir_off, ir_len, plan, out_off] */
 // through LDS H_T at a time.  Any length: the ER span is not limited by a
 // transform size (192 kHz x 150 ms + 8192 IR taps = 36 992 taps).  Output:
 // h_len floats at hs_off, cut into partitions by k_fir_h / k_fir4_hpart / k_fir8_hpart.
-constexpr int H_T = 256, H_PER = 4, H_TILE = H_T * H_PER, H_IRMAX = 8192;
 __global__ void __launch_bounds__(H_T)
 k_h_build(const PresetRt* __restrict__ rt, const int32_t* __restrict__ tile_begin, int n_presets,
           const int32_t* __restrict__ er_off, const double* __restrict__ er_gain,
@@ -48,49 +48,7 @@ k_h_build(const PresetRt* __restrict__ rt, const int32_t* __restrict__ tile_begi
     const int b = blockIdx.x;
     const int p = find_preset(tile_begin, n_presets, b);
     const PresetRt& r = rt[p];
-    const int hl = r.h_len;
-    const int irl = r.ir_len > 0 ? r.ir_len : 1;
-    const int t0 = (b - tile_begin[p]) * H_TILE;
-    const int tid = threadIdx.x;
-    const double* src = ir_bank + r.ir_off;
-    for (int i = tid; i < irl + 2 * H_TILE; i += H_T) {
-        const int d = i - H_TILE;
-        irp[i] = (d >= 0 && d < irl) ? (r.ir_len > 0 ? (float)src[d] : 1.0f) : 0.0f;
-    }
-    // taps whose shifted IR reaches [t0, t0 + H_TILE): o in (t0 - irl, t0 + H_TILE)
-    const int32_t* off = er_off + r.er_base;
-    const double* gain = er_gain + r.er_base;
-    int lo = 0, hi = r.n_taps;          // first o > t0 - irl
-    while (lo < hi) { const int m = (lo + hi) >> 1; if (off[m] > t0 - irl) hi = m; else lo = m + 1; }
-    const int klo = lo;
-    hi = r.n_taps;                      // first o >= t0 + H_TILE
-    while (lo < hi) { const int m = (lo + hi) >> 1; if (off[m] >= t0 + H_TILE) hi = m; else lo = m + 1; }
-    const int khi = lo;
-    __syncthreads();
-    double acc[H_PER];
-#pragma unroll
-    for (int i = 0; i < H_PER; ++i) {                          // delta * IR
-        const int t = t0 + tid + i * H_T;
-        acc[i] = t < irl ? (double)irp[H_TILE + t] : 0.0;
-    }
-    for (int k0 = klo; k0 < khi; k0 += H_T) {
-        const int kn = khi - k0 < H_T ? khi - k0 : H_T;
-        __syncthreads();                                        // previous chunk's reads done
-        if (tid < kn) { s_off[tid] = off[k0 + tid]; s_g[tid] = gain[k0 + tid]; }
-        __syncthreads();
-        for (int k = 0; k < kn; ++k) {
-            const float* base = irp + (H_TILE + t0 - s_off[k]) + tid;   // in [0, irl + H_TILE]
-            const double g = s_g[k];
-#pragma unroll
-            for (int i = 0; i < H_PER; ++i) acc[i] = fma(g, (double)base[i * H_T], acc[i]);
-        }
-    }
-    float* h = hs + r.hs_off;
-#pragma unroll
-    for (int i = 0; i < H_PER; ++i) {
-        const int t = t0 + tid + i * H_T;
-        if (t < hl) h[t] = (float)acc[i];
-    }
+    h_build_tile(r, r.h_len, (b - tile_begin[p]) * H_TILE, er_off, er_gain, ir_bank, irp, s_off, s_g, hs + r.hs_off);
 }
 
 // One workgroup per (preset, partition q) of the presets whose spectra are not

@@ -39,6 +39,18 @@ hipError_t launch_spec3(unsigned grid, hipStream_t s, const msg_event* events, c
                         float* grain_pool);
 
 void fir_init_attrs();
+// the float64 space FIR of heavily saturated renders (kernels_fir64.h): flag, h, H_q, blocks
+struct Fir64Launch {
+    const PresetRt* rt; int n_presets; const double* stats; unsigned* maxbits;
+    int32_t* slot_of; int32_t* slot_preset; int32_t* n_slots; int cap; int force;
+    const Fir64Rt* fr; int tmax, qmax, bmax;
+    const int32_t* er_off; const double* er_gain; const double* irbank;
+    float* h64; int64_t h_stride; double2* hs64; int64_t hs_stride;
+    const Real64Plan* plans; int plan; int lds_bytes;
+    const float* x; float* y;
+};
+void fir64_init_attrs();
+hipError_t launch_fir64(const Fir64Launch& a, hipStream_t s);
 hipError_t launch_ir_spec(unsigned grid, int lds_bytes, hipStream_t s, const int64_t* jobs, int n_jobs,
                           const RealPlan* fir_plans, const double* ir_bank, float2* ir_spec);
 // h = (delta + ER) * IR in the time domain, one workgroup per H_TILE taps of a preset

@@ -200,6 +200,7 @@ struct msg_ctx {
     float2* d_fir4tab = nullptr; // k_fir4 twiddle tables (M = 16384)
     bool fir4 = true;            // M = 16384 blocks on k_fir4 (MSGPU_FIR4=0: k_fir2, A/B and tests)
     bool fir8 = true;            // N = 65536 one-partition filters on k_fir8 (MSGPU_FIR8=0: off, A/B and tests)
+    int fir64 = 1;               // float64 FIR of saturated renders: 0 off, 1 predicted, 2 every FIR preset (MSGPU_FIR64)
     // Q <= 2 presets on the streaming k_fir4s (MSGPU_FIR4S=1; off by default: at
     // C3's 24 blocks per preset its H re-reads miss L2 and cancel the saved transforms)
     bool fir4s = false;
@@ -241,6 +242,13 @@ struct msg_ctx {
     Slice<int32_t> spec_ct_list;
     Slice<double> irbank;
     DevBuf<unsigned> maxbits;
+    // float64 space FIR of saturated renders (kernels_fir64.h)
+    Slice<Fir64Rt> f64rt;
+    Slice<int32_t> st_count, odd_list, odd_cnt;
+    DevBuf<double> f64_stats;                   // per preset: sum y^2, sum (1 + (d y)^2)^-2
+    DevBuf<int32_t> f64_slot_of, f64_slot_preset, f64_nslots;
+    DevBuf<float> f64_h;
+    DevBuf<double2> f64_hs;
     // float64 grain chain (kernels_grain64.h)
     Plan64Store plans64;
     Slice<Ev64> ev64;
@@ -672,6 +680,7 @@ msg_ctx* msg_create(int device_ordinal) {
     }
     if (const char* e = getenv("MSGPU_FIR4")) ctx->fir4 = e[0] != '0';
     if (const char* e = getenv("MSGPU_FIR8")) ctx->fir8 = e[0] != '0';
+    if (const char* e = getenv("MSGPU_FIR64")) ctx->fir64 = atoi(e);
     if (const char* e = getenv("MSGPU_FIR4S")) ctx->fir4s = e[0] == '1';
     if (const char* e = getenv("MSGPU_FIR4S_WGS")) ctx->fir4s_wgs = std::max(1, atoi(e));
     if (const char* e = getenv("MSGPU_FIR4S_K")) ctx->fir4s_kmax = std::max(2, std::min(64, atoi(e)));
@@ -702,6 +711,7 @@ msg_ctx* msg_create(int device_ordinal) {
     fft_bench_init_attrs();
     grain64_init_attrs();
     stereo_odd_init_attrs();
+    fir64_init_attrs();
     return ctx.release();
 }
 
@@ -739,6 +749,8 @@ void msg_destroy(msg_ctx* ctx) {
     ctx->micro.release(); ctx->grain.release();
     ctx->mono_a.release(); ctx->mono_y.release(); ctx->hspec.release();
     ctx->hscratch.release(); ctx->maxbits.release();
+    ctx->f64_stats.release(); ctx->f64_slot_of.release(); ctx->f64_slot_preset.release(); ctx->f64_nslots.release();
+    ctx->f64_h.release(); ctx->f64_hs.release();
     for (void* p : ctx->plans64.allocs) hipFree(p);
     ctx->plans64.dev.release();
     ctx->micro64.release(); ctx->grain64.release(); ctx->state64.release(); ctx->save64.release();
@@ -1255,6 +1267,10 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
         if (info[p].n_slots > info[p].n_events)
             memset(ert + slot_base[p] + info[p].n_events, 0,
                    sizeof(EventRt) * (size_t)(info[p].n_slots - info[p].n_events));
+    std::vector<Fir64Rt> f64rt(P);
+    std::vector<int32_t> st_count(P);
+    int f64_cand = 0, f64_qmax = 0, f64_bmax = 0, f64_stmax = 0;
+    int64_t f64_hmax = 0;
     std::vector<int32_t> gen_list, spec_small, spec_big, tile_begin(P), fir_begin(P), h_begin(P), st_begin(P),
         fir_plan_of(P, 0);
     std::vector<double> irbank;
@@ -1497,7 +1513,22 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
         r.drive = (float)pr.sat_drive;
         r.peak = (float)pr.peak;
         st_begin[p] = stiles;
-        stiles += (int32_t)((inf.out_n + ST_TILE - 1) / ST_TILE);
+        st_count[p] = (int32_t)((inf.out_n + ST_TILE - 1) / ST_TILE);
+        stiles += st_count[p];
+        {   // the float64 FIR's shape (kernels_fir64.h), for every FIR preset
+            Fir64Rt& f = f64rt[p];
+            f.h_len = r.fir_on ? (int32_t)pick[p].M : 0;
+            f.q = (f.h_len + FIR64_P - 1) / FIR64_P;
+            f.blocks = (int32_t)((inf.out_n + FIR64_B - 1) / FIR64_B);
+            f.st_tiles = st_count[p];
+            if (r.fir_on) {
+                f64_cand++;
+                f64_hmax = std::max<int64_t>(f64_hmax, f.h_len);
+                f64_qmax = std::max(f64_qmax, f.q);
+                f64_bmax = std::max(f64_bmax, f.blocks);
+                f64_stmax = std::max(f64_stmax, f.st_tiles);
+            }
+        }
         tiles += (int32_t)((inf.out_n + OLA_TILE - 1) / OLA_TILE);
         pool += (inf.pool_len + 3) & ~int64_t(3);   // 16-byte aligned grain regions (float4 loads)
         ysum += (inf.out_n + 3) & ~int64_t(3);   // keep every mono region 16-byte aligned
@@ -1662,6 +1693,12 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
         }
     }
     const auto hC = hclock::now();
+    int f64_plan = -1;                                   // the float64 FIR's transform (kernels_fir64.h)
+    if (ctx->fir64 > 0 && f64_cand > 0) {
+        std::string why;
+        f64_plan = real64_plan(ctx->plans64, FIR64_N, why);
+        if (f64_plan < 0) return fail(ctx, MSG_E_DEVICE, "float64 FIR plan: " + why);
+    }
     HIPCHK(ctx, sync_plans(ctx->grain_plans, s));
     HIPCHK(ctx, sync_plans(ctx->fir_plans, s));
     HIPCHK(ctx, sync_plans(ctx->plans64, s));
@@ -1750,6 +1787,25 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
     HIPCHK(ctx, h2d(&ctx->ir8_jobs.p, ir8_jobs.data(), sizeof(int64_t) * ir8_jobs.size()));
     HIPCHK(ctx, h2d(&ctx->hpart_jobs.p, hpart_jobs.data(), sizeof(int2) * hpart_jobs.size()));
     HIPCHK(ctx, hipMemsetAsync(ctx->maxbits.p, 0, sizeof(unsigned) * P, s));
+    // the float64 FIR chain: slots for up to FIR64_CAP flagged presets of the batch
+    const bool f64_on = ctx->fir64 > 0 && f64_cand > 0;
+    const int f64_cap = std::min(f64_cand, FIR64_CAP);
+    const int64_t f64_hstride = (f64_hmax + 3) & ~int64_t(3);
+    const int64_t f64_hsstride = (int64_t)f64_qmax * FIR64_K;
+    if (f64_on) {
+        HIPCHK(ctx, ctx->f64_stats.ensure(2 * (size_t)P));
+        HIPCHK(ctx, ctx->f64_slot_of.ensure(P));
+        HIPCHK(ctx, ctx->f64_slot_preset.ensure(f64_cap));
+        HIPCHK(ctx, ctx->f64_nslots.ensure(1));
+        HIPCHK(ctx, ctx->f64_h.ensure((size_t)(f64_cap * f64_hstride)));
+        HIPCHK(ctx, ctx->f64_hs.ensure((size_t)(f64_cap * f64_hsstride)));
+        HIPCHK(ctx, hipMemsetAsync(ctx->f64_stats.p, 0, sizeof(double) * 2 * P, s));
+        HIPCHK(ctx, h2d(&ctx->f64rt.p, f64rt.data(), sizeof(Fir64Rt) * P));
+    }
+    const int32_t n_odd = (int32_t)odd_presets.size();
+    HIPCHK(ctx, h2d(&ctx->st_count.p, st_count.data(), sizeof(int32_t) * P));
+    HIPCHK(ctx, h2d(&ctx->odd_list.p, odd_presets.data(), sizeof(int32_t) * odd_presets.size()));
+    HIPCHK(ctx, h2d(&ctx->odd_cnt.p, &n_odd, sizeof(int32_t)));
     HIPCHK(ctx, h2d(&ctx->ev64.p, ev64.data(), sizeof(Ev64) * ev64.size()));
     HIPCHK(ctx, h2d(&ctx->g64_list.p, g64_list.data(), sizeof(int32_t) * g64_list.size()));
     HIPCHK(ctx, h2d(&ctx->gen64_list.p, gen64_list.data(), sizeof(int32_t) * gen64_list.size()));
@@ -1870,6 +1926,24 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
     }
     // ---- stereo, tanh, normalise ----
     stage_mark(ctx, 6, s);
+    // peak of L (and the float64 FIR's error predictor) over the float32 y
+    hipLaunchKernelGGL(k_stereo_max, dim3((unsigned)stiles), dim3(ST_T), 0, s, ctx->prt.p, ctx->st_begin.p, P,
+                       yb, ctx->so_r2.p, ctx->maxbits.p, f64_on ? ctx->f64_stats.p : (double*)nullptr, 0);
+    HIPCHK(ctx, hipGetLastError());
+    if (f64_on) {   // flagged presets: the FIR again in float64, y overwritten (kernels_fir64.h)
+        Fir64Launch a;
+        a.rt = ctx->prt.p; a.n_presets = P; a.stats = ctx->f64_stats.p; a.maxbits = ctx->maxbits.p;
+        a.slot_of = ctx->f64_slot_of.p; a.slot_preset = ctx->f64_slot_preset.p; a.n_slots = ctx->f64_nslots.p;
+        a.cap = f64_cap; a.force = ctx->fir64 >= 2 ? 1 : 0;
+        a.fr = ctx->f64rt.p; a.tmax = (int)((f64_hmax + H_BUILD_TILE - 1) / H_BUILD_TILE); a.qmax = f64_qmax;
+        a.bmax = f64_bmax;
+        a.er_off = ctx->er_off.p; a.er_gain = ctx->er_gain.p; a.irbank = ctx->irbank.p;
+        a.h64 = ctx->f64_h.p; a.h_stride = f64_hstride; a.hs64 = ctx->f64_hs.p; a.hs_stride = f64_hsstride;
+        a.plans = ctx->plans64.dev.p; a.plan = f64_plan;
+        a.lds_bytes = FIR64_K * (int)sizeof(double2);   // the packed transform and its Nyquist slot
+        a.x = ctx->mono_a.p; a.y = yb;
+        HIPCHK(ctx, launch_fir64(a, s));
+    }
     ++ctx->batch_serial;
     for (int p : odd_presets) {           // odd out_n: R = irfft(rfft(roll(y, -dr)) . rot) (MS:432-435)
         const int64_t n = info[p].out_n;
@@ -1902,8 +1976,17 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
         HIPCHK(ctx, launch_stereo_odd(n, ctx->so_row, ctx->so_col, prt[p].dr, w, yb + prt[p].y_off, it->second.p, ctx->so_A.p,
                                       ctx->so_r2.p + prt[p].r2_off, s));
     }
-    hipLaunchKernelGGL(k_stereo_max, dim3((unsigned)stiles), dim3(ST_T), 0, s, ctx->prt.p, ctx->st_begin.p, P,
-                       yb, ctx->so_r2.p, ctx->maxbits.p);
+    if (f64_on)   // the float64 presets' peak from their new y (and R)
+        hipLaunchKernelGGL(k_stereo_remax, dim3((unsigned)std::min(f64_cap * f64_stmax, 256)), dim3(ST_T), 0, s,
+                           ctx->prt.p, ctx->st_count.p, ctx->f64_slot_preset.p, ctx->f64_nslots.p, f64_stmax, yb,
+                           ctx->so_r2.p, ctx->maxbits.p);
+    if (n_odd > 0) {   // odd lengths: the peak of the rotated R
+        int tmax = 0;
+        for (int p : odd_presets) tmax = std::max(tmax, st_count[p]);
+        hipLaunchKernelGGL(k_stereo_remax, dim3((unsigned)std::min<int64_t>((int64_t)n_odd * tmax, 4096)), dim3(ST_T),
+                           0, s, ctx->prt.p, ctx->st_count.p, ctx->odd_list.p, ctx->odd_cnt.p, tmax, yb,
+                           ctx->so_r2.p, ctx->maxbits.p);
+    }
     HIPCHK(ctx, hipGetLastError());
     hipLaunchKernelGGL(k_stereo_out, dim3((unsigned)stiles), dim3(ST_T), 0, s, ctx->prt.p, ctx->st_begin.p, P,
                        yb, ctx->so_r2.p, ctx->maxbits.p, out_dev);

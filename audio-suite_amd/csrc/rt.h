@@ -113,6 +113,17 @@ struct Chain64 {
     int64_t mem_off;              // imprint memory (doubles, max_n/2 + 1)
 };
 
+// The float64 space FIR of heavily saturated renders (kernels_fir64.h): one
+// record per FIR preset, the shape of its float64 overlap-save.
+constexpr int FIR64_N = 16384, FIR64_P = FIR64_N / 2, FIR64_B = FIR64_N - FIR64_P + 1, FIR64_K = FIR64_N / 2 + 1;
+constexpr int FIR64_CAP = 128;     // presets per batch that can take it (slots, in batch order)
+struct Fir64Rt {
+    int32_t h_len;                 // taps of h (<= out_n)
+    int32_t q;                     // partitions of FIR64_P taps
+    int32_t blocks;                // output blocks of FIR64_B frames
+    int32_t st_tiles;              // stereo tiles (k_stereo_remax)
+};
+
 constexpr int GEN_T = 64;          // one wave per event
 constexpr int OLA_T = 256;
 constexpr int OLA_TILE = 4096;

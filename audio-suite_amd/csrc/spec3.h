@@ -29,8 +29,11 @@
 // checked exhaustively by tools/lds_banks.py).
 //
 // Eligibility (host, spec3_eligible): grain length 37500, chain = band limit
-// [+ stretch] with no tilt or power warp, and the stretched band no wider than
-// M/2 (so Y[M - k] = 0 wherever Y[k] is used).  Other events keep k_spectral_ct.
+// [+ stretch] with no tilt or power warp.  A stretched band no wider than M/2
+// (C3) has Y[M - k] = 0 wherever Y[k] is used: the packed inverse inputs are
+// built once per kept bin.  A wider one (C4's x4 stretch, ky ~ 0.96 M) builds
+// each inverse input from Y[i] and Y[M - i] inside inverse pass 1, gathering
+// from X in LDS.  Other events keep k_spectral_ct.
 #pragma once
 #include <cmath>
 #include <vector>
@@ -231,12 +234,53 @@ MSG_DEV void s3_rest(float2* buf, const float2* tab, const EventRt* __restrict__
     }
     __syncthreads();
     SPEC_STAMP(3);
+    const bool stretch = (ex.ops & SPEC_STRETCH) != 0;
+    const double inv_f = ex.s3_inv_f;
+    if (ky > M / 2) {
+        // ---- wide band (C4's x4 stretch: Y reaches past M/2, so both Y[i] and
+        // Y[M - i] feed inverse input i): the stretch gather and the irfft packing
+        // run inside inverse pass 1, reading X (bins < kz) straight from LDS
+        j = otid();
+        {
+            // Y[k] = interp(k / f, X) (MS:117-128), zero from ky up
+            auto Y = [&](int k) -> float2 {
+                if (k >= ky) return make_float2(0.f, 0.f);
+                if (!stretch) return k < kz ? buf[k] : make_float2(0.f, 0.f);
+                const double xs = (double)k * inv_f;
+                if (!(xs <= (double)(K - 1) && xs < (double)kz)) return make_float2(0.f, 0.f);
+                const int j0 = (int)xs;
+                const float fr = (float)(xs - (double)j0);
+                const float2 a = buf[j0];
+                const float2 b = j0 + 1 < kz ? buf[j0 + 1] : make_float2(0.f, 0.f);
+                return make_float2((b.x - a.x) * fr + a.x, (b.y - a.y) * fr + a.y);
+            };
+            float2 v[P::R1];
+            if (j < P::NB1)
+                s3_pass1<P>(v, j, [&](int i) {
+                    // conj Z'[i] = PL(Y[i], w_i) + PH(Y[M - i], w_{M-i}), the narrow band's
+                    // two per-bin terms (w_x = exp(-i pi x / M); w_{M-x} = -conj w_x)
+                    if (i == 0) {                               // DC and Nyquist: real parts (irfft)
+                        const float y0 = Y(0).x, yM = Y(M).x;
+                        return make_float2(0.5f * (y0 + yM), -0.5f * (y0 - yM));
+                    }
+                    const bool lo = i <= M / 2;
+                    const float2 wk = s3_w2M<P>(tab, lo ? i : M - i);
+                    const float2 wi = lo ? wk : make_float2(-wk.x, wk.y);      // w_i
+                    const float2 a = Y(i), b = Y(M - i);
+                    const float2 e1 = cscale(a, 0.5f), o1 = cscale(cmulc(a, wi), 0.5f);
+                    // mirror term with w_{M-i} = -conj(w_i): o1' = -(b . w_i) / 2
+                    const float2 e2 = cscale(b, 0.5f), o2 = cscale(cmul(b, wi), -0.5f);
+                    return make_float2((e1.x - o1.y) + (e2.x + o2.y), -(e1.y + o1.x) + (e2.y - o2.x));
+                });
+            __syncthreads();                            // X fully read
+            if (j < P::NB1) s3_store_a<P>(buf, v, j);
+        }
+        __syncthreads();
+    } else {
     // ---- stretch gather Y = S(X) (MS:117-128) and the irfft packing of bins k
     // and M - k (Y[M - k] = 0 in the band), conjugated for the forward engine
     // (inverse = conj . F . conj): inverse pass 1's nonzero inputs
     {
-        const bool stretch = (ex.ops & SPEC_STRETCH) != 0;
-        const double inv_f = ex.s3_inv_f;
         for (int k = otid(); k < ky; k += T) {
             float2 y;
             if (!stretch) {
@@ -278,6 +322,7 @@ MSG_DEV void s3_rest(float2* buf, const float2* tab, const EventRt* __restrict__
         if (j < P::NB1) s3_store_a<P>(buf, v, j);
     }
     __syncthreads();
+    }
     SPEC_STAMP(4);
     s3_pass2<P>(buf, tab);
     SPEC_STAMP(5);

@@ -698,6 +698,7 @@ def main():
                 "stage_ms": head["stage_ms"], "stage_algorithmic_GBs": head["stage_algorithmic_GBs"],
                 "design_msamples_per_s": head["design_msamples_per_s"],
                 "checked": head["check"],
+                "from_dicts": head.get("from_dicts"),
                 "cpu_baseline": cpu,
                 "dropin_latency": lat,
                 "points": points,

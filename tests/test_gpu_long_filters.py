@@ -21,6 +21,7 @@ from conftest import extra_params
 pytestmark = pytest.mark.gpu
 
 RMS_TOL = 1e-5
+FIR_TOL = 5e-6    # long and ER + IR space filters: half the budget (kernels_fir64.h)
 
 
 def rms(a, b):
@@ -47,7 +48,7 @@ def test_long_space_filters(msgpu, irs, extra_renders, golden_extra):
     for name, p, a in zip(LONG, params, outs):
         err = rms(a, extra_renders[f"{name}_audio"])
         print(f"{name}: rms err {err:.3e}")
-        assert err <= RMS_TOL, name
+        assert err <= FIR_TOL, name
     single, _ = msgpu.render(params[0])
     assert np.array_equal(single, outs[0])          # batching does not change results
 
@@ -78,7 +79,7 @@ def test_long_space_filter_partitions(msgpu, irs):
             os.environ.pop("MSGPU_FIR4", None)
         err = rms(outs[flag][: ref.shape[0]], ref)
         print(f"MSGPU_FIR4={flag}: rms err vs oracle {err:.3e}")
-        assert err <= RMS_TOL
+        assert err <= FIR_TOL
 
 
 @pytest.mark.parametrize("name", ["ODD44", "ODD192L"])
@@ -196,5 +197,53 @@ def test_fir8_kernel_agrees(msgpu, irs, full_renders):
         for flag in outs:
             e = rms(outs[flag][off:off + n], ref)
             print(f"case {i} [MSGPU_FIR8={flag}]: rms err vs oracle {e:.3e}")
-            assert e <= RMS_TOL, (i, flag)
+            assert e <= (RMS_TOL if i in (0, 3) else FIR_TOL), (i, flag)
     assert rms(outs["0"], outs["1"]) <= RMS_TOL
+
+
+def _render_env(params, env):
+    import os
+    import torch
+    from msgpu.engine import Engine
+    from msgpu.pack import PackedBatch
+    packed = PackedBatch(params)
+    os.environ.update(env)
+    try:
+        eng = Engine(0)
+    finally:
+        for k in env:
+            os.environ.pop(k, None)
+    o = eng.render_packed(packed)
+    torch.cuda.synchronize(0)
+    return packed, o.cpu().numpy()
+
+
+def test_fir64_route(msgpu, irs, extra_renders, golden_extra):
+    """The float64 FIR (kernels_fir64.h): MSGPU_FIR64=2 puts every FIR preset on
+    it, =0 none.  Forced, C3 and the saturated ER + IR filters all match the
+    reference / oracle; the predictor (default) leaves C3 on the float32 kernels
+    (bit-identical to MSGPU_FIR64=0) and moves the saturated ones (errors printed
+    for all three routes)."""
+    from oracle import msound_oracle as O
+    base = dict(gen_mode="Resonant strike", event_process="Poisson", _ir_audio=irs["tiny_room_ir"])
+    params = [msgpu.config_params("C3", seed=1001, irs=irs, out_dur_s=0.25),
+              extra_params(golden_extra, irs, "ERIR192t2000"),
+              msgpu.merged(base, base_sr=192000, out_dur_s=0.6826, space_ir_on=True, seed=21, er_cloud_on=True,
+                           space_ir_max_samps=8192),
+              msgpu.merged(base, base_sr=48000, out_dur_s=0.7, space_ir_on=True, seed=22, er_cloud_on=True,
+                           space_ir_max_samps=8192, stereo_width=0.3)]
+    refs = [None, extra_renders["ERIR192t2000_audio"], O.render(params[2])[0], O.render(params[3])[0]]
+    outs = {m: _render_env(params, {"MSGPU_FIR64": m}) for m in ("0", "1", "2")}
+    for i in range(len(params)):
+        for m, (packed, o) in outs.items():
+            off, n = int(packed.offsets[i]), int(packed.out_n[i])
+            ref = refs[i] if refs[i] is not None else O.render(params[i])[0]
+            e = rms(o[off:off + n], ref)
+            print(f"case {i} [MSGPU_FIR64={m}]: rms err {e:.3e}")
+            if m != "0":
+                assert e <= FIR_TOL, (i, m)
+    p0, o0 = outs["0"]
+    p1, o1 = outs["1"]
+    n0 = int(p0.out_n[0])
+    assert np.array_equal(o0[:n0], o1[:n0])               # C3 stays on the float32 FIR
+

@@ -10,6 +10,7 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 RMS_TOL = 1e-5
+FIR_TOL = 5e-6   # long / ER + IR space filters: half the budget (kernels_fir64.h)
 
 
 def rms(a, b):
@@ -164,7 +165,9 @@ def test_fir_transform_sizes(msgpu, irs):
         ref, _ = O.render(p)
         errs.append(rms(a, ref))
         print(f"fir case {i}: rms err {errs[-1]:.3e}")
-    assert all(e <= RMS_TOL for e in errs), errs
+    # ER + IR filters (cases 5 and 7) saturate the clip; the float64 FIR keeps them
+    # at half the budget (<= 5e-6), the others at the tolerance
+    assert all(e <= (FIR_TOL if i in (5, 7) else RMS_TOL) for i, e in enumerate(errs)), errs
 
 
 def test_fir_16384_kernels_agree(msgpu, irs, monkeypatch):
@@ -429,21 +432,26 @@ def test_progress_messages_match_reference(msgpu, irs, full_renders):
         assert msgs == case["messages"], (name, msgs[:4], case["messages"][:4])
 
 
-@pytest.mark.parametrize("stretch,roll,cut", [(0.5, None, None), (2.0, 0.0, None), (4.0, None, 36000.0),
-                                              (4.0, 0.0, 37400.0), (1.0, None, None)])
-def test_spec3_band_pruned_vs_general(msgpu, irs, monkeypatch, stretch, roll, cut):
+@pytest.mark.parametrize("cfg,stretch,roll,cut", [("C3", 0.5, None, None), ("C3", 2.0, 0.0, None),
+                                                  ("C3", 4.0, None, 36000.0), ("C3", 4.0, 0.0, 37400.0),
+                                                  ("C3", 1.0, None, None), ("C3", 4.0, None, None),
+                                                  ("C4", 4.0, None, None), ("C4", 4.0, 0.0, None),
+                                                  ("C4", 3.3, None, 14000.0), ("C4", 2.6, 4000.0, 23000.0)])
+def test_spec3_band_pruned_vs_general(msgpu, irs, monkeypatch, cfg, stretch, roll, cut):
     """The band-pruned 37 500-sample spectral kernel (k_spec3, default) against
     the general compile-time-plan kernel (MSGPU_SPEC3=0): stretch below 1, at 1
-    and above, no roll-off, and stretched bands whose top bin ky nears M/2 (a
-    36 kHz or 37.4 kHz cutoff at x100 unfold, stretch x4).  Both match the
-    oracle at 1e-5 RMS and each other, audio and meta grain_last."""
+    and above, no roll-off, stretched bands whose top bin ky stays below M/2
+    (C3 x4 at 18 kHz) and wide ones past it (C4's x4 stretch at x200 unfold:
+    ky ~ 0.96 M, and a 36 kHz or 37.4 kHz cutoff at x100), which build each
+    inverse input from Y[i] and Y[M - i].  Both match the oracle at 1e-5 RMS and
+    each other, audio and meta grain_last."""
     from oracle import msound_oracle as O
     kw = dict(seed=31, out_dur_s=0.1, partial_stretch=stretch)
     if roll is not None:
         kw["bandlimit_roll_hz"] = roll
     if cut is not None:
         kw["bandlimit_out_hz"] = cut
-    p = msgpu.config_params("C3", irs=irs, **kw)
+    p = msgpu.config_params(cfg, irs=irs, **kw)
     got = {}
     for flag in ("0", "1"):
         monkeypatch.setenv("MSGPU_SPEC3", flag)
