@@ -3,6 +3,7 @@
 #include "spec3.h"
 #include "launch.h"
 #include <cstdlib>
+#include <cmath>
 
 void spec3_init_attrs() {
     (void)hipFuncSetAttribute((const void*)k_spec3<Spec3P18750>, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -16,7 +17,7 @@ bool spec3_tables(std::vector<float>& out) {
 
 // The event runs on k_spec3 (see spec3.h "Eligibility"): returns true and its band.
 bool spec3_eligible(int n, int ops, int gen_sr, double cutoff_gen, double roll, double stretch, int64_t float_off,
-                    int32_t* kb, int32_t* kz, int32_t* ky, double* inv_f) {
+                    int32_t* kb, int32_t* kz, int32_t* ky, double* inv_f, int32_t* exact32) {
     using P = Spec3P18750;
     if (n != 2 * P::M || (float_off & 1)) return false;
     if (ops & (SPEC_TILT_NOISE | SPEC_TILT_SKEW | SPEC_WARP)) return false;
@@ -24,10 +25,18 @@ bool spec3_eligible(int n, int ops, int gen_sr, double cutoff_gen, double roll, 
     const Spec3Band b = s3_band(n, gen_sr, cutoff_gen, roll, (ops & SPEC_STRETCH) != 0, stretch);
     if (b.kz > b.ky) return false;
     if (b.ky <= P::M / 2 ? !s3_band_fits<P>(b.kz, b.ky)                       // narrow: X, Z' halves in LDS
-                         : 2 * ((b.kz + 15) & ~15) > P::BUF) return false;     // wide: Z[k], Z[M-k], then X
+                         : (2 * ((b.kz + 15) & ~15) > P::BUF || b.ky > P::BUF ||  // wide: Z[k], Z[M-k]; Y over X,
+                            ((ops & SPEC_STRETCH) && stretch <= 1.0))) return false;   // which needs f > 1
     static const bool wide_on = !(getenv("MSGPU_S3_WIDE") && getenv("MSGPU_S3_WIDE")[0] == '0');   // A/B switch
     if (b.ky > P::M / 2 && !wide_on) return false;
     *kb = b.kb; *kz = b.kz; *ky = b.ky; *inv_f = b.inv_f;
+    // k / f exact in float32 for every bin k < 2^15 (the wide path's gather):
+    // 1 / f = q 2^-12 with q's odd part below 2^24 / 2^15
+    double sc = b.inv_f * 4096.0;
+    bool ok = sc == std::floor(sc) && sc > 0.0 && sc < 4096.0 * 4096.0;
+    if (ok)
+        while (std::fmod(sc, 2.0) == 0.0) sc *= 0.5;
+    *exact32 = (ok && sc < 512.0) ? 1 : 0;
     return true;
 }
 

@@ -180,10 +180,38 @@ struct GenBasicConst {
     float inv_sigma;     // gaussian click
 };
 MSG_DEV float ring_phase(float jf, float fa, float fb) {
+#pragma clang fp contract(off)
     const float p = jf * fa;
     const float e = fmaf(jf, fa, -p);                 // exact: j * fa = p + e
     float ph = (p - floorf(p)) + (e + jf * fb);
     return ph - floorf(ph);
+}
+// (sin, cos)(2 pi frac(j f / sr)) to float32 accuracy for the chunk bases and
+// the rotation table of the resonant strike: the phase as a float pair (hi +
+// lo, lo the rounding of hi) and sinpi / cospi of hi corrected to first order
+// in lo.  The hardware sine of the rounded phase left a ~5e-7 relative error
+// coherent at the ring frequency, which the band limit passes and a saturating
+// space filter + tanh clip (MS:31-34) amplified to ~6e-6 RMS at 48 kHz
+// (tools/diag_fir64.py).  Contraction is off: fused into p - floor(p), the
+// product j fa would enter f0 unrounded and its tail e a second time (a phase
+// error of up to ulp(j f / sr) / 2: 7e-4 rad at j = 40000, f / sr = 0.0875,
+// tools/probe/ring_probe.hip).
+MSG_DEV float2 ring_sincos(float jf, float fa, float fb) {
+#pragma clang fp contract(off)
+    const float p = jf * fa;
+    const float e = fmaf(jf, fa, -p);
+    const float f0 = p - floorf(p), f1 = e + jf * fb;
+    float hi = f0 + f1;
+    float lo = (f0 - hi) + f1;                        // |f0| >= |f1|: exact two-sum tail
+    const float fl = -floorf(hi);
+    const float h2 = hi + fl;                         // two-sum: the wrap's rounding joins lo
+    const float bv = h2 - hi;
+    lo += (hi - (h2 - bv)) + (fl - bv);
+    hi = h2;
+    const float a = 2.0f * hi;
+    const float sn = sinpif(a), cs = cospif(a);
+    const float d = 6.2831853071795865f * lo;         // 2 pi lo, |d| ~ 1e-7
+    return make_float2(fmaf(d, cs, sn), fmaf(-d, sn, cs));
 }
 MSG_DEV float gen_basic_sample(const GenBasicConst& c, int j, float nrm) {
     float x;
@@ -293,9 +321,8 @@ k_gen_normal(const msg_preset* __restrict__ presets, const msg_event* __restrict
     if (!RAW64 && c.mode == MSG_GEN_RESONANT) {
         for (int i = (int)threadIdx.x; i < 128; i += GEN_T * GEN_K) {
             const float rf = (float)(i - 64);
-            const float ph = ring_phase(rf, c.fa, c.fb);
-            s_rot[i] = make_float4(__builtin_amdgcn_cosf(ph), __builtin_amdgcn_sinf(ph),
-                                   0.9f * __builtin_amdgcn_exp2f(rf * c.k_ring),
+            const float2 sc = ring_sincos(rf, c.fa, c.fb);
+            s_rot[i] = make_float4(sc.y, sc.x, 0.9f * __builtin_amdgcn_exp2f(rf * c.k_ring),
                                    0.25f * __builtin_amdgcn_exp2f(rf * c.k_exc));
         }
     }
@@ -442,9 +469,8 @@ k_gen_normal(const msg_preset* __restrict__ presets, const msg_event* __restrict
         if (reson) {
             if (lane < G) {
                 const float jb = (float)(p0 + 64 * lane);
-                const float ph = ring_phase(jb, c.fa, c.fb);
-                s_grp[wv][lane] = make_float4(__builtin_amdgcn_sinf(ph), __builtin_amdgcn_cosf(ph),
-                                              __builtin_amdgcn_exp2f(fmaxf(jb * c.k_ring, -126.f)),
+                const float2 sc = ring_sincos(jb, c.fa, c.fb);
+                s_grp[wv][lane] = make_float4(sc.x, sc.y, __builtin_amdgcn_exp2f(fmaxf(jb * c.k_ring, -126.f)),
                                               __builtin_amdgcn_exp2f(fmaxf(jb * c.k_exc, -126.f)));
             }
             __syncthreads();                      // orders the LDS writes before the reads
@@ -479,9 +505,8 @@ k_gen_normal(const msg_preset* __restrict__ presets, const msg_event* __restrict
                         off = d + 64;
                     } else {                          // a slow normal spanned > 64 draws: exact base
                         const float j0 = (float)pc;
-                        const float ph0 = ring_phase(j0, c.fa, c.fb);
-                        u = make_float4(__builtin_amdgcn_sinf(ph0), __builtin_amdgcn_cosf(ph0),
-                                        __builtin_amdgcn_exp2f(fmaxf(j0 * c.k_ring, -126.f)),
+                        const float2 sc = ring_sincos(j0, c.fa, c.fb);
+                        u = make_float4(sc.x, sc.y, __builtin_amdgcn_exp2f(fmaxf(j0 * c.k_ring, -126.f)),
                                         __builtin_amdgcn_exp2f(fmaxf(j0 * c.k_exc, -126.f)));
                         off = 64;
                     }

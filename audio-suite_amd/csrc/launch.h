@@ -33,7 +33,7 @@ hipError_t launch_spectral_ct(int plan, unsigned grid, hipStream_t s, const msg_
 void spec3_init_attrs();
 bool spec3_tables(std::vector<float>& out);
 bool spec3_eligible(int n, int ops, int gen_sr, double cutoff_gen, double roll, double stretch, int64_t float_off,
-                    int32_t* kb, int32_t* kz, int32_t* ky, double* inv_f);
+                    int32_t* kb, int32_t* kz, int32_t* ky, double* inv_f, int32_t* exact32);
 hipError_t launch_spec3(unsigned grid, hipStream_t s, const msg_event* events, const EventRt* ert, const PresetRt* rt,
                         const float2* tables, const int32_t* ev_list, int n_list, const float* micro_pool,
                         float* grain_pool);

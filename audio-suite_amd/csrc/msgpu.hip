@@ -1658,7 +1658,7 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
             const int ctp = (x.ops && use_ct) ? spectral_ct_plan(e.n) : -1;
             if (use_s3 && x.ops &&
                 spec3_eligible(e.n, x.ops, x.gen_sr, x.cutoff_gen, x.roll, x.stretch, r.pool_base + e.pool_off,
-                               &x.s3_kb, &x.s3_kz, &x.s3_ky, &x.s3_inv_f))
+                               &x.s3_kb, &x.s3_kz, &x.s3_ky, &x.s3_inv_f, &x.s3_pad))
                 L.s3.push_back(ei);
             else if (ctp >= 0)
                 L.ct[ctp].push_back(ei);

@@ -76,7 +76,7 @@ struct EventRt {
     double env_tau;        // noise/skewed envelope time constant (s)
     double warp_power;     // fft_warp_power exponent (MS:103-115)
     // band of the band-pruned spectral kernel (spec3.h, host-computed by s3_band)
-    int32_t s3_kb, s3_kz, s3_ky, s3_pad;
+    int32_t s3_kb, s3_kz, s3_ky, s3_pad;   // s3_pad: k / f exact in float32 (wide band's gather)
     double s3_inv_f;
 };
 enum : int32_t {

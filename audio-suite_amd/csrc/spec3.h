@@ -238,41 +238,67 @@ MSG_DEV void s3_rest(float2* buf, const float2* tab, const EventRt* __restrict__
     const double inv_f = ex.s3_inv_f;
     if (ky > M / 2) {
         // ---- wide band (C4's x4 stretch: Y reaches past M/2, so both Y[i] and
-        // Y[M - i] feed inverse input i): the stretch gather and the irfft packing
-        // run inside inverse pass 1, reading X (bins < kz) straight from LDS
-        j = otid();
+        // Y[M - i] feed inverse input i).  Y = S(X) is gathered once per bin into
+        // LDS over X itself: bins [kz, ky) first (they read X below kz and write
+        // above it), then bins [0, kz) chunk by chunk from the top (a wide band
+        // has f > 1, so S reads X only below the bin it writes).
         {
-            // Y[k] = interp(k / f, X) (MS:117-128), zero from ky up
-            auto Y = [&](int k) -> float2 {
-                if (k >= ky) return make_float2(0.f, 0.f);
+            // k / f in float when that is exact for every k (ex.s3_pad: 1 / f a dyadic
+            // fraction, e.g. the x4 stretch), else in float64 as the narrow path does
+            const bool exact32 = ex.s3_pad != 0;
+            const float inv_f32 = (float)inv_f;
+            auto Y = [&](int k) -> float2 {       // interp(k / f, X) (MS:117-128)
                 if (!stretch) return k < kz ? buf[k] : make_float2(0.f, 0.f);
-                const double xs = (double)k * inv_f;
-                if (!(xs <= (double)(K - 1) && xs < (double)kz)) return make_float2(0.f, 0.f);
-                const int j0 = (int)xs;
-                const float fr = (float)(xs - (double)j0);
+                int j0;
+                float fr;
+                if (exact32) {
+                    const float xs = (float)k * inv_f32;
+                    if (!(xs <= (float)(K - 1) && xs < (float)kz)) return make_float2(0.f, 0.f);
+                    j0 = (int)xs;
+                    fr = xs - (float)j0;
+                } else {
+                    const double xs = (double)k * inv_f;
+                    if (!(xs <= (double)(K - 1) && xs < (double)kz)) return make_float2(0.f, 0.f);
+                    j0 = (int)xs;
+                    fr = (float)(xs - (double)j0);
+                }
                 const float2 a = buf[j0];
                 const float2 b = j0 + 1 < kz ? buf[j0 + 1] : make_float2(0.f, 0.f);
                 return make_float2((b.x - a.x) * fr + a.x, (b.y - a.y) * fr + a.y);
             };
+            for (int k = kz + otid(); k < ky; k += T) buf[k] = Y(k);
+            // [0, kz) in T-bin chunks from the top down: chunk [a, a + T) reads X
+            // below (a + T) / f + 1 <= a + T, so one barrier between a chunk's
+            // reads and its writes orders it against every lower chunk's reads
+            // (a register array over all of [0, kz) spilled to scratch)
+            for (int a = ((kz - 1) / T) * T; a >= 0; a -= T) {
+                const int k = a + otid();
+                const float2 v = k < kz ? Y(k) : make_float2(0.f, 0.f);
+                __syncthreads();
+                if (k < kz) buf[k] = v;
+            }
+        }
+        __syncthreads();
+        // ---- inverse pass 1 from Y in LDS: conj Z'[i] = PL(Y[i], w_i) + PH(Y[M - i],
+        // w_{M-i}), the narrow band's two per-bin terms (w_x = exp(-i pi x / M);
+        // w_{M-x} = -conj w_x)
+        j = otid();
+        {
+            const float2 z0 = make_float2(0.f, 0.f);
             float2 v[P::R1];
             if (j < P::NB1)
                 s3_pass1<P>(v, j, [&](int i) {
-                    // conj Z'[i] = PL(Y[i], w_i) + PH(Y[M - i], w_{M-i}), the narrow band's
-                    // two per-bin terms (w_x = exp(-i pi x / M); w_{M-x} = -conj w_x)
-                    if (i == 0) {                               // DC and Nyquist: real parts (irfft)
-                        const float y0 = Y(0).x, yM = Y(M).x;
-                        return make_float2(0.5f * (y0 + yM), -0.5f * (y0 - yM));
-                    }
+                    const float2 a = i < ky ? buf[i] : z0, b = M - i < ky ? buf[M - i] : z0;
+                    if (i == 0) return make_float2(0.5f * (a.x + b.x), -0.5f * (a.x - b.x));   // DC, Nyquist (irfft)
                     const bool lo = i <= M / 2;
                     const float2 wk = s3_w2M<P>(tab, lo ? i : M - i);
                     const float2 wi = lo ? wk : make_float2(-wk.x, wk.y);      // w_i
-                    const float2 a = Y(i), b = Y(M - i);
                     const float2 e1 = cscale(a, 0.5f), o1 = cscale(cmulc(a, wi), 0.5f);
                     // mirror term with w_{M-i} = -conj(w_i): o1' = -(b . w_i) / 2
                     const float2 e2 = cscale(b, 0.5f), o2 = cscale(cmul(b, wi), -0.5f);
                     return make_float2((e1.x - o1.y) + (e2.x + o2.y), -(e1.y + o1.x) + (e2.y - o2.x));
                 });
-            __syncthreads();                            // X fully read
+            __syncthreads();                            // Y fully read
             if (j < P::NB1) s3_store_a<P>(buf, v, j);
         }
         __syncthreads();

@@ -465,3 +465,21 @@ def test_spec3_band_pruned_vs_general(msgpu, irs, monkeypatch, cfg, stretch, rol
         print(f"stretch {stretch} roll {roll} cut {cut} MSGPU_SPEC3={flag}: audio rms {err:.3e}, grain rel {gerr:.3e}")
         assert err <= RMS_TOL and gerr <= 1e-5
     assert rms(got["0"][0], got["1"][0]) <= RMS_TOL
+
+
+@pytest.mark.parametrize("sr,unfold", [(48000, 25.0), (192000, 25.0), (384000, 100.0), (44100, 7.3)])
+def test_resonant_generator_accuracy(msgpu, sr, unfold):
+    """The resonant strike's float32 samples (meta micro_last, MS:253-258)
+    against the oracle: float32 rounding only (the chunk bases and rotation
+    table from an exact-wrap phase pair and sinpi / cospi, FP contraction off
+    in the phase split: contracted, j fa's rounding entered the phase twice,
+    5e-7 relative and growing with j, 7e-8 without; profiles/r04k_gpu_tests.txt)."""
+    from oracle import msound_oracle as O
+    p = msgpu.merged(gen_mode="Resonant strike", event_process="Single", base_sr=sr, time_unfold=unfold,
+                     out_dur_s=0.05, seed=7, er_cloud_on=False, space_ir_on=False, ring_hz=5300.0)
+    _, m = msgpu.render(p)
+    _, rm = O.render(p)
+    g, r = np.asarray(m["micro_last"], np.float64), rm["micro_last"]
+    rel = float(np.sqrt(np.mean((g - r) ** 2) / np.mean(r ** 2)))
+    print(f"{sr} Hz x{unfold}: micro rel err {rel:.2e}")
+    assert rel <= 1.5e-7

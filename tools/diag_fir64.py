@@ -66,5 +66,78 @@ def main():
         print(" | ".join(line), flush=True)
 
 
-if __name__ == "__main__":
+if __name__ == "__main__" and len(sys.argv) == 1:
     main()
+
+
+def meta_errors():
+    """Relative RMS error of the device's micro_last / grain_last (float32 chain)
+    against the oracle's, per case: the generator's and the spectral chain's share."""
+    irs = dict(np.load(os.path.join(REPO, "tests", "golden", "irs.npz")))
+    base = dict(gen_mode="Resonant strike", event_process="Single", _ir_audio=None, space_ir_on=False,
+                er_cloud_on=False)
+    for sr, unf, st in ((48000, 25.0, 1.0), (192000, 25.0, 1.0), (384000, 100.0, 2.0), (48000, 25.0, 2.0)):
+        for mode in ("Resonant strike", "Gaussian click", "Noise burst"):
+            p = msgpu.merged(base, gen_mode=mode, base_sr=sr, time_unfold=unf, partial_stretch=st, out_dur_s=0.05,
+                             seed=7)
+            a, m = msgpu.render(p)
+            ra, rm = O.render(p)
+            rel = lambda x, y: float(np.sqrt(np.mean((x - y) ** 2) / np.mean(y ** 2)))  # noqa: E731
+            print(f"{sr} x{unf} st{st} {mode:16s} n={rm['micro_last'].size}: micro rel {rel(m['micro_last'], rm['micro_last']):.2e}"
+                  f"  grain rel {rel(m['grain_last'], rm['grain_last']):.2e}", flush=True)
+
+
+if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "meta":
+    meta_errors()
+
+
+def variants():
+    """R48 (48 kHz ER + IR, 0.7 s) with one factor changed at a time, float64 FIR forced."""
+    irs = dict(np.load(os.path.join(REPO, "tests", "golden", "irs.npz")))
+    base = dict(gen_mode="Resonant strike", event_process="Poisson", _ir_audio=irs["tiny_room_ir"], base_sr=48000,
+                out_dur_s=0.7, space_ir_on=True, seed=22, er_cloud_on=True, space_ir_max_samps=8192, stereo_width=0.3)
+    vs = {"base": {}, "gauss": dict(gen_mode="Gaussian click"), "noise": dict(gen_mode="Noise burst"),
+          "flat_env": dict(env_a=0.0, env_d=0.0, env_s=1.0, env_r=0.0), "no_band": dict(bandlimit_on=False),
+          "no_stereo": dict(stereo_on=False), "drive0": dict(sat_drive=0.0), "no_er": dict(er_cloud_on=False),
+          "unfold1": dict(time_unfold=1.0)}
+    os.environ["MSGPU_FIR64"] = "2"
+    from msgpu.engine import Engine
+    from msgpu.pack import PackedBatch
+    import torch
+    eng = Engine(0)
+    os.environ.pop("MSGPU_FIR64", None)
+    for name, kw in vs.items():
+        p = msgpu.merged(base, **kw)
+        ref, _ = O.render(p)
+        o = eng.render_packed(PackedBatch([p]))
+        torch.cuda.synchronize(0)
+        print(f"R48 {name:10s}: rms err {rms(o.cpu().numpy(), ref):.3e}", flush=True)
+
+
+if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "variants":
+    variants()
+
+
+def gen_detail():
+    """Where the resonant strike's float32 error sits within one grain."""
+    for sr, unf in ((48000, 25.0), (384000, 100.0)):
+        p = msgpu.merged(gen_mode="Resonant strike", event_process="Single", base_sr=sr, time_unfold=unf,
+                         out_dur_s=0.05, seed=7, er_cloud_on=False, space_ir_on=False)
+        _, m = msgpu.render(p)
+        _, rm = O.render(p)
+        g, r = np.asarray(m["micro_last"], np.float64), rm["micro_last"]
+        n = r.size
+        e = g - r
+        np.savez(os.path.join(REPO, "gpurun_out", f"gen_{sr}.npz"), g=g, r=r)
+        rr = np.sqrt(np.mean(r ** 2))
+        print(f"{sr}: n {n} rel {np.sqrt(np.mean(e ** 2)) / rr:.2e}; max |e| {np.abs(e).max():.2e} at {np.abs(e).argmax()}")
+        for a, b in ((0, 64), (64, 512), (512, n // 4), (n // 4, n // 2), (n // 2, n - 64), (n - 64, n)):
+            print(f"   [{a},{b}) rms e {np.sqrt(np.mean(e[a:b] ** 2)):.2e} rms r {np.sqrt(np.mean(r[a:b] ** 2)):.2e}"
+                  f" corr(e, r) {np.corrcoef(e[a:b], r[a:b])[0, 1]:.2f}")
+        print("   e[:8]", np.array2string(e[:8], precision=2), "r[:8]", np.array2string(r[:8], precision=3))
+        rat = e[64:512] / np.where(np.abs(r[64:512]) > 1e-3, r[64:512], np.nan)
+        print(f"   e/r [64,512): median {np.nanmedian(rat):.2e} std {np.nanstd(rat):.2e}")
+
+
+if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "gen":
+    gen_detail()
