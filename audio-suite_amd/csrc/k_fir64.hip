@@ -8,7 +8,7 @@ void fir64_init_attrs() {
 }
 
 hipError_t launch_fir64(const Fir64Launch& a, hipStream_t s) {
-    hipLaunchKernelGGL(k_fir64_flag, dim3(1), dim3(1024), 0, s, a.rt, a.n_presets, a.stats, a.maxbits, a.slot_of,
+    hipLaunchKernelGGL(k_fir64_flag, dim3(1), dim3(64), 0, s, a.rt, a.n_presets, a.stats, a.maxbits, a.slot_of,
                        a.slot_preset, a.n_slots, a.cap, a.force);
     // small persistent grids: with no flagged preset every workgroup exits at once,
     // and one waiting for a CU held by another stream's kernel delays little

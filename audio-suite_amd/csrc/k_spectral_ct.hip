@@ -9,6 +9,7 @@ template <class P> static void ct_attr() {
 
 void spectral_ct_init_attrs() {
     ct_attr<SpecP18750>(); ct_attr<SpecP15000>(); ct_attr<SpecP1200>(); ct_attr<SpecP960>(); ct_attr<SpecP750>();
+    ct_attr<SpecP240>();
 }
 
 // index of the compile-time plan for grain length n, -1 if none
@@ -19,6 +20,7 @@ int spectral_ct_plan(int n) {
         case 2 * SpecP1200::M: return 2;
         case 2 * SpecP960::M: return 3;
         case 2 * SpecP750::M: return 4;
+        case 2 * SpecP240::M: return 5;
         default: return -1;
     }
 }
@@ -30,6 +32,7 @@ bool spectral_ct_tables(int plan, std::vector<float>& out) {
         case 2: spec_ct_tables<SpecP1200>(out); return true;
         case 3: spec_ct_tables<SpecP960>(out); return true;
         case 4: spec_ct_tables<SpecP750>(out); return true;
+        case 5: spec_ct_tables<SpecP240>(out); return true;
         default: return false;
     }
 }
@@ -52,6 +55,7 @@ hipError_t launch_spectral_ct(int plan, unsigned grid, hipStream_t s, const msg_
         case 2: return ct_go<SpecP1200>(grid, s, events, ert, rt, tables, ev_list, n_list, micro_pool, grain_pool);
         case 3: return ct_go<SpecP960>(grid, s, events, ert, rt, tables, ev_list, n_list, micro_pool, grain_pool);
         case 4: return ct_go<SpecP750>(grid, s, events, ert, rt, tables, ev_list, n_list, micro_pool, grain_pool);
+        case 5: return ct_go<SpecP240>(grid, s, events, ert, rt, tables, ev_list, n_list, micro_pool, grain_pool);
         default: return hipErrorInvalidValue;
     }
 }

@@ -36,17 +36,17 @@
 constexpr int FIR64_T = 512, FIR64_E = 16;          // the float64 LDS engine (G64_T, G64_MAXE)
 constexpr double FIR64_PRED = 5e-7;                  // predicted float32 error above which a preset takes float64
 
-// Flag kernel: one thread per preset; slots in batch order (one workgroup scans).
-__global__ void __launch_bounds__(1024)
+// Flag kernel: one wave walks the presets 64 at a time, slots in batch order
+// (a 64-thread workgroup finds a CU at once beside other streams' kernels,
+// where a 1024-thread one waited ~80 us for a free CU).
+__global__ void __launch_bounds__(64)
 k_fir64_flag(const PresetRt* __restrict__ rt, int n_presets, const double* __restrict__ stats,
              unsigned* __restrict__ maxbits, int32_t* __restrict__ slot_of, int32_t* __restrict__ slot_preset,
              int32_t* __restrict__ n_slots, int cap, int force) {
-    __shared__ int32_t s_cnt[1024 / 64 + 1];
-    __shared__ int32_t s_base;
-    if (threadIdx.x == 0) s_base = 0;
-    __syncthreads();
-    for (int p0 = 0; p0 < n_presets; p0 += blockDim.x) {
-        const int p = p0 + (int)threadIdx.x;
+    const int lane = (int)threadIdx.x;
+    int base = 0;
+    for (int p0 = 0; p0 < n_presets; p0 += 64) {
+        const int p = p0 + lane;
         bool f = false;
         if (p < n_presets) {
             const PresetRt& r = rt[p];
@@ -64,28 +64,16 @@ k_fir64_flag(const PresetRt* __restrict__ rt, int n_presets, const double* __res
                 f = force || pred > FIR64_PRED;
             }
         }
-        // slots in preset order: a block-wide exclusive scan of f
         const uint64_t bal = __ballot(f);
-        const int lane = (int)(threadIdx.x & 63), wv = (int)(threadIdx.x >> 6);
-        if (lane == 0) s_cnt[wv] = __popcll(bal);
-        __syncthreads();
-        int before = s_base;
-        for (int w = 0; w < wv; ++w) before += s_cnt[w];
-        before += __popcll(bal & ((1ULL << lane) - 1));
+        const int before = base + __popcll(bal & ((1ULL << lane) - 1));
         if (f && before < cap) {
             slot_of[p] = before;
             slot_preset[before] = p;
             maxbits[p] = 0u;                               // k_stereo_remax takes the float64 y's peak
         }
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            int tot = 0;
-            for (int w = 0; w < (int)(blockDim.x >> 6); ++w) tot += s_cnt[w];
-            s_base += tot;
-        }
-        __syncthreads();
+        base += __popcll(bal);
     }
-    if (threadIdx.x == 0) *n_slots = s_base < cap ? s_base : cap;
+    if (lane == 0) *n_slots = base < cap ? base : cap;
 }
 
 // h of the slots' presets (k_h_build's tile, float64 sums, float32 taps).

@@ -21,7 +21,7 @@ hipError_t launch_spectral(bool big, unsigned grid, int lds_bytes, hipStream_t s
                            float* micro_pool, float* grain_pool);
 
 // compile-time-plan spectral kernels for hot grain lengths (spec_ct.h)
-constexpr int SPEC_CT_PLANS = 5;
+constexpr int SPEC_CT_PLANS = 6;
 void spectral_ct_init_attrs();
 int spectral_ct_plan(int n);
 bool spectral_ct_tables(int plan, std::vector<float>& out);

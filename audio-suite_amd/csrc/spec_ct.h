@@ -182,9 +182,10 @@ inline void spec_ct_tables(std::vector<float>& out) {
 }
 
 // The hot lengths: C3/C4 (37500), C5 reading B (30000), C2 (2400), C5 reading A
-// (1920) and the factory default (1500).
+// (1920), the factory default (1500) and H48 (480: 384 kHz x 1.25 ms).
 using SpecP18750 = SpecPlan<18750, 768, 25, 5, 5, 5, 6>;
 using SpecP15000 = SpecPlan<15000, 640, 25, 5, 5, 6, 4>;
 using SpecP1200 = SpecPlan<1200, 64, 25, 6, 8>;
 using SpecP960 = SpecPlan<960, 64, 15, 8, 8>;
 using SpecP750 = SpecPlan<750, 64, 25, 5, 6>;
+using SpecP240 = SpecPlan<240, 64, 5, 6, 8>;

@@ -47,7 +47,10 @@ HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: 8.0 TB/s spec
 PROFILES = os.path.join(REPO, "profiles")
 # bench stage -> the kernels it times (rocprofv3 kernel-name prefixes)
 STAGE_KERNEL = {"generate": ("k_gen_normal",), "spectral": ("k_spec3", "k_spectral"), "overlap_add": ("k_ola_env",),
-                "fir_kernel": ("k_fir8<", "k_fir4<", "k_fir2<"), "stereo": ("k_stereo_max", "k_stereo_out"),
+                "fir_kernel": ("k_fir8<", "k_fir4<", "k_fir2<"),
+                # the stereo window also holds the float64 FIR route (flag, h, spectra,
+                # blocks, peak again) and the odd-length rotation
+                "stereo": ("k_stereo_max", "k_stereo_out", "k_stereo_remax", "k_fir64", "k_h64", "k_hspec64", "k_so_"),
                 "fir_h": ("k_fir8_hconv", "k_fir8_spec", "k_h_build", "k_fir4_hpart", "k_fir_h", "k_ir_spec")}
 STAGE_NAMES = ["plan", "host_prep", "generate", "spectral", "overlap_add", "fir", "stereo", "total",
                "fir_kernel", "fir_h", "host_plan_wall", "host_records_wall", "host_upload_wall",

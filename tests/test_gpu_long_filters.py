@@ -149,6 +149,18 @@ def test_h48_metric_point(msgpu, irs, extra_renders, golden_extra):
         assert abs(float(a64[:, 1].sum()) - g["sum_r"]) <= RMS_TOL * n, name
 
 
+@pytest.mark.parametrize("ct", ["0", "1"])
+def test_h48_grain_plans(msgpu, irs, extra_renders, golden_extra, monkeypatch, ct):
+    """H48's 480-sample grains on the compile-time plan (SpecPlan<240>: radices
+    5, 6, 8, one wave per grain) and on the runtime-plan kernel
+    (MSGPU_SPEC_CT=0): both match the reference's seed-1000 buffer."""
+    monkeypatch.setenv("MSGPU_SPEC_CT", ct)
+    a, _ = msgpu.render(extra_params(golden_extra, irs, "H48_1000"))
+    err = rms(a, extra_renders["H48_1000_audio"])
+    print(f"H48 MSGPU_SPEC_CT={ct}: rms err {err:.3e}")
+    assert err <= RMS_TOL
+
+
 def test_fir8_kernel_agrees(msgpu, irs, full_renders):
     """One-partition filters of 12 k .. 45 k taps run on k_fir8 (N = 65 536, two
     half-size transforms on the k_fir4 engine); MSGPU_FIR8=0 puts them back on
