@@ -30,6 +30,25 @@
 #pragma once
 #include "fir4_fft.h"
 
+// Phase timing (debug builds with -DMSG_STAMPS, tools/fir8_stamps.py): block-summed
+// wall-clock deltas per phase of k_fir8, read back with msg_debug_stamps_fir.
+#ifdef MSG_STAMPS
+__device__ unsigned long long g_fir_stamps[16];
+#define FIR_STAMP(i)                                                             \
+    do {                                                                         \
+        __syncthreads();                                                         \
+        if (threadIdx.x == 0) {                                                  \
+            const long long now_ = wall_clock64();                               \
+            atomicAdd(&g_fir_stamps[i], (unsigned long long)(now_ - stamp_));    \
+            stamp_ = now_;                                                       \
+        }                                                                        \
+    } while (0)
+#define FIR_STAMP_INIT long long stamp_ = wall_clock64()
+#else
+#define FIR_STAMP(i) do {} while (0)
+#define FIR_STAMP_INIT do {} while (0)
+#endif
+
 namespace fir8 {
 using G = Fir4Geo<16384>;
 constexpr int MH = 16384, M = 2 * MH, N = 2 * M;
@@ -216,6 +235,7 @@ k_fir8(const PresetRt* __restrict__ rt, const int2* __restrict__ jobs, const flo
     extern __shared__ __attribute__((aligned(16))) float2 lds[];
     float2* tab = lds;
     float2* buf = lds + G::TAB;
+    FIR_STAMP_INIT;
     const int2 job = jobs[xcd_block(blockIdx.x, gridDim.x)];
     const PresetRt& pr = rt[job.x];
     const int P = pr.fir_P;                       // Q == 1
@@ -228,16 +248,23 @@ k_fir8(const PresetRt* __restrict__ rt, const int2* __restrict__ jobs, const flo
     tc.put(tab);
     __syncthreads();                              // tables visible
     dif_split(tab, a, b);
+    FIR_STAMP(0);
     const float2* He = hspec + pr.h_off;
     const float2* Ho = He + (MH + 1);
     float2 v[2][R4], acc[2][R4], A[R1];
     fwd_half<false>(buf, tab, a, v);
+    FIR_STAMP(1);
     even_mac_pre(tab, v, He, acc);
+    FIR_STAMP(2);
     inv_half<false>(buf, tab, acc, A);
+    FIR_STAMP(3);
     fwd_half<true>(buf, tab, b, v);
+    FIR_STAMP(4);
     odd_mac_pre(tab, v, Ho, acc);
+    FIR_STAMP(5);
     float2 (&B)[R1] = a;                          // a is dead: its registers take B
     inv_half<true>(buf, tab, acc, B);
+    FIR_STAMP(6);
     // F[m] = A + W_M^m B, F[m + MH] = A - W_M^m B; z'[m] = conj(F[m]) / M
     const int t = otid();
     const float2 wt = fir4_wM(tab, G::OFF_PLO, G::OFF_PHI, t);
@@ -252,6 +279,7 @@ k_fir8(const PresetRt* __restrict__ rt, const int2* __restrict__ jobs, const flo
         for (int h = 0; h < 2; ++h)                   // segment sample u = 2 (t + r NB1 + h MH)
             so.put((uint32_t)(d0 + 2 * (r * NB1 + h * MH)), make_float2(f[h].x * s, -f[h].y * s));
     }
+    FIR_STAMP(7);
 }
 
 // ---------------------------------------------------------------------------

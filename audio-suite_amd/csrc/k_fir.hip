@@ -200,3 +200,14 @@ hipError_t launch_fft_bench(bool po2, unsigned grid, int lds_bytes, hipStream_t 
                            s, plans, plan, reps, sink);
     return hipGetLastError();
 }
+
+#ifdef MSG_STAMPS
+// phase stamps of k_fir8 (debug builds): read and reset
+extern "C" int msg_debug_stamps_fir(unsigned long long* out, int n) {
+    unsigned long long h[16];
+    if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_fir_stamps), sizeof(h)) != hipSuccess) return 3;
+    for (int i = 0; i < n && i < 16; ++i) out[i] = h[i];
+    const unsigned long long z[16] = {};
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_fir_stamps), z, sizeof(z)) == hipSuccess ? 0 : 3;
+}
+#endif
