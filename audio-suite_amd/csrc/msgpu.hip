@@ -201,6 +201,13 @@ struct msg_ctx {
     bool fir4 = true;            // M = 16384 blocks on k_fir4 (MSGPU_FIR4=0: k_fir2, A/B and tests)
     bool fir8 = true;            // N = 65536 one-partition filters on k_fir8 (MSGPU_FIR8=0: off, A/B and tests)
     int fir64 = 1;               // float64 FIR of saturated renders: 0 off, 1 predicted, 2 every FIR preset (MSGPU_FIR64)
+    // k_fir8 blocks (MSGPU_FIR8P): 0 one workgroup per block, 1 persistent workgroups
+    // (one per CU, per-XCD block counters; C3 isolated FIR 2.03 -> 1.86 ms, C5 131.6
+    // -> 125.9 ms per step, profiles/r04r_ab.json), 2 persistent + the next block's
+    // segment streamed through L2 during the epilogue (measured slower: 2.05 - 2.10 ms),
+    // 3 persistent + the next segment loaded into registers during the epilogue
+    int fir8p = 1;
+    int n_cu = 256;              // compute units (persistent grids)
     // Q <= 2 presets on the streaming k_fir4s (MSGPU_FIR4S=1; off by default: at
     // C3's 24 blocks per preset its H re-reads miss L2 and cancel the saved transforms)
     bool fir4s = false;
@@ -247,6 +254,7 @@ struct msg_ctx {
     Slice<int32_t> st_count, odd_list, odd_cnt;
     DevBuf<double> f64_stats;                   // per preset: sum y^2, sum (1 + (d y)^2)^-2
     DevBuf<int32_t> f64_slot_of, f64_slot_preset, f64_nslots;
+    DevBuf<int32_t> fir8_ctr;           // k_fir8p's per-XCD block counters
     DevBuf<float> f64_h;
     DevBuf<double2> f64_hs;
     // float64 grain chain (kernels_grain64.h)
@@ -681,6 +689,12 @@ msg_ctx* msg_create(int device_ordinal) {
     if (const char* e = getenv("MSGPU_FIR4")) ctx->fir4 = e[0] != '0';
     if (const char* e = getenv("MSGPU_FIR8")) ctx->fir8 = e[0] != '0';
     if (const char* e = getenv("MSGPU_FIR64")) ctx->fir64 = atoi(e);
+    if (const char* e = getenv("MSGPU_FIR8P")) ctx->fir8p = atoi(e);
+    {
+        int cu = 0;
+        if (hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, device_ordinal) == hipSuccess && cu >= MSG_XCDS)
+            ctx->n_cu = cu;
+    }
     if (const char* e = getenv("MSGPU_FIR4S")) ctx->fir4s = e[0] == '1';
     if (const char* e = getenv("MSGPU_FIR4S_WGS")) ctx->fir4s_wgs = std::max(1, atoi(e));
     if (const char* e = getenv("MSGPU_FIR4S_K")) ctx->fir4s_kmax = std::max(2, std::min(64, atoi(e)));
@@ -1903,7 +1917,13 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
         for (int i = 0; i < 7; ++i) {
             if (fjob_off[i + 1] <= fjob_off[i]) continue;
             const unsigned nj = (unsigned)(fjob_off[i + 1] - fjob_off[i]);
-            if (i == 6)
+            if (i == 6 && ctx->fir8p > 0) {
+                // persistent: one workgroup per CU (at most one per block), a multiple of the XCD count
+                const unsigned grid = (unsigned)std::max(MSG_XCDS, (std::min((int)nj, ctx->n_cu) / MSG_XCDS) * MSG_XCDS);
+                HIPCHK(ctx, ctx->fir8_ctr.ensure((size_t)MSG_XCDS * FIR8P_CTR));
+                HIPCHK(ctx, launch_fir8p(nj, grid, ctx->fir8p - 1, s, ctx->prt.p, ctx->fir_jobs.p + fjob_off[i],
+                                         ctx->d_fir4tab, ctx->hspec.p, ctx->mono_a.p, ctx->mono_y.p, ctx->fir8_ctr.p));
+            } else if (i == 6)
                 HIPCHK(ctx, launch_fir8(nj, s, ctx->prt.p, ctx->fir_jobs.p + fjob_off[i], ctx->d_fir4tab, ctx->hspec.p,
                                         ctx->mono_a.p, ctx->mono_y.p));
             else if (i == 5)

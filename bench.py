@@ -136,6 +136,8 @@ def measured_traffic(prefixes, cfg, batch):
 def kernel_label(stage):
     if stage == "fir_kernel":           # one of them per preset, by FIR size (C3/C4/C5: k_fir8)
         return " / ".join(k.rstrip("<") for k in STAGE_KERNEL[stage])
+    if stage == "stereo":               # the window also holds the float64 route's flag / slot kernels
+        return "k_stereo_max+k_stereo_out (window incl. the float64 FIR route's flag)"
     return "+".join(k.rstrip("<") for k in STAGE_KERNEL[stage])
 
 
