@@ -294,15 +294,13 @@ k_fir8(const PresetRt* __restrict__ rt, const int2* __restrict__ jobs, const flo
 // filter spectrum), then help the other XCDs' ranges.  A workgroup stays on
 // its CU for the launch, so the blocks no longer queue for CUs freed by other
 // streams' kernels (the FIR window per 341-preset launch in the timed region:
-// 2.69 -> 0.69 ms).  PREFETCH = 1 (MSGPU_FIR8P=2) also streams the next
-// block's segment through L2 during the epilogue with LDS-DMA loads into a
-// 1 KB landing slot whose contents are never read; measured slower (the
-// blocks of an isolated launch run in step, so the prefetch joins the same
-// HBM burst as the segment loads it was meant to hide).
+// 2.69 -> 0.69 ms).  Two ways of hiding the segment load behind the previous
+// block were measured and dropped (profiles/r04r_ab.json, r04t_*): streaming
+// it through L2 during the epilogue with LDS-DMA loads into a never-read slot
+// (the blocks of a launch run in step, so the prefetch joins the same HBM
+// burst: isolated FIR 2.05 - 2.10 ms against 1.86), and loading it into the
+// registers the epilogue frees (328 B of spills per lane: 2.64 - 2.70 ms).
 // ---------------------------------------------------------------------------
-typedef __attribute__((address_space(1))) void fir8_gvoid;
-typedef __attribute__((address_space(3))) void fir8_lvoid;
-
 namespace fir8 {
 // this XCD's share [lo, lo + cnt) of n jobs (the xcd_block partition)
 MSG_DEV void xcd_range(int n, int x, int& lo, int& cnt) {
@@ -310,23 +308,9 @@ MSG_DEV void xcd_range(int n, int x, int& lo, int& cnt) {
     lo = x < rem ? x * (per + 1) : rem * (per + 1) + (x - rem) * per;
     cnt = per + (x < rem ? 1 : 0);
 }
-// the segment of job j through L2: 16-byte granules of x[s0, s0 + N) inside [0, n)
-MSG_DEV void prefetch_segment(const PresetRt* __restrict__ rt, int2 j, const float* __restrict__ x_in,
-                              float4* slot) {
-    const PresetRt& pr = rt[j.x];
-    const int64_t s0 = (int64_t)j.y * pr.fir_B - (pr.fir_P - 1);
-    const int64_t a = s0 > 0 ? s0 : 0;
-    const int64_t e = s0 + N < pr.out_n ? s0 + N : pr.out_n;
-    if (e <= a) return;
-    // mono regions start 16-byte aligned and are padded to a multiple of 4 floats
-    const float* base = x_in + pr.y_off + ((a >> 2) << 2);
-    const int ng = (int)(((e + 3) >> 2) - (a >> 2));
-    for (int g = (int)threadIdx.x; g < ng; g += T)
-        __builtin_amdgcn_global_load_lds((fir8_gvoid*)(base + 4 * g), (fir8_lvoid*)slot, 16, 0, 0);
-}
 }  // namespace fir8
 
-template <int PREFETCH>
+template <int UNUSED = 0>
 __global__ void __launch_bounds__(fir8::T)
 k_fir8p(const PresetRt* __restrict__ rt, const int2* __restrict__ jobs, int n_jobs, const float2* __restrict__ tables,
         const float2* __restrict__ hspec, const float* __restrict__ x_in, float* __restrict__ y_out,
@@ -334,7 +318,6 @@ k_fir8p(const PresetRt* __restrict__ rt, const int2* __restrict__ jobs, int n_jo
     using namespace fir8;
     extern __shared__ __attribute__((aligned(16))) float2 lds[];
     __shared__ int s_take[2];
-    __shared__ __attribute__((aligned(16))) float4 s_slot[64];   // LDS-DMA landing slot (never read)
     float2* tab = lds;
     float2* buf = lds + G::TAB;
     const int t = otid();
@@ -346,8 +329,6 @@ k_fir8p(const PresetRt* __restrict__ rt, const int2* __restrict__ jobs, int n_jo
     if (t == 0) s_take[0] = atomicAdd(ctr + x0 * FIR8P_CTR, 1);
     __syncthreads();                              // tables visible, first take
     int cur = s_take[0], par = 1;
-    float2 a[R1], b[R1];
-    bool have = false;                            // PREFETCH 2: a, b already hold this block's segment
     for (;;) {
         while (cur >= cnt) {                      // range done: the next XCD's (uniform)
             if (++k == MSG_XCDS) return;
@@ -365,7 +346,8 @@ k_fir8p(const PresetRt* __restrict__ rt, const int2* __restrict__ jobs, int n_jo
         const int P = pr.fir_P;                   // Q == 1
         const int64_t n = pr.out_n;
         const int64_t t0 = (int64_t)job.y * pr.fir_B;
-        if (!have) load_halves(x_in + pr.y_off, n, t0 - (P - 1), a, b);
+        float2 a[R1], b[R1];
+        load_halves(x_in + pr.y_off, n, t0 - (P - 1), a, b);
         if (t == 0) s_take[par] = atomicAdd(ctr + xr * FIR8P_CTR, 1);   // the block after this one
         dif_split(tab, a, b);
         const float2* He = hspec + pr.h_off;
@@ -379,23 +361,8 @@ k_fir8p(const PresetRt* __restrict__ rt, const int2* __restrict__ jobs, int n_jo
         float2 (&B)[R1] = a;                      // a is dead: its registers take B
         inv_half<true>(buf, tab, acc, B);
         const int nxt = s_take[par];              // written before this block's first barrier
-        // the epilogue's LDS reads come first: the compiler makes any LDS read
-        // after an LDS-DMA load wait for it
-        const float2 wt = fir4_wM(tab, G::OFF_PLO, G::OFF_PHI, t);
-        if (PREFETCH == 1 && nxt < cnt) prefetch_segment(rt, jobs[lo + nxt], x_in, s_slot);
-        // PREFETCH 2: the next block's segment (interior blocks: whole and 8-byte
-        // aligned) loads into a[r] / b[r] as the epilogue frees them (B is a)
-        bool pf = false;
-        const float2* zn = nullptr;
-        if (PREFETCH == 2 && nxt < cnt) {
-            const int2 jn = jobs[lo + nxt];
-            const PresetRt& pn = rt[jn.x];
-            const int64_t s0n = (int64_t)jn.y * pn.fir_B - (pn.fir_P - 1);
-            const float* xs = x_in + pn.y_off + s0n;
-            pf = s0n >= 0 && s0n + N <= pn.out_n && (((uintptr_t)xs) & 7) == 0;
-            zn = reinterpret_cast<const float2*>(xs);
-        }
         // F[m] = A + W_M^m B, F[m + MH] = A - W_M^m B; z'[m] = conj(F[m]) / M
+        const float2 wt = fir4_wM(tab, G::OFF_PLO, G::OFF_PHI, t);
         const SegOut so = seg_out(y_out, pr.y_off, t0, n, N - P + 1, P);
         const int d0 = 2 * t - (P - 1);
         const float s = 1.0f / (float)M;
@@ -406,12 +373,7 @@ k_fir8p(const PresetRt* __restrict__ rt, const int2* __restrict__ jobs, int n_jo
 #pragma unroll
             for (int h = 0; h < 2; ++h)
                 so.put((uint32_t)(d0 + 2 * (r * NB1 + h * MH)), make_float2(f[h].x * s, -f[h].y * s));
-            if (PREFETCH == 2 && pf) {
-                a[r] = at32(zn, t + r * NB1);
-                b[r] = at32(zn, t + r * NB1 + MH);
-            }
         }
-        have = pf;
         cur = nxt;
         par ^= 1;
     }

@@ -27,10 +27,6 @@ void fir_init_attrs() {
                               Fir4Geo<16384>::LDS_BYTES);
     (void)hipFuncSetAttribute((const void*)k_fir8p<0>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               Fir4Geo<16384>::LDS_BYTES);
-    (void)hipFuncSetAttribute((const void*)k_fir8p<1>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              Fir4Geo<16384>::LDS_BYTES);
-    (void)hipFuncSetAttribute((const void*)k_fir8p<2>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              Fir4Geo<16384>::LDS_BYTES);
     (void)hipFuncSetAttribute((const void*)k_fir8_hconv<0>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               Fir4Geo<16384>::LDS_BYTES);
     (void)hipFuncSetAttribute((const void*)k_fir8_spec<double>, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -134,21 +130,13 @@ hipError_t launch_fir8(unsigned grid, hipStream_t s, const PresetRt* rt, const i
 }
 
 // persistent k_fir8 (fir8_fft.h): one resident workgroup per CU, blocks from
-// per-XCD counters (zeroed here, MSG_XCDS x FIR8P_CTR int32), prefetch 0 / 1 (L2) / 2 (registers)
-hipError_t launch_fir8p(unsigned n_jobs, unsigned grid, int prefetch, hipStream_t s, const PresetRt* rt,
-                        const int2* jobs, const float2* tables, const float2* hspec, const float* x_in, float* y_out,
-                        int32_t* ctr) {
+// per-XCD counters (zeroed here, MSG_XCDS x FIR8P_CTR int32)
+hipError_t launch_fir8p(unsigned n_jobs, unsigned grid, hipStream_t s, const PresetRt* rt, const int2* jobs,
+                        const float2* tables, const float2* hspec, const float* x_in, float* y_out, int32_t* ctr) {
     hipError_t e = hipMemsetAsync(ctr, 0, sizeof(int32_t) * MSG_XCDS * FIR8P_CTR, s);
     if (e != hipSuccess) return e;
-    if (prefetch == 2)
-        hipLaunchKernelGGL((k_fir8p<2>), dim3(grid), dim3(fir8::T), Fir4Geo<16384>::LDS_BYTES, s, rt, jobs,
-                           (int)n_jobs, tables, hspec, x_in, y_out, ctr);
-    else if (prefetch == 1)
-        hipLaunchKernelGGL((k_fir8p<1>), dim3(grid), dim3(fir8::T), Fir4Geo<16384>::LDS_BYTES, s, rt, jobs,
-                           (int)n_jobs, tables, hspec, x_in, y_out, ctr);
-    else
-        hipLaunchKernelGGL((k_fir8p<0>), dim3(grid), dim3(fir8::T), Fir4Geo<16384>::LDS_BYTES, s, rt, jobs,
-                           (int)n_jobs, tables, hspec, x_in, y_out, ctr);
+    hipLaunchKernelGGL((k_fir8p<0>), dim3(grid), dim3(fir8::T), Fir4Geo<16384>::LDS_BYTES, s, rt, jobs, (int)n_jobs,
+                       tables, hspec, x_in, y_out, ctr);
     return hipGetLastError();
 }
 

@@ -203,9 +203,7 @@ struct msg_ctx {
     int fir64 = 1;               // float64 FIR of saturated renders: 0 off, 1 predicted, 2 every FIR preset (MSGPU_FIR64)
     // k_fir8 blocks (MSGPU_FIR8P): 0 one workgroup per block, 1 persistent workgroups
     // (one per CU, per-XCD block counters; C3 isolated FIR 2.03 -> 1.86 ms, C5 131.6
-    // -> 125.9 ms per step, profiles/r04r_ab.json), 2 persistent + the next block's
-    // segment streamed through L2 during the epilogue (measured slower: 2.05 - 2.10 ms),
-    // 3 persistent + the next segment loaded into registers during the epilogue
+    // -> 125.9 ms per step, profiles/r04r_ab.json)
     int fir8p = 1;
     int n_cu = 256;              // compute units (persistent grids)
     // Q <= 2 presets on the streaming k_fir4s (MSGPU_FIR4S=1; off by default: at
@@ -1921,7 +1919,7 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
                 // persistent: one workgroup per CU (at most one per block), a multiple of the XCD count
                 const unsigned grid = (unsigned)std::max(MSG_XCDS, (std::min((int)nj, ctx->n_cu) / MSG_XCDS) * MSG_XCDS);
                 HIPCHK(ctx, ctx->fir8_ctr.ensure((size_t)MSG_XCDS * FIR8P_CTR));
-                HIPCHK(ctx, launch_fir8p(nj, grid, ctx->fir8p - 1, s, ctx->prt.p, ctx->fir_jobs.p + fjob_off[i],
+                HIPCHK(ctx, launch_fir8p(nj, grid, s, ctx->prt.p, ctx->fir_jobs.p + fjob_off[i],
                                          ctx->d_fir4tab, ctx->hspec.p, ctx->mono_a.p, ctx->mono_y.p, ctx->fir8_ctr.p));
             } else if (i == 6)
                 HIPCHK(ctx, launch_fir8(nj, s, ctx->prt.p, ctx->fir_jobs.p + fjob_off[i], ctx->d_fir4tab, ctx->hspec.p,

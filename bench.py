@@ -47,7 +47,7 @@ HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: 8.0 TB/s spec
 PROFILES = os.path.join(REPO, "profiles")
 # bench stage -> the kernels it times (rocprofv3 kernel-name prefixes)
 STAGE_KERNEL = {"generate": ("k_gen_normal",), "spectral": ("k_spec3", "k_spectral"), "overlap_add": ("k_ola_env",),
-                "fir_kernel": ("k_fir8<", "k_fir4<", "k_fir2<"),
+                "fir_kernel": ("k_fir8p<", "k_fir8<", "k_fir4<", "k_fir2<"),
                 # the stereo window also holds the float64 FIR route (flag, h, spectra,
                 # blocks, peak again) and the odd-length rotation
                 "stereo": ("k_stereo_max", "k_stereo_out", "k_stereo_remax", "k_fir64", "k_h64", "k_hspec64", "k_so_"),
@@ -134,7 +134,7 @@ def measured_traffic(prefixes, cfg, batch):
 
 
 def kernel_label(stage):
-    if stage == "fir_kernel":           # one of them per preset, by FIR size (C3/C4/C5: k_fir8)
+    if stage == "fir_kernel":           # one of them per preset, by FIR size (C3/C4/C5: k_fir8p)
         return " / ".join(k.rstrip("<") for k in STAGE_KERNEL[stage])
     if stage == "stereo":               # the window also holds the float64 route's flag / slot kernels
         return "k_stereo_max+k_stereo_out (window incl. the float64 FIR route's flag)"

@@ -262,18 +262,17 @@ def test_fir64_route(msgpu, irs, extra_renders, golden_extra):
 
 
 def test_fir8_persistent_bit_identical(msgpu, irs, full_renders):
-    """k_fir8's persistent form (MSGPU_FIR8P=1: one workgroup per CU taking
-    blocks from per-XCD counters; =2, the default, also streaming the next
-    block's segment through L2) computes every block with the same arithmetic
-    as one workgroup per block (=0): the outputs are bit-identical, for a batch
+    """k_fir8's persistent form (MSGPU_FIR8P=1, the default: one workgroup per
+    CU taking blocks from per-XCD counters) computes every block with the same
+    arithmetic as one workgroup per block (=0): the outputs are bit-identical,
+    for a batch
     whose block count is not a multiple of the XCD count (edge blocks, short
     presets, a preset without a filter among them) and for C3."""
     params = [msgpu.config_params("C3", seed=1000 + s, irs=irs) for s in range(3)]
     params += [msgpu.config_params("C3", seed=2000, irs=irs, out_dur_s=0.06),
                msgpu.config_params("C3", seed=2001, irs=irs, out_dur_s=0.035),   # C3's attack: 7680 frames
                msgpu.merged(out_dur_s=0.2, seed=5)]
-    outs = {m: _render_env(params, {"MSGPU_FIR8P": m})[1] for m in ("0", "1", "2")}
+    outs = {m: _render_env(params, {"MSGPU_FIR8P": m})[1] for m in ("0", "1")}
     assert np.array_equal(outs["0"], outs["1"])
-    assert np.array_equal(outs["0"], outs["2"])
     packed, _ = _render_env(params[:1], {})
-    assert rms(outs["2"][:int(packed.out_n[0])], full_renders["C3_audio"]) <= RMS_TOL
+    assert rms(outs["1"][:int(packed.out_n[0])], full_renders["C3_audio"]) <= RMS_TOL

@@ -436,7 +436,9 @@ def test_progress_messages_match_reference(msgpu, irs, full_renders):
                                                   ("C3", 4.0, None, 36000.0), ("C3", 4.0, 0.0, 37400.0),
                                                   ("C3", 1.0, None, None), ("C3", 4.0, None, None),
                                                   ("C4", 4.0, None, None), ("C4", 4.0, 0.0, None),
-                                                  ("C4", 3.3, None, 14000.0), ("C4", 2.6, 4000.0, 23000.0)])
+                                                  ("C4", 3.3, None, 14000.0), ("C4", 2.6, 4000.0, 23000.0),
+                                                  ("C5", 4.0, None, None), ("C5", 2.0, None, 600.0),
+                                                  ("C5", 0.5, None, None), ("C5", 1.0, 0.0, 300.0)])
 def test_spec3_band_pruned_vs_general(msgpu, irs, monkeypatch, cfg, stretch, roll, cut):
     """The band-pruned 37 500-sample spectral kernel (k_spec3, default) against
     the general compile-time-plan kernel (MSGPU_SPEC3=0): stretch below 1, at 1
@@ -444,9 +446,12 @@ def test_spec3_band_pruned_vs_general(msgpu, irs, monkeypatch, cfg, stretch, rol
     (C3 x4 at 18 kHz) and wide ones past it (C4's x4 stretch at x200 unfold:
     ky ~ 0.96 M, and a 36 kHz or 37.4 kHz cutoff at x100), which build each
     inverse input from Y[i] and Y[M - i].  Both match the oracle at 1e-5 RMS and
-    each other, audio and meta grain_last."""
+    each other, audio and meta grain_last.  C5's 1920-sample grains (a band limit
+    above the design Nyquist, stretches 4, 2, 0.5, 1) run k_spectral_ct either
+    way: a 960-point k_spec3 plan matched them (1.1e-6 RMS) but was no faster
+    (C5 spectral 4.12 vs 4.09 ms isolated, profiles/r04v_c5_spec3.json)."""
     from oracle import msound_oracle as O
-    kw = dict(seed=31, out_dur_s=0.1, partial_stretch=stretch)
+    kw = dict(seed=31, out_dur_s=2.0 if cfg == "C5" else 0.1, partial_stretch=stretch)
     if roll is not None:
         kw["bandlimit_roll_hz"] = roll
     if cut is not None:
