@@ -322,6 +322,9 @@ k_fir8p(const PresetRt* __restrict__ rt, const int2* __restrict__ jobs, int n_jo
     float2* buf = lds + G::TAB;
     const int t = otid();
     { TabCopy<G::TAB_USED, T> tc; tc.fetch(tables); tc.put(tab); }
+    // ctr[x * FIR8P_CTR]: XCD x's next block; ctr[MSG_XCDS * FIR8P_CTR]: workgroups
+    // done.  The last workgroup to finish zeroes them for the next launch (no
+    // memset kernel: one would queue for a CU behind the other streams' work).
     // ranges in order: this workgroup's XCD first, then the others'
     const int x0 = (int)(blockIdx.x % MSG_XCDS);
     int k = 0, lo, cnt;
@@ -331,7 +334,7 @@ k_fir8p(const PresetRt* __restrict__ rt, const int2* __restrict__ jobs, int n_jo
     int cur = s_take[0], par = 1;
     for (;;) {
         while (cur >= cnt) {                      // range done: the next XCD's (uniform)
-            if (++k == MSG_XCDS) return;
+            if (++k == MSG_XCDS) break;
             const int x = (x0 + k) % MSG_XCDS;
             xcd_range(n_jobs, x, lo, cnt);
             __syncthreads();                      // every wave has read s_take[par] of the last block
@@ -340,6 +343,7 @@ k_fir8p(const PresetRt* __restrict__ rt, const int2* __restrict__ jobs, int n_jo
             cur = s_take[par];
             par ^= 1;
         }
+        if (k == MSG_XCDS) break;
         const int xr = (x0 + k) % MSG_XCDS;
         const int2 job = jobs[lo + cur];
         const PresetRt& pr = rt[job.x];
@@ -376,6 +380,11 @@ k_fir8p(const PresetRt* __restrict__ rt, const int2* __restrict__ jobs, int n_jo
         }
         cur = nxt;
         par ^= 1;
+    }
+    // every take of this workgroup has returned (thread 0 made them in order)
+    if (t == 0 && atomicAdd(ctr + MSG_XCDS * FIR8P_CTR, 1) == (int)gridDim.x - 1) {
+        for (int x = 0; x < MSG_XCDS; ++x) ctr[x * FIR8P_CTR] = 0;
+        ctr[MSG_XCDS * FIR8P_CTR] = 0;
     }
 }
 

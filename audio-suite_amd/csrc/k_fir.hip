@@ -130,11 +130,10 @@ hipError_t launch_fir8(unsigned grid, hipStream_t s, const PresetRt* rt, const i
 }
 
 // persistent k_fir8 (fir8_fft.h): one resident workgroup per CU, blocks from
-// per-XCD counters (zeroed here, MSG_XCDS x FIR8P_CTR int32)
+// per-XCD counters (ctr: (MSG_XCDS + 1) x FIR8P_CTR int32, zero before the first
+// launch; each launch leaves them zero)
 hipError_t launch_fir8p(unsigned n_jobs, unsigned grid, hipStream_t s, const PresetRt* rt, const int2* jobs,
                         const float2* tables, const float2* hspec, const float* x_in, float* y_out, int32_t* ctr) {
-    hipError_t e = hipMemsetAsync(ctr, 0, sizeof(int32_t) * MSG_XCDS * FIR8P_CTR, s);
-    if (e != hipSuccess) return e;
     hipLaunchKernelGGL((k_fir8p<0>), dim3(grid), dim3(fir8::T), Fir4Geo<16384>::LDS_BYTES, s, rt, jobs, (int)n_jobs,
                        tables, hspec, x_in, y_out, ctr);
     return hipGetLastError();

@@ -62,18 +62,24 @@ constexpr int GEN_K = MSG_GEN_K;
 #ifndef MSG_GEN_LDS
 #define MSG_GEN_LDS 1
 #endif
-// Emission of a chunk (tuning macro): 2 = the resonant value from per-group chunk
-// bases and a 128-entry offset table, rank by v_mbcnt, the valid lanes as the
-// exec mask; 1 = the round-2 form (the chunk's base evaluated per chunk, rank by
+// Emission of a chunk (tuning macro): 3 = the resonant value from bases at
+// multiples of 64 samples, evaluated 64 at a time (one per lane, once per 64
+// chunks) into LDS, rotated by a 128-entry offset table; 2 = the round-3 form
+// (bases at each group's chunk starts, evaluated by lanes g < G once per group
+// of 8 chunks); rank by v_mbcnt and the valid lanes as the exec mask in both;
+// 1 = the round-2 form (the chunk's base evaluated per chunk, rank by
 // popcount); 0 = cost experiment only (raw normals, wrong output).
 #ifndef MSG_GEN_NOSLOW
 #define MSG_GEN_NOSLOW 0
 #endif
 #ifndef MSG_GEN_EMIT
-#define MSG_GEN_EMIT 2
+#define MSG_GEN_EMIT 3
 #endif
 #if MSG_GEN_EMIT != 1 && !MSG_GEN_LDS
-#error "MSG_GEN_EMIT 0/2 need MSG_GEN_LDS"
+#error "MSG_GEN_EMIT 0/2/3 need MSG_GEN_LDS"
+#endif
+#if MSG_GEN_EMIT == 3 && MSG_GEN_K != 1
+#error "MSG_GEN_EMIT 3 evaluates its bases with one wave per event"
 #endif
 // Jump-ahead constants and the ziggurat fast-path table (ki >> 20, wi * 2^20 as
 // float32 bits).
@@ -262,7 +268,10 @@ k_gen_normal(const msg_preset* __restrict__ presets, const msg_event* __restrict
     __shared__ double s_wi[256];
     __shared__ uint2 s_kw[256];          // (ki >> 20, wi * 2^20 as float32 bits): the fast path's one read
     __shared__ float s_fif[256];         // fi as float32: the slow path's wedge test
-#if MSG_GEN_EMIT == 2
+#if MSG_GEN_EMIT == 3
+    __shared__ float4 s_rot[128];        // resonant: (cos, sin)(2 pi r f/sr), 0.9 * 2^(r k_ring), 0.25 * 2^(r k_exc), r = i
+    __shared__ float4 s_base[64];        // resonant: (sin, cos, 2^(j k_ring), 2^(j k_exc)) at j = 64 (q0 + i)
+#elif MSG_GEN_EMIT == 2
     __shared__ float4 s_rot[128];        // resonant: (cos, sin)(2 pi r f/sr), 0.9 * 2^(r k_ring), 0.25 * 2^(r k_exc), r = i - 64
     __shared__ float4 s_grp[GEN_K][GEN_G];   // resonant, per wave: (sin, cos, 2^(j k_ring), 2^(j k_exc)) at j = group start + 64 g
 #else
@@ -313,7 +322,20 @@ k_gen_normal(const msg_preset* __restrict__ presets, const msg_event* __restrict
     // emitted, r = the lane's rank) from the chunk's uniform sin/cos and decay
     // at j0 and the per-rank rotation/decay table (angle addition, one ds_read
     // per sample instead of the phase reduction, a sine and two exponentials).
-#if MSG_GEN_EMIT == 2
+#if MSG_GEN_EMIT == 3
+    // The value at j = B + t (B = 64 floor(j0 / 64) for the chunk starting at j0,
+    // t in [0, 127)) is the rotation of the base's (sin, cos, decays) by the
+    // offset table entry t, with the 0.9 and 0.25 gains folded into the table.
+    int q0 = -64;                         // s_base holds the bases 64 (q0 + i), i < 64
+    if (!RAW64 && c.mode == MSG_GEN_RESONANT) {
+        for (int i = (int)threadIdx.x; i < 128; i += GEN_T * GEN_K) {
+            const float rf = (float)i;
+            const float2 sc = ring_sincos(rf, c.fa, c.fb);
+            s_rot[i] = make_float4(sc.y, sc.x, 0.9f * __builtin_amdgcn_exp2f(rf * c.k_ring),
+                                   0.25f * __builtin_amdgcn_exp2f(rf * c.k_exc));
+        }
+    }
+#elif MSG_GEN_EMIT == 2
     // Two-level form: the value at j = B + t (B = a group's chunk base, |t| < 64
     // or t in [-64, 0) after slow draws shifted the chunk) is the rotation of the
     // base's (sin, cos, decays) by the offset table entry t, with the 0.9 and
@@ -461,7 +483,9 @@ k_gen_normal(const msg_preset* __restrict__ presets, const msg_event* __restrict
             local = lin;
             rpar ^= 1;
         }
-#if MSG_GEN_EMIT == 2
+#if MSG_GEN_EMIT == 3
+        const bool reson = !RAW64 && c.mode == MSG_GEN_RESONANT;
+#elif MSG_GEN_EMIT == 2
         // resonant: lanes g < G evaluate the group's chunk bases p0 + 64 g (one set
         // of transcendentals per group instead of per chunk)
         const bool reson = !RAW64 && c.mode == MSG_GEN_RESONANT;
@@ -487,7 +511,39 @@ k_gen_normal(const msg_preset* __restrict__ presets, const msg_event* __restrict
                     if (j < n) out64[j] = x[g];
                 }
             }
-#if MSG_GEN_EMIT == 2
+#if MSG_GEN_EMIT == 3
+            else {
+                // rank among the valid lanes (v_mbcnt), the valid mask as the exec mask
+                const int rk = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(valid >> 32),
+                                                              __builtin_amdgcn_mbcnt_lo((uint32_t)valid, 0u));
+                const bool vl = __builtin_amdgcn_inverse_ballot_w64(valid);
+                const int room = n - pc;          // uniform
+                float* __restrict__ ob = out + pc;
+                if (reson) {
+                    // j = pc + rk = 64 q + (d + rk), d = pc - 64 q in [0, 64)
+                    const int q = pc >> 6, d = pc & 63;
+                    if (q - q0 >= 64) {           // uniform, once per 64 chunks: the next 64 bases
+                        q0 = q;
+                        const float jb = (float)(64 * (q0 + lane));
+                        const float2 sc = ring_sincos(jb, c.fa, c.fb);
+                        __syncthreads();          // the previous bases are read
+                        s_base[lane] = make_float4(sc.x, sc.y, __builtin_amdgcn_exp2f(fmaxf(jb * c.k_ring, -126.f)),
+                                                   __builtin_amdgcn_exp2f(fmaxf(jb * c.k_exc, -126.f)));
+                        __syncthreads();
+                    }
+                    const float4 u = s_base[q - q0];
+                    const bool edge = pc < c.fade || pc + 64 > c.n - c.fade;
+                    if (vl && rk < room) {
+                        const float4 tb = s_rot[rk + d];
+                        float v = fmaf(u.x, tb.x, u.y * tb.y) * (u.z * tb.z) + x[g] * (u.w * tb.w);
+                        if (edge) v = gen_fade(c, pc + rk, v);
+                        ob[rk] = v;
+                    }
+                } else if (vl && rk < room) {
+                    ob[rk] = gen_basic_sample(c, pc + rk, (float)x[g]);
+                }
+            }
+#elif MSG_GEN_EMIT == 2
             else {
                 // rank among the valid lanes (v_mbcnt), the valid mask as the exec mask
                 const int rk = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(valid >> 32),

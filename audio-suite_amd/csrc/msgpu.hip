@@ -206,6 +206,7 @@ struct msg_ctx {
     // -> 125.9 ms per step, profiles/r04r_ab.json)
     int fir8p = 1;
     int n_cu = 256;              // compute units (persistent grids)
+    int fir8p_cus = 0;           // persistent FIR workgroups (MSGPU_FIR8P_CUS, A/B; 0: one per CU)
     // Q <= 2 presets on the streaming k_fir4s (MSGPU_FIR4S=1; off by default: at
     // C3's 24 blocks per preset its H re-reads miss L2 and cancel the saved transforms)
     bool fir4s = false;
@@ -688,6 +689,7 @@ msg_ctx* msg_create(int device_ordinal) {
     if (const char* e = getenv("MSGPU_FIR8")) ctx->fir8 = e[0] != '0';
     if (const char* e = getenv("MSGPU_FIR64")) ctx->fir64 = atoi(e);
     if (const char* e = getenv("MSGPU_FIR8P")) ctx->fir8p = atoi(e);
+    if (const char* e = getenv("MSGPU_FIR8P_CUS")) ctx->fir8p_cus = std::max(0, atoi(e));
     {
         int cu = 0;
         if (hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, device_ordinal) == hipSuccess && cu >= MSG_XCDS)
@@ -1917,8 +1919,12 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
             const unsigned nj = (unsigned)(fjob_off[i + 1] - fjob_off[i]);
             if (i == 6 && ctx->fir8p > 0) {
                 // persistent: one workgroup per CU (at most one per block), a multiple of the XCD count
-                const unsigned grid = (unsigned)std::max(MSG_XCDS, (std::min((int)nj, ctx->n_cu) / MSG_XCDS) * MSG_XCDS);
-                HIPCHK(ctx, ctx->fir8_ctr.ensure((size_t)MSG_XCDS * FIR8P_CTR));
+                const int cus = ctx->fir8p_cus > 0 ? std::min(ctx->fir8p_cus, ctx->n_cu) : ctx->n_cu;
+                const unsigned grid = (unsigned)std::max(MSG_XCDS, (std::min((int)nj, cus) / MSG_XCDS) * MSG_XCDS);
+                if (!ctx->fir8_ctr.p) {   // zeroed once; every launch leaves the counters zero
+                    HIPCHK(ctx, ctx->fir8_ctr.ensure((size_t)(MSG_XCDS + 1) * FIR8P_CTR));
+                    HIPCHK(ctx, hipMemsetAsync(ctx->fir8_ctr.p, 0, sizeof(int32_t) * ctx->fir8_ctr.cap, s));
+                }
                 HIPCHK(ctx, launch_fir8p(nj, grid, s, ctx->prt.p, ctx->fir_jobs.p + fjob_off[i],
                                          ctx->d_fir4tab, ctx->hspec.p, ctx->mono_a.p, ctx->mono_y.p, ctx->fir8_ctr.p));
             } else if (i == 6)
