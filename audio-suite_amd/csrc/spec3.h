@@ -63,6 +63,11 @@ struct Spec3Plan {
     static MSG_HD constexpr int phB(int x) { return x + (x / NB3) * PADB; }
 };
 
+// MSG_S3_WIDE_TW: the wide band's inverse pass 1 takes w_i as w_j times a
+// compile-time constant per r instead of a two-level table product per input
+#ifndef MSG_S3_WIDE_TW
+#define MSG_S3_WIDE_TW 1
+#endif
 // MSG_S3_PLAN (tuning builds): radices R1, R2, R3 and the exchange-B pad
 #ifndef MSG_S3_PLAN
 #define MSG_S3_PLAN 25, 30, 25, 11
@@ -267,14 +272,18 @@ MSG_DEV void s3_rest(float2* buf, const float2* tab, const EventRt* __restrict__
                 return make_float2((b.x - a.x) * fr + a.x, (b.y - a.y) * fr + a.y);
             };
             for (int k = kz + otid(); k < ky; k += T) buf[k] = Y(k);
+            __syncthreads();                            // those reads reach up to ~kz
             // [0, kz) in T-bin chunks from the top down: chunk [a, a + T) reads X
             // below (a + T) / f + 1 <= a + T, so one barrier between a chunk's
             // reads and its writes orders it against every lower chunk's reads
-            // (a register array over all of [0, kz) spilled to scratch)
+            // (a register array over all of [0, kz) spilled to scratch).  No
+            // read of this loop reaches past (kz - 1) / f + 1, so the chunks
+            // above it need no barrier (C4: 2 of 6 chunks take one).
+            const int rmax = stretch ? (int)((double)(kz - 1) * inv_f) + 2 : kz;   // one bin of margin
             for (int a = ((kz - 1) / T) * T; a >= 0; a -= T) {
                 const int k = a + otid();
                 const float2 v = k < kz ? Y(k) : make_float2(0.f, 0.f);
-                __syncthreads();
+                if (a <= rmax) __syncthreads();         // uniform
                 if (k < kz) buf[k] = v;
             }
         }
@@ -286,6 +295,24 @@ MSG_DEV void s3_rest(float2* buf, const float2* tab, const EventRt* __restrict__
         {
             const float2 z0 = make_float2(0.f, 0.f);
             float2 v[P::R1];
+#if MSG_S3_WIDE_TW
+            // inputs i = j + r NB1: w_i = w_j . exp(-i pi r NB1 / M), one table twiddle
+            // per thread and a compile-time constant per r (no table reads per input)
+            const float2 wj = s3_w2M<P>(tab, j < P::NB1 ? j : 0);
+            if (j < P::NB1)
+                s3_pass1<P>(v, j, [&](int i) {
+                    const float2 a = i < ky ? buf[i] : z0, b = M - i < ky ? buf[M - i] : z0;
+                    if (i == 0) return make_float2(0.5f * (a.x + b.x), -0.5f * (a.x - b.x));   // DC, Nyquist (irfft)
+                    const int r = (i - j) / P::NB1;
+                    const float2 wr = make_float2((float)__builtin_cos(3.14159265358979323846 * r * P::NB1 / M),
+                                                  (float)-__builtin_sin(3.14159265358979323846 * r * P::NB1 / M));
+                    const float2 wi = r == 0 ? wj : cmul(wj, wr);           // w_i
+                    const float2 e1 = cscale(a, 0.5f), o1 = cscale(cmulc(a, wi), 0.5f);
+                    // mirror term with w_{M-i} = -conj(w_i): o1' = -(b . w_i) / 2
+                    const float2 e2 = cscale(b, 0.5f), o2 = cscale(cmul(b, wi), -0.5f);
+                    return make_float2((e1.x - o1.y) + (e2.x + o2.y), -(e1.y + o1.x) + (e2.y - o2.x));
+                });
+#else
             if (j < P::NB1)
                 s3_pass1<P>(v, j, [&](int i) {
                     const float2 a = i < ky ? buf[i] : z0, b = M - i < ky ? buf[M - i] : z0;
@@ -298,6 +325,7 @@ MSG_DEV void s3_rest(float2* buf, const float2* tab, const EventRt* __restrict__
                     const float2 e2 = cscale(b, 0.5f), o2 = cscale(cmul(b, wi), -0.5f);
                     return make_float2((e1.x - o1.y) + (e2.x + o2.y), -(e1.y + o1.x) + (e2.y - o2.x));
                 });
+#endif
             __syncthreads();                            // Y fully read
             if (j < P::NB1) s3_store_a<P>(buf, v, j);
         }
