@@ -28,10 +28,10 @@ def render_batch(params_list, device: int = 0, devices=None):
     return _rb(params_list, device)
 
 
-def DevicePool(devices, stub: bool = False):
+def DevicePool(devices, stub: bool = False, share_devices: bool = False):
     """One render worker per GPU (multi.py); create it before any GPU call."""
     from .multi import DevicePool as _P
-    return _P(devices, stub)
+    return _P(devices, stub, share_devices)
 
 
 def stft_mag_db(x, sr=None, win=2048, hop=256, max_frames=3000, device: int = 0):

@@ -98,12 +98,14 @@ def _render_into(eng, params, buf, frame_off, out_n):
 class DevicePool:
     """One worker process per device; ``render_batch`` shards by predicted cost."""
 
-    def __init__(self, devices, stub: bool = False):
+    def __init__(self, devices, stub: bool = False, share_devices: bool = False):
+        """``share_devices=True`` lets several workers use one device (a rehearsal
+        of the multi-process path on a one-GPU box, tools/multi_rehearsal.py)."""
         import multiprocessing as mp
         self.devices = [int(d) for d in devices]
         if not self.devices:
             raise ValueError("no devices")
-        if len(set(self.devices)) != len(self.devices):
+        if not share_devices and len(set(self.devices)) != len(self.devices):
             raise ValueError("devices must be distinct")
         if not stub and _gpu_touched():
             raise RuntimeError("DevicePool must be created before this process makes its first GPU call "

@@ -592,6 +592,9 @@ def parse():
     ap.add_argument("--point-steps", type=int, default=10)
     ap.add_argument("--dry-run", type=float, default=0.0, metavar="MS",
                     help="CPU launcher test: a step sleeps MS*(rank+1) ms instead of rendering")
+    ap.add_argument("--rehearse-one-gpu", action="store_true",
+                    help="every rank renders on device 0 (a rehearsal of the multi-rank path on a "
+                         "one-GPU box; the ranks share the GPU, so the line is not a scaling point)")
     return ap.parse_args()
 
 
@@ -640,11 +643,23 @@ def launch(args):
     return code
 
 
+def line_stream():
+    """The bench line's own stream: fd 1 as it was, while fd 1 itself is pointed
+    at stderr for everything else in this process (gloo prints its "[Gloo] Rank
+    r is connected to ..." lines to fd 1 from C++), so stdout carries the one
+    JSON line and nothing else."""
+    sys.stdout.flush()
+    out = os.fdopen(os.dup(1), "w", buffering=1)
+    os.dup2(2, 1)
+    return out
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world == 1 and args.gpus > 1:
         sys.exit(launch(args))
+    out = line_stream()
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
@@ -659,14 +674,15 @@ def main():
     comm = Comm(rank, world)
     try:
         if args.dry_run:
-            return dry_main(args, comm, cfg, seeds, local, cpus)
+            return dry_main(args, comm, cfg, seeds, local, cpus, out)
         irs = load_irs()
         with open(os.path.join(REPO, "tests", "golden", "golden_info.json")) as f:
             golden = json.load(f)["summaries"]
         with open(os.path.join(REPO, "tests", "golden", "golden_extra.json")) as f:
             golden.update(json.load(f)["summaries"])          # H48_1000..1003 (tools/gen_golden_r3.py)
         gate = None if args.gate in ("", "none") else tuple(int(v) for v in args.gate.split(","))
-        runner = GpuRunner(local, max(1, args.streams), gate, threaded=args.enqueue == "threads")
+        device = 0 if args.rehearse_one_gpu else local
+        runner = GpuRunner(device, max(1, args.streams), gate, threaded=args.enqueue == "threads")
         head = measure(runner, cfg, seeds, default_sub(cfg, args, batch), args.steps, args.warmup, comm, irs,
                        golden, iso_steps=args.iso_steps, from_dicts_steps=args.from_dicts_steps)
         points = {}
@@ -679,7 +695,7 @@ def main():
                                  irs, golden, iso_steps=args.iso_steps,
                                  from_dicts_steps=psteps if (pc == "H48" and args.from_dicts_steps) else 0)
         lat = dropin_latency(cpu) if (rank == 0 and world == 1 and not args.no_cpu) else None
-        ranks = comm.gather({"rank": rank, "pid": os.getpid(), "device": local,
+        ranks = comm.gather({"rank": rank, "pid": os.getpid(), "device": device,
                              "cpus": [cpus[0], cpus[-1], len(cpus)], "host_threads": host_threads(),
                              "seeds": [seeds[0], seeds[-1]], "elapsed_s": round(head["_rank_s"], 6),
                              "frames": head["frames_per_gpu_step"] * args.steps})
@@ -697,7 +713,9 @@ def main():
                            "events_per_gpu_step": head["events_per_gpu_step"],
                            "design_samples_per_gpu_step": head["design_samples_per_gpu_step"],
                            "sub_batches_per_gpu": head["sub_batches"],
-                           "parallelism": f"preset-sharded x{world}", "streams_per_gpu": len(runner.engs),
+                           "parallelism": f"preset-sharded x{world}" + (
+                               " (rehearsal: every rank on device 0)" if args.rehearse_one_gpu else ""),
+                           "streams_per_gpu": len(runner.engs),
                            "stream_gate": args.gate, "enqueue": args.enqueue},
                 "roofline": head["roofline"], "roofline_isolated": head.get("roofline_isolated"),
                 "stage_ms": head["stage_ms"], "stage_algorithmic_GBs": head["stage_algorithmic_GBs"],
@@ -709,12 +727,14 @@ def main():
                 "points": points,
                 "ranks": ranks,
             }
-            print(json.dumps(line), flush=True)
+            if args.rehearse_one_gpu:
+                line["rehearsal"] = "all ranks shared device 0: checks the multi-rank path, not a scaling point"
+            print(json.dumps(line), file=out, flush=True)
     finally:
         comm.close()
 
 
-def dry_main(args, comm, cfg, seeds, local, cpus):
+def dry_main(args, comm, cfg, seeds, local, cpus, out):
     """The launcher path with the device work stubbed (CPU tests): same seeds,
     same timing protocol, per-rank record; prints a 'dry_run' line, no metric."""
     from msgpu.pack import PackedBatch
@@ -730,7 +750,7 @@ def dry_main(args, comm, cfg, seeds, local, cpus):
     if comm.rank == 0:
         total = sum(r["frames"] for r in ranks)
         print(json.dumps({"dry_run": True, "n_gpus": comm.world, "elapsed_max_s": elapsed,
-                          "value": total / elapsed / 1e6, "ranks": ranks}), flush=True)
+                          "value": total / elapsed / 1e6, "ranks": ranks}), file=out, flush=True)
 
 
 if __name__ == "__main__":

@@ -72,8 +72,9 @@ def _run_bench(*args, env_extra=None, timeout=300):
     r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), *args], capture_output=True, text=True,
                        timeout=timeout, env=env, cwd=REPO)
     assert r.returncode == 0, r.stderr[-3000:]
-    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
-    assert len(lines) == 1, r.stdout
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
+    # stdout is the one JSON line: gloo's "[Gloo] Rank r is connected to ..." goes to stderr
+    assert len(lines) == 1 and lines[0].startswith("{"), r.stdout
     return json.loads(lines[0])
 
 
@@ -121,6 +122,7 @@ def test_torchrun_two_ranks_dry_run():
            "--gpus", "2", "--steps", "3", "--warmup", "1", "--batch", "2", "--config", "C2", "--dry-run", "40"]
     r = subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-3000:]
+    assert all(x.startswith("{") for x in r.stdout.splitlines() if x.strip()), r.stdout   # nothing but the line
     lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
     assert len(lines) == 1, r.stdout                       # rank 0 only
     d = lines[0]
