@@ -288,6 +288,7 @@ MSG_DEV void s3_rest(float2* buf, const float2* tab, const EventRt* __restrict__
             }
         }
         __syncthreads();
+        SPEC_STAMP(7);                                  // (stamps build) the wide band's Y gather
         // ---- inverse pass 1 from Y in LDS: conj Z'[i] = PL(Y[i], w_i) + PH(Y[M - i],
         // w_{M-i}), the narrow band's two per-bin terms (w_x = exp(-i pi x / M);
         // w_{M-x} = -conj w_x)

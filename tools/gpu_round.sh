@@ -1,8 +1,8 @@
 #!/bin/bash
-# GPU box (round 4): the GPU suite (all failures listed), then the default bench
+# GPU box: the GPU suite (all failures listed), then the default bench
 # line when the suite ended normally (pass or test failures, no fault/timeout).
 set -o pipefail
-tag=${1:-r04b}
+tag=${1:?usage: tools/gpu_round.sh TAG}
 mkdir -p gpurun_out
 timeout -k 10 500 python -u -m pytest tests -m gpu -v -s --timeout 200 --timeout-method thread \
   > gpurun_out/${tag}_gpu_tests.txt 2>&1

@@ -32,10 +32,13 @@ fn(buf, 16)
 eng.render_packed(packed, out)
 eng.torch.cuda.synchronize()
 fn(buf, 16)
+# stamp 7 (wide band only) closes the Y gather; stamp 4 then holds inverse pass 1 alone
 names = ["setup+F pass1 (HBM)", "F pass2", "F pass3+band Z", "split+mask", "I pass1 (gather)", "I pass2",
-         "I pass3 (HBM)"]
-tot = sum(buf[i] for i in range(7))
+         "I pass3 (HBM)", "wide: Y gather"]
+order = [0, 1, 2, 3, 7, 4, 5, 6]
+tot = sum(buf[i] for i in range(8))
 n_ev = sum(int(i.n_events) for i in eng.last_plan())
-for i, nm in enumerate(names):
+for i in order:
+    nm = names[i]
     print(f"{nm:22s} {buf[i] / max(1, n_ev) / 100.0:10.2f} us/event  {100.0 * buf[i] / max(1, tot):5.1f} %")
 print("events", n_ev, "(wall_clock64 at 100 MHz)")
