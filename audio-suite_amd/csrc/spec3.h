@@ -89,6 +89,36 @@ MSG_DEV void s3_pass1(float2 (&v)[P::R1], int j, In&& in) {
     for (int r = 0; r < P::R1; ++r) v[r] = in(j + r * P::NB1);
     Dft<P::R1, false>::run(v);
 }
+// The stretch interpolation Y[k] = interp(k / f, X) over X[0, kz) (zero
+// outside; MS:117-128), branch-free: both loads issue at clamped indices and
+// the range tests select (a divergent early return cost ~25 scalar and
+// exec-mask instructions per bin).  EXACT32: k / f is exact in float32
+// (1 / f dyadic, spec3_eligible's exact32), with the same j0 and fraction as
+// the float64 form.
+template <bool EXACT32>
+MSG_DEV float2 s3_interp(const float2* buf, int k, int kz, int K, float inv_f32, double inv_f) {
+    int j0;
+    float fr;
+    bool in;
+    if (EXACT32) {
+        const float xs = (float)k * inv_f32;
+        in = xs <= (float)(K - 1) && xs < (float)kz;
+        j0 = in ? (int)xs : 0;
+        fr = xs - (float)j0;
+    } else {
+        const double xs = (double)k * inv_f;
+        in = xs <= (double)(K - 1) && xs < (double)kz;
+        j0 = in ? (int)xs : 0;
+        fr = (float)(xs - (double)j0);
+    }
+    const bool has1 = j0 + 1 < kz;
+    const float2 a = buf[j0];
+    const float2 b1 = buf[has1 ? j0 + 1 : j0];
+    const float2 b = has1 ? b1 : make_float2(0.f, 0.f);
+    const float2 y = make_float2((b.x - a.x) * fr + a.x, (b.y - a.y) * fr + a.y);
+    return in ? y : make_float2(0.f, 0.f);
+}
+
 template <class P> MSG_DEV void s3_store_a(float2* buf, const float2 (&v)[P::R1], int j) {
 #pragma unroll
     for (int r = 0; r < P::R1; ++r) buf[j * P::R1 + r] = v[r];   // exchange A, identity layout
@@ -249,43 +279,34 @@ MSG_DEV void s3_rest(float2* buf, const float2* tab, const EventRt* __restrict__
         // has f > 1, so S reads X only below the bin it writes).
         {
             // k / f in float when that is exact for every k (ex.s3_pad: 1 / f a dyadic
-            // fraction, e.g. the x4 stretch), else in float64 as the narrow path does
+            // fraction, e.g. the x4 stretch), else in float64 as the narrow path does.
+            // The loops are instantiated per case (uniform): tested inside the loop,
+            // the flags cost exec-mask instructions per bin.
             const bool exact32 = ex.s3_pad != 0;
             const float inv_f32 = (float)inv_f;
-            auto Y = [&](int k) -> float2 {       // interp(k / f, X) (MS:117-128)
-                if (!stretch) return k < kz ? buf[k] : make_float2(0.f, 0.f);
-                int j0;
-                float fr;
-                if (exact32) {
-                    const float xs = (float)k * inv_f32;
-                    if (!(xs <= (float)(K - 1) && xs < (float)kz)) return make_float2(0.f, 0.f);
-                    j0 = (int)xs;
-                    fr = xs - (float)j0;
-                } else {
-                    const double xs = (double)k * inv_f;
-                    if (!(xs <= (double)(K - 1) && xs < (double)kz)) return make_float2(0.f, 0.f);
-                    j0 = (int)xs;
-                    fr = (float)(xs - (double)j0);
-                }
-                const float2 a = buf[j0];
-                const float2 b = j0 + 1 < kz ? buf[j0 + 1] : make_float2(0.f, 0.f);
-                return make_float2((b.x - a.x) * fr + a.x, (b.y - a.y) * fr + a.y);
-            };
-            for (int k = kz + otid(); k < ky; k += T) buf[k] = Y(k);
-            __syncthreads();                            // those reads reach up to ~kz
             // [0, kz) in T-bin chunks from the top down: chunk [a, a + T) reads X
-            // below (a + T) / f + 1 <= a + T, so one barrier between a chunk's
+            // at or below its own bins (f > 1), so one barrier between a chunk's
             // reads and its writes orders it against every lower chunk's reads
             // (a register array over all of [0, kz) spilled to scratch).  No
             // read of this loop reaches past (kz - 1) / f + 1, so the chunks
             // above it need no barrier (C4: 2 of 6 chunks take one).
             const int rmax = stretch ? (int)((double)(kz - 1) * inv_f) + 2 : kz;   // one bin of margin
-            for (int a = ((kz - 1) / T) * T; a >= 0; a -= T) {
-                const int k = a + otid();
-                const float2 v = k < kz ? Y(k) : make_float2(0.f, 0.f);
-                if (a <= rmax) __syncthreads();         // uniform
-                if (k < kz) buf[k] = v;
-            }
+            auto gather = [&](auto Y) {
+                for (int k = kz + otid(); k < ky; k += T) buf[k] = Y(k);
+                __syncthreads();                        // those reads reach up to ~kz
+                for (int a = ((kz - 1) / T) * T; a >= 0; a -= T) {
+                    const int k = a + otid();
+                    const float2 v = k < kz ? Y(k) : make_float2(0.f, 0.f);
+                    if (a <= rmax) __syncthreads();     // uniform
+                    if (k < kz) buf[k] = v;
+                }
+            };
+            if (!stretch)
+                gather([&](int k) { return k < kz ? buf[k] : make_float2(0.f, 0.f); });
+            else if (exact32)
+                gather([&](int k) { return s3_interp<true>(buf, k, kz, K, inv_f32, inv_f); });
+            else
+                gather([&](int k) { return s3_interp<false>(buf, k, kz, K, inv_f32, inv_f); });
         }
         __syncthreads();
         SPEC_STAMP(7);                                  // (stamps build) the wide band's Y gather
@@ -332,36 +353,33 @@ MSG_DEV void s3_rest(float2* buf, const float2* tab, const EventRt* __restrict__
         }
         __syncthreads();
     } else {
+    const bool exact32 = ex.s3_pad != 0;
+    const float inv_f32 = (float)inv_f;
     // ---- stretch gather Y = S(X) (MS:117-128) and the irfft packing of bins k
     // and M - k (Y[M - k] = 0 in the band), conjugated for the forward engine
     // (inverse = conj . F . conj): inverse pass 1's nonzero inputs
     {
-        for (int k = otid(); k < ky; k += T) {
-            float2 y;
-            if (!stretch) {
-                y = buf[k];
-            } else {
-                const double xs = (double)k * inv_f;
-                y = make_float2(0.f, 0.f);
-                if (xs >= 0.0 && xs <= (double)(K - 1) && xs < (double)kz) {
-                    const int j0 = (int)xs;
-                    const float fr = (float)(xs - (double)j0);
-                    const float2 a = buf[j0];
-                    const float2 b = j0 + 1 < kz ? buf[j0 + 1] : make_float2(0.f, 0.f);
-                    y = make_float2((b.x - a.x) * fr + a.x, (b.y - a.y) * fr + a.y);
+        auto pack = [&](auto Y) {                   // instantiated per case, as the wide gather
+            for (int k = otid(); k < ky; k += T) {
+                const float2 y = Y(k);
+                if (k == 0) {
+                    buf[pl] = make_float2(0.5f * y.x, -0.5f * y.x);   // imag of Y[0] ignored; Y[M] = 0
+                    buf[zs] = make_float2(0.f, 0.f);
+                } else {
+                    const float2 w = s3_w2M<P>(tab, k);
+                    const float2 e1 = cscale(y, 0.5f);
+                    const float2 o1 = cscale(cmulc(y, w), 0.5f);
+                    buf[pl + k] = make_float2(e1.x - o1.y, -(e1.y + o1.x));
+                    buf[ph + k] = make_float2(e1.x + o1.y, e1.y - o1.x);
                 }
             }
-            if (k == 0) {
-                buf[pl] = make_float2(0.5f * y.x, -0.5f * y.x);   // imag of Y[0] ignored; Y[M] = 0
-                buf[zs] = make_float2(0.f, 0.f);
-            } else {
-                const float2 w = s3_w2M<P>(tab, k);
-                const float2 e1 = cscale(y, 0.5f);
-                const float2 o1 = cscale(cmulc(y, w), 0.5f);
-                buf[pl + k] = make_float2(e1.x - o1.y, -(e1.y + o1.x));
-                buf[ph + k] = make_float2(e1.x + o1.y, e1.y - o1.x);
-            }
-        }
+        };
+        if (!stretch)
+            pack([&](int k) { return buf[k]; });
+        else if (exact32)
+            pack([&](int k) { return s3_interp<true>(buf, k, kz, K, inv_f32, inv_f); });
+        else
+            pack([&](int k) { return s3_interp<false>(buf, k, kz, K, inv_f32, inv_f); });
     }
     __syncthreads();
     // ---- inverse pass 1 (inputs zero outside the stretched band)

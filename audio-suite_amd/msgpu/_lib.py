@@ -11,7 +11,7 @@ import os
 import threading
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.environ.get("MSGPU_LIB", os.path.join(HERE, "libmsgpu.so"))
+LIB_PATH = os.environ.get("MSGPU_LIB") or os.path.join(HERE, "libmsgpu.so")   # unset or empty: the product library
 ABI_VERSION = 2
 
 # status codes (msg_status)
