@@ -119,6 +119,21 @@ MSG_DEV float2 s3_interp(const float2* buf, int k, int kz, int K, float inv_f32,
     return in ? y : make_float2(0.f, 0.f);
 }
 
+// (a.x / 2 - o.y, a.y / 2 + o.x) as one packed FMA (a / 2 - i o for the wide
+// band's inverse inputs; halving is exact, so each half is fma(0.5, a, +-o))
+MSG_DEV f2v s3_half_mi(float2 a, float2 o) {
+    f2v r;
+    asm("v_pk_fma_f32 %0, 0.5, %1, %2 op_sel:[0,0,1] op_sel_hi:[0,1,0] neg_lo:[0,0,1]"
+        : "=v"(r) : "v"(vv(a)), "v"(vv(o)));
+    return r;
+}
+// (a.x + b.x, a.y - b.y)
+MSG_DEV f2v s3_add_neghi(f2v a, f2v b) {
+    f2v r;
+    asm("v_pk_add_f32 %0, %1, %2 neg_hi:[0,1]" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+
 template <class P> MSG_DEV void s3_store_a(float2* buf, const float2 (&v)[P::R1], int j) {
 #pragma unroll
     for (int r = 0; r < P::R1; ++r) buf[j * P::R1 + r] = v[r];   // exchange A, identity layout
@@ -320,7 +335,9 @@ MSG_DEV void s3_rest(float2* buf, const float2* tab, const EventRt* __restrict__
 #if MSG_S3_WIDE_TW
             // inputs i = j + r NB1: w_i = w_j . exp(-i pi r NB1 / M), one table twiddle
             // per thread and a compile-time constant per r (no table reads per input)
-            const float2 wj = s3_w2M<P>(tab, j < P::NB1 ? j : 0);
+            // the 1/2 of both terms folded into the twiddle (w / 2 is exact, so every
+            // product below is exactly half the unscaled one: the same bits)
+            const float2 wjh = cscale(s3_w2M<P>(tab, j < P::NB1 ? j : 0), 0.5f);
             if (j < P::NB1)
                 s3_pass1<P>(v, j, [&](int i) {
                     const float2 a = i < ky ? buf[i] : z0, b = M - i < ky ? buf[M - i] : z0;
@@ -328,11 +345,12 @@ MSG_DEV void s3_rest(float2* buf, const float2* tab, const EventRt* __restrict__
                     const int r = (i - j) / P::NB1;
                     const float2 wr = make_float2((float)__builtin_cos(3.14159265358979323846 * r * P::NB1 / M),
                                                   (float)-__builtin_sin(3.14159265358979323846 * r * P::NB1 / M));
-                    const float2 wi = r == 0 ? wj : cmul(wj, wr);           // w_i
-                    const float2 e1 = cscale(a, 0.5f), o1 = cscale(cmulc(a, wi), 0.5f);
-                    // mirror term with w_{M-i} = -conj(w_i): o1' = -(b . w_i) / 2
-                    const float2 e2 = cscale(b, 0.5f), o2 = cscale(cmul(b, wi), -0.5f);
-                    return make_float2((e1.x - o1.y) + (e2.x + o2.y), -(e1.y + o1.x) + (e2.y - o2.x));
+                    const float2 wh = r == 0 ? wjh : cmul(wjh, wr);         // w_i / 2
+                    const float2 o1 = cmulc(a, wh);                          // a conj(w_i) / 2
+                    // mirror term with w_{M-i} = -conj(w_i): -(b . w_i) / 2
+                    const float2 p2 = cmul(b, wh);
+                    const f2v t1 = s3_half_mi(a, o1), t2 = s3_half_mi(b, p2);
+                    return ff(s3_add_neghi(t2, t1));     // (t1.x + t2.x, -t1.y + t2.y)
                 });
 #else
             if (j < P::NB1)
