@@ -248,12 +248,17 @@ MSG_DEV void s3_rest(float2* buf, const float2* tab, const EventRt* __restrict__
         float2 v[P::R3];
         if (j < P::NB3) s3_pass3<P>(buf, tab, v, j);
         __syncthreads();                            // exchange B fully read
+        // a thread keeps v[r] only for r in two uniform ranges (i < kz needs
+        // r <= (kz - 1) / NB3, M - i < kz needs r >= R3 - 2 - (kz - 1) / NB3): scalar
+        // tests skip the per-lane tests and exec-mask writes of the other r
+        const int rlo = __builtin_amdgcn_readfirstlane((kz - 1) / P::NB3);
+        const int rhi = __builtin_amdgcn_readfirstlane(P::R3 - 2 - (kz - 1) / P::NB3);
         if (j < P::NB3) {
 #pragma unroll
             for (int r = 0; r < P::R3; ++r) {
                 const int i = j + r * P::NB3;
-                if (i < kz) buf[i] = v[r];
-                if (M - i < kz && i > 0) buf[zh + (M - i)] = v[r];
+                if (r <= rlo && i < kz) buf[i] = v[r];
+                if (r >= rhi && M - i < kz && i > 0) buf[zh + (M - i)] = v[r];
             }
         }
     }
@@ -403,9 +408,15 @@ MSG_DEV void s3_rest(float2* buf, const float2* tab, const EventRt* __restrict__
     // ---- inverse pass 1 (inputs zero outside the stretched band)
     j = otid();
     {
+        const int qlo = __builtin_amdgcn_readfirstlane((ky - 1) / P::NB1);
+        const int qhi = __builtin_amdgcn_readfirstlane(P::R1 - 2 - (ky - 1) / P::NB1);
         float2 v[P::R1];
         if (j < P::NB1)
             s3_pass1<P>(v, j, [&](int i) {
+                // inputs i = j + r NB1 outside the band for every thread: r between
+                // the uniform bounds (as forward pass 3's band write), no LDS read
+                const int r = (i - j) / P::NB1;
+                if (r > qlo && r < qhi) return make_float2(0.f, 0.f);
                 const int at = i < ky ? pl + i : (M - i < ky ? ph + (M - i) : zs);
                 return buf[at];
             });
