@@ -95,3 +95,20 @@ def test_pool_refuses_after_gpu_use(monkeypatch):
     monkeypatch.setitem(engine._engines, 0, object())
     with pytest.raises(RuntimeError, match="before this process"):
         multi.DevicePool([0, 1])
+
+
+def test_shared_device_rehearsal(irs):
+    """Two workers on one device only with share_devices=True (the one-GPU
+    rehearsal, tools/multi_rehearsal.py); the split is the same cost cut."""
+    with pytest.raises(ValueError, match="distinct"):
+        DevicePool([0, 0], stub=True)
+    p = DevicePool([0, 0], stub=True, share_devices=True)
+    try:
+        params = mixed(irs)
+        outs = p.render_batch(params)
+        assert [int(a[0, 0]) for a in outs] == list(range(len(params)))
+        split = p.last_split
+        assert [s["device"] for s in split] == [0, 0] and len({s["pid"] for s in split}) == 2
+        assert [split[0]["presets"][0], split[0]["presets"][1], split[1]["presets"][1]] == balance(plan_costs(params), 2)
+    finally:
+        p.close()
