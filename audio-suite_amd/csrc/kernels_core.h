@@ -658,16 +658,12 @@ MSG_DEV int events_starting_by(const msg_event* __restrict__ ev, int n, int64_t 
     return lo;
 }
 
-// Traversal order against the Infinity Cache (tuning A/B): MSG_OLA_REV /
-// MSG_STMAX_REV = 1 walk each XCD's job range backwards, so a consumer starts
-// on the most recently written end of its producer's output (spectral grains
-// -> overlap-add, FIR output -> stereo max) and leaves its own first jobs most
-// recent for the next, forward kernel.
+// Traversal order against the Infinity Cache (tuning A/B): MSG_OLA_REV = 1
+// walks each XCD's job range backwards, so overlap-add starts on the most
+// recently written end of the spectral kernel's grains (measured neutral,
+// profiles/r03ak_traversal_ab.txt).
 #ifndef MSG_OLA_REV
 #define MSG_OLA_REV 0
-#endif
-#ifndef MSG_STMAX_REV
-#define MSG_STMAX_REV 0
 #endif
 MSG_DEV int job_order(int rev) {
     const int b = xcd_block(blockIdx.x, gridDim.x);
@@ -742,334 +738,5 @@ k_ola_env(const msg_event* __restrict__ events, const PresetRt* __restrict__ rt,
     for (int u = 0; u < PER; ++u) {
         const int t = (int)t0 + (int)threadIdx.x + u * OLA_T;
         if (t < t1) y[t] = acc[u] * adsr_at(r, t);
-    }
-}
-
-// ---------------------------------------------------------------------------
-// Stereo (even n: exact 25-tap Bessel FIR form of the spectral rotation),
-// tanh saturation and peak normalisation.
-// ---------------------------------------------------------------------------
-// A block handles ST_TILE frames [t0, t0+ST_TILE) of one preset; each thread
-// owns runs of 4 consecutive frames.  The right-channel window
-// y[(t0 + dr - 24 + u) mod n], u < ST_TILE + 48, is staged in LDS with
-// coalesced loads; a run's 25-tap outputs then need 13 ds_read_b128 of the
-// window instead of 100 scalar reads (the kernels were LDS-issue bound).
-// L[t] = y[(t - dl) mod n] is staged the same way in k_stereo_out.
-constexpr int ST_RUNS = ST_TILE / (4 * ST_T);     // runs of 4 frames per thread
-static_assert(ST_TILE >= 4 * ST_T && ST_TILE % (4 * ST_T) == 0,
-              "MSG_ST_TILE must be a multiple of 4 * ST_T (every frame of a tile has a run)");
-static_assert((2 * ST_TILE + 48) * 4 <= 160 * 1024, "MSG_ST_TILE: stereo tile window exceeds the 160 KiB LDS of a CU");
-constexpr int ST_WIN = ST_TILE + 48;
-constexpr int ST_WPER = (ST_WIN + ST_T - 1) / ST_T;
-constexpr int ST_LPER = ST_TILE / ST_T;
-
-struct StereoTile {
-    int t0, cnt;             // first frame, frames in this tile
-    int lbase;               // (t0 - dl) mod n
-};
-
-MSG_DEV int mod_n(int64_t i, int64_t n) {
-    i %= n;
-    return (int)(i < 0 ? i + n : i);
-}
-
-// Stage len floats y[(b0 + u) mod n] into w[0 .. len): coalesced loads into
-// registers (stereo_load), then LDS stores (stereo_store), split so that a
-// kernel can have every global load of its tile in flight before the first
-// store waits on them.
-template <int PER>
-MSG_DEV void stereo_load(const float* __restrict__ y, int n, int b0, int len, float (&v)[PER]) {
-    if (b0 + len <= n) {                       // no wrap (nearly every tile): one base, 32-bit offsets
-        const float* yb = y + b0;
-#pragma unroll
-        for (int i = 0; i < PER; ++i) {
-            const int u = threadIdx.x + i * ST_T;
-            v[i] = u < len ? at32(yb, (uint32_t)u) : 0.f;
-        }
-    } else if (n >= len) {                     // one wrap at most
-#pragma unroll
-        for (int i = 0; i < PER; ++i) {
-            const int u = threadIdx.x + i * ST_T;
-            int j = b0 + u;
-            if (j >= n) j -= n;
-            v[i] = u < len ? at32(y, (uint32_t)j) : 0.f;
-        }
-    } else {
-#pragma unroll
-        for (int i = 0; i < PER; ++i) {
-            const int u = threadIdx.x + i * ST_T;
-            v[i] = u < len ? y[(b0 + u) % n] : 0.f;
-        }
-    }
-}
-template <int PER>
-MSG_DEV void stereo_store(int len, const float (&v)[PER], float* w) {
-#pragma unroll
-    for (int i = 0; i < PER; ++i) {
-        const int u = threadIdx.x + i * ST_T;
-        if (u < len) w[u] = v[i];
-    }
-}
-
-MSG_DEV StereoTile stereo_tile(const PresetRt& r, int64_t t0) {
-    const int n = (int)r.out_n;
-    StereoTile st;
-    st.t0 = (int)t0;
-    st.cnt = (int)(t0 + ST_TILE < n ? ST_TILE : n - t0);
-    st.lbase = mod_n(t0 - r.dl, n);
-    return st;
-}
-
-// R[u + k] = sum_m J_m w[u + k + 2m], k < 4, u a multiple of 4 (same fma order as the
-// reference-checked scalar form: m = 0 .. 24); x receives w[u .. u + 52).
-MSG_DEV void stereo_r4(const PresetRt& r, const float* w, int u, float (&R)[4], float (&x)[52]) {
-    const float4* w4 = reinterpret_cast<const float4*>(w + u);
-#pragma unroll
-    for (int i = 0; i < 13; ++i) {
-        const float4 q = w4[i];
-        x[4 * i] = q.x; x[4 * i + 1] = q.y; x[4 * i + 2] = q.z; x[4 * i + 3] = q.w;
-    }
-    // outputs (u, u+1) and (u+2, u+3) as packed pairs: the pair (x[k+2m], x[k+1+2m])
-    // is one aligned register pair, so each tap is one v_pk_fma per pair
-    typedef float f2 __attribute__((ext_vector_type(2)));
-    f2 a01 = f2{0.f, 0.f}, a23 = f2{0.f, 0.f};
-#pragma unroll
-    for (int m = 0; m < 25; ++m) {
-        const f2 b = f2{r.bess[m], r.bess[m]};
-        a01 = __builtin_elementwise_fma(b, f2{x[2 * m], x[2 * m + 1]}, a01);
-        a23 = __builtin_elementwise_fma(b, f2{x[2 * m + 2], x[2 * m + 3]}, a23);
-    }
-    R[0] = a01.x; R[1] = a01.y; R[2] = a23.x; R[3] = a23.y;
-}
-
-// max|L|, |R| of one tile of preset p into maxbits[p]; with stats, also
-// sum y^2 and sum (1 + (d y)^2)^-2 over the tile's frames into stats[2p ..]
-// (the float64 FIR's error predictor, kernels_fir64.h).
-MSG_DEV void stereo_max_tile(const PresetRt& r, int p, int tile, const float* __restrict__ ybuf,
-                             const float* __restrict__ rbuf, unsigned* __restrict__ maxbits, double* __restrict__ stats,
-                             bool with_r2, float* w, float* wm) {
-    const float* y = ybuf + r.y_off;
-    const int n = (int)r.out_n;
-    const StereoTile st = stereo_tile(r, (int64_t)tile * ST_TILE);
-    // max|L| over all frames equals max|y| (L is a rotation of y).  With the
-    // Bessel FIR, the centre tap of output u + k is y[(t0 + u + k + dr) mod n]:
-    // over all tiles those cover every sample once, so max|y| comes from the
-    // staged window; otherwise read y directly (16-byte aligned regions, t0 a
-    // multiple of ST_TILE).
-    const bool fir = r.stereo_fir == 1;
-    float4 yv[ST_RUNS];
-    if (fir) {
-        float wv[ST_WPER];
-        stereo_load<ST_WPER>(y, n, mod_n((int64_t)st.t0 + r.dr - 24, n), ST_WIN, wv);
-        stereo_store<ST_WPER>(ST_WIN, wv, w);
-    } else {
-#pragma unroll
-        for (int i = 0; i < ST_RUNS; ++i) {
-            const int u = 4 * (threadIdx.x + i * ST_T);
-            if (u + 4 <= st.cnt) {
-                yv[i] = *reinterpret_cast<const float4*>(y + st.t0 + u);
-            } else {
-                yv[i].x = u < st.cnt ? y[st.t0 + u] : 0.f;
-                yv[i].y = u + 1 < st.cnt ? y[st.t0 + u + 1] : 0.f;
-                yv[i].z = u + 2 < st.cnt ? y[st.t0 + u + 2] : 0.f;
-                yv[i].w = 0.f;
-            }
-        }
-    }
-    __syncthreads();
-    const float d = r.drive > 0.f ? r.drive : 0.f;
-    float m = 0.f, s2 = 0.f, sq = 0.f;
-    auto stat = [&](float v) {
-        const float u = d * v;
-        const float q = __builtin_amdgcn_rcpf(fmaf(u, u, 1.f));
-        s2 = fmaf(v, v, s2);
-        sq = fmaf(q, q, sq);
-    };
-#pragma unroll
-    for (int i = 0; i < ST_RUNS; ++i) {
-        const int u = 4 * (threadIdx.x + i * ST_T);
-        if (fir) {
-            if (u < st.cnt) {
-                float R[4], x[52];
-                stereo_r4(r, w, u, R, x);
-#pragma unroll
-                for (int k = 0; k < 4; ++k)
-                    if (u + k < st.cnt) {
-                        m = fmaxf(m, fmaxf(fabsf(R[k]), fabsf(x[k + 24])));
-                        if (stats) stat(x[k + 24]);
-                    }
-            }
-            continue;
-        }
-        m = fmaxf(m, fmaxf(fmaxf(fabsf(yv[i].x), fabsf(yv[i].y)), fmaxf(fabsf(yv[i].z), fabsf(yv[i].w))));
-        if (stats) {
-            if (u < st.cnt) stat(yv[i].x);
-            if (u + 1 < st.cnt) stat(yv[i].y);
-            if (u + 2 < st.cnt) stat(yv[i].z);
-            if (u + 3 < st.cnt) stat(yv[i].w);
-        }
-        if (r.stereo_fir == 2 && with_r2) {
-#pragma unroll
-            for (int k = 0; k < 4; ++k)
-                if (u + k < st.cnt) m = fmaxf(m, fabsf(rbuf[r.r2_off + st.t0 + u + k]));
-        }
-    }
-    for (int off = 32; off > 0; off >>= 1) m = fmaxf(m, __shfl_xor(m, off));
-    if (stats)
-        for (int off = 32; off > 0; off >>= 1) { s2 += __shfl_xor(s2, off); sq += __shfl_xor(sq, off); }
-    if ((threadIdx.x & 63) == 0) {
-        wm[threadIdx.x >> 6] = m;
-        wm[ST_T / 64 + (threadIdx.x >> 6)] = s2;
-        wm[2 * (ST_T / 64) + (threadIdx.x >> 6)] = sq;
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        float v = wm[0];
-        for (int k = 1; k < ST_T / 64; ++k) v = fmaxf(v, wm[k]);
-        atomicMax(maxbits + p, __float_as_uint(v));
-        if (stats) {
-            double a = 0.0, b = 0.0;
-            for (int k = 0; k < ST_T / 64; ++k) { a += (double)wm[ST_T / 64 + k]; b += (double)wm[2 * (ST_T / 64) + k]; }
-            atomicAdd(stats + 2 * p, a);
-            atomicAdd(stats + 2 * p + 1, b);
-        }
-    }
-}
-
-__global__ void __launch_bounds__(ST_T)
-k_stereo_max(const PresetRt* __restrict__ rt, const int32_t* __restrict__ st_begin, int n_presets,
-             const float* __restrict__ ybuf, const float* __restrict__ rbuf, unsigned* __restrict__ maxbits,
-             double* __restrict__ stats, int with_r2) {
-    __shared__ __attribute__((aligned(16))) float w[ST_WIN];
-    __shared__ float wm[3 * (ST_T / 64)];
-    const int b = job_order(MSG_STMAX_REV);
-    const int p = find_preset(st_begin, n_presets, b);
-    stereo_max_tile(rt[p], p, b - st_begin[p], ybuf, rbuf, maxbits, rt[p].fir_on ? stats : nullptr, with_r2 != 0,
-                    w, wm);
-}
-
-// The float64 FIR's presets again (kernels_fir64.h): their peak from the new y.
-__global__ void __launch_bounds__(ST_T)
-k_stereo_remax(const PresetRt* __restrict__ rt, const int32_t* __restrict__ st_count,
-               const int32_t* __restrict__ slot_preset, const int32_t* __restrict__ n_slots, int tmax,
-               const float* __restrict__ ybuf, const float* __restrict__ rbuf, unsigned* __restrict__ maxbits) {
-    __shared__ __attribute__((aligned(16))) float w[ST_WIN];
-    __shared__ float wm[3 * (ST_T / 64)];
-    const int ns = *n_slots;
-    for (int j = blockIdx.x; j < ns * tmax; j += gridDim.x) {
-        const int sl = j / tmax, t = j - sl * tmax;
-        const int p = slot_preset[sl];
-        if (t >= st_count[p]) continue;                          // uniform
-        __syncthreads();
-        stereo_max_tile(rt[p], p, t, ybuf, rbuf, maxbits, nullptr, true, w, wm);
-    }
-}
-
-// tanh from the hardware exp2 and reciprocal (two transcendentals instead of the
-// library tanhf's ~30 instructions; k_stereo_out runs two per frame):
-// 1 - 2 / (e^{2|x|} + 1), |error| <= ~2 float32 ulp of 1, and an odd Taylor
-// polynomial below |x| = 0.05 where the subtraction would lose relative digits.
-// MSG_TANH_TAYLOR = 0 (tuning only) drops the polynomial: the subtraction's
-// ~1e-7 absolute error becomes a large relative one once the peak normalisation
-// scales a quiet render (drive x peak << 1) back up, and test_feedback_imprint_chain
-// fails (profiles/r03ab_stereo_ab.json).
-#ifndef MSG_TANH_TAYLOR
-#define MSG_TANH_TAYLOR 1
-#endif
-MSG_DEV float tanh_fast(float x) {
-    const float ax = fabsf(x);
-    const float e = __builtin_amdgcn_exp2f(fminf(2.8853900817779268f * ax, 126.f));   // e^{2|x|}
-    float t = 1.0f - 2.0f * __builtin_amdgcn_rcpf(e + 1.0f);
-#if MSG_TANH_TAYLOR
-    const float x2 = ax * ax;
-    if (ax < 0.05f) t = ax * fmaf(x2, fmaf(x2, 0.13333333f, -0.33333333f), 1.0f);
-#endif
-    return copysignf(t, x);
-}
-MSG_DEV float sat(float v, float d, float inv_td) { return d > 0.f ? tanh_fast(v * d) * inv_td : v; }
-// tanh_fast of an (L, R) pair in the packed form: the arithmetic runs as
-// v_pk_* pairs, the four transcendentals stay scalar (same operations and
-// rounding as tanh_fast on each lane).
-typedef float f2p __attribute__((ext_vector_type(2)));
-MSG_DEV f2p tanh_fast2(f2p x) {
-    const f2p ax = __builtin_elementwise_abs(x);
-    const f2p a = __builtin_elementwise_min(2.8853900817779268f * ax, f2p{126.f, 126.f});
-    const f2p e1 = f2p{__builtin_amdgcn_exp2f(a.x), __builtin_amdgcn_exp2f(a.y)} + 1.0f;
-    const f2p r = f2p{__builtin_amdgcn_rcpf(e1.x), __builtin_amdgcn_rcpf(e1.y)};
-    f2p t = 1.0f - 2.0f * r;
-#if MSG_TANH_TAYLOR
-    const f2p x2 = ax * ax;
-    const f2p tp = ax * __builtin_elementwise_fma(x2, __builtin_elementwise_fma(x2, f2p{0.13333333f, 0.13333333f},
-                                                                                f2p{-0.33333333f, -0.33333333f}),
-                                                  f2p{1.0f, 1.0f});
-    t.x = ax.x < 0.05f ? tp.x : t.x;
-    t.y = ax.y < 0.05f ? tp.y : t.y;
-#endif
-    return __builtin_elementwise_copysign(t, x);
-}
-
-__global__ void __launch_bounds__(ST_T)
-k_stereo_out(const PresetRt* __restrict__ rt, const int32_t* __restrict__ st_begin, int n_presets,
-             const float* __restrict__ ybuf, const float* __restrict__ rbuf, const unsigned* __restrict__ maxbits,
-             float* __restrict__ out) {
-    __shared__ __attribute__((aligned(16))) float w[ST_WIN];
-    __shared__ __attribute__((aligned(16))) float lw[ST_TILE];
-    const int b = xcd_block(blockIdx.x, gridDim.x);
-    const int p = find_preset(st_begin, n_presets, b);
-    const PresetRt& r = rt[p];
-    const float* y = ybuf + r.y_off;
-    const int n = (int)r.out_n;
-    const StereoTile st = stereo_tile(r, (int64_t)(b - st_begin[p]) * ST_TILE);
-    {
-        float lv[ST_LPER], wv[ST_WPER];
-        stereo_load<ST_LPER>(y, n, r.stereo_fir ? st.lbase : st.t0, st.cnt, lv);
-        if (r.stereo_fir == 1) stereo_load<ST_WPER>(y, n, mod_n((int64_t)st.t0 + r.dr - 24, n), ST_WIN, wv);
-        stereo_store<ST_LPER>(st.cnt, lv, lw);
-        if (r.stereo_fir == 1) stereo_store<ST_WPER>(ST_WIN, wv, w);
-    }
-    const float d = r.drive;
-    const float inv_td = d > 0.f ? 1.0f / tanh_fast(d) : 1.f;
-    const float M = __uint_as_float(maxbits[p]);
-    const float mc = sat(M, d, inv_td);
-    const float scale = mc > 0.f ? r.peak / mc : 1.f;
-    const float k_out = inv_td * scale;                     // one multiply per channel after the tanh
-    float2* o = reinterpret_cast<float2*>(out) + r.out_off + st.t0;
-    const bool o16 = ((r.out_off + st.t0) & 1) == 0;      // float4 stores of two frames
-    __syncthreads();
-#pragma unroll
-    for (int i = 0; i < ST_RUNS; ++i) {
-        const int u = 4 * (threadIdx.x + i * ST_T);
-        if (u >= st.cnt) continue;
-        const float4 l4 = *reinterpret_cast<const float4*>(lw + u);
-        const float L[4] = {l4.x, l4.y, l4.z, l4.w};
-        float R[4];
-        if (r.stereo_fir == 1) {
-            float x[52];
-            stereo_r4(r, w, u, R, x);
-        } else {
-#pragma unroll
-            for (int k = 0; k < 4; ++k)
-                R[k] = r.stereo_fir == 2 ? (u + k < st.cnt ? rbuf[r.r2_off + st.t0 + u + k] : 0.f) : L[k];
-        }
-        float2 v[4];
-        if (d > 0.f) {
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const f2p t = tanh_fast2(f2p{L[k], R[k]} * d) * k_out;
-                v[k] = make_float2(t.x, t.y);
-            }
-        } else {
-#pragma unroll
-            for (int k = 0; k < 4; ++k) v[k] = make_float2(L[k] * scale, R[k] * scale);
-        }
-        if (o16 && u + 4 <= st.cnt) {
-            float4* o4 = reinterpret_cast<float4*>(reinterpret_cast<char*>(o) + (uint32_t)u * 8u);   // 32-bit offset
-            o4[0] = make_float4(v[0].x, v[0].y, v[1].x, v[1].y);
-            o4[1] = make_float4(v[2].x, v[2].y, v[3].x, v[3].y);
-        } else {
-#pragma unroll
-            for (int k = 0; k < 4; ++k)
-                if (u + k < st.cnt) at32(o, (uint32_t)(u + k)) = v[k];
-        }
     }
 }

@@ -9,22 +9,27 @@
 // floor of an exact-twiddle FFT is 5-7e-6 RMS there (tools/fir_error_model.py),
 // next to the 1e-5 tolerance.  Such presets get the FIR again in float64:
 //
-//   k_stereo_max (first pass) accumulates per preset sum y^2 and
-//     sum (1 + (d y)^2)^-2 (the share of samples the clip leaves in its
-//     linear range) over the float32 y;
-//   k_fir64_flag predicts the float32 error from them (eps32 rms(y) x
-//     sqrt(share) x the clip's slope and the peak scale: within 2-3x of the
-//     exact-twiddle float32 error, tools/fir_error_model.py) and gives every
-//     preset above FIR64_PRED a float64 slot, in batch order, up to the batch's
-//     slot count; their stereo peak is reset;
+//   k_stereo_fused / k_stereo_max (first pass, kernels_stereo.h) adds per
+//     preset sum y^2 and sum (1 + (d y)^2)^-2 (the share of samples the clip
+//     leaves in its linear range) over the float32 y, in tile order, predicts
+//     the float32 error from them (fir64_pred, rt.h: eps32 rms(y) x
+//     sqrt(share) x the clip's slope and the peak scale, within 2-3x of the
+//     exact-twiddle float32 error, tools/fir_error_model.py) and flags every
+//     preset above FIR64_PRED (flag64);
+//   k_fir64_flag gives every flagged preset a slot, in batch order, and resets
+//     its stereo peak;
+//   then, per window of `cap` slots (all of them at once unless their buffers
+//   would pass FIR64_WINDOW_BYTES):
 //   k_h64      h = (delta + ER) * IR in the time domain (k_h_build's tiles);
 //   k_hspec64  H_q = rfft_N(h[q P, q P + P)) in float64, N = 16384, P = N/2;
 //   k_fir64    one output block of B = N - P + 1 frames: sum_q rfft(seg_q) H_q
 //              (Q + 1 float64 transforms on the LDS engine of the grain chain)
 //              -> irfft -> y as float32 (its rounding: ~1e-8 RMS);
-// then the odd-length stereo rotation and k_stereo_max run again for the slots
-// (kernels_stereo_odd.h, k_stereo_remax) before k_stereo_out.
-//
+// then the odd-length stereo rotation and the peak pass run again for the
+// slots (kernels_stereo_odd.h, k_stereo_remax) and k_stereo_out_list writes
+// their output (k_stereo_fused deferred it).  A preset's route depends only on
+// its own render, never on the batch it shares (at most 128 slots
+// had been served, in batch order).
 // Every kernel of the chain walks a virtual (slot, unit) space in a grid-stride
 // loop and skips units of empty slots, so a batch without flagged presets (C3,
 // C4, C5, the shipped presets but wavelet_mist) pays a few microseconds.
@@ -34,61 +39,47 @@
 #include "hbuild.h"
 
 constexpr int FIR64_T = 512, FIR64_E = 16;          // the float64 LDS engine (G64_T, G64_MAXE)
-constexpr double FIR64_PRED = 5e-7;                  // predicted float32 error above which a preset takes float64
 
-// Flag kernel: one wave walks the presets 64 at a time, slots in batch order
+// Slot kernel: one wave walks the presets 64 at a time, slots in batch order
 // (a 64-thread workgroup finds a CU at once beside other streams' kernels,
 // where a 1024-thread one waited ~80 us for a free CU).
 __global__ void __launch_bounds__(64)
-k_fir64_flag(const PresetRt* __restrict__ rt, int n_presets, const double* __restrict__ stats,
-             unsigned* __restrict__ maxbits, int32_t* __restrict__ slot_of, int32_t* __restrict__ slot_preset,
-             int32_t* __restrict__ n_slots, int cap, int force) {
+k_fir64_flag(int n_presets, const int32_t* __restrict__ flag64, unsigned* __restrict__ maxbits,
+             int32_t* __restrict__ slot_preset, int32_t* __restrict__ n_slots) {
     const int lane = (int)threadIdx.x;
     int base = 0;
     for (int p0 = 0; p0 < n_presets; p0 += 64) {
         const int p = p0 + lane;
-        bool f = false;
-        if (p < n_presets) {
-            const PresetRt& r = rt[p];
-            slot_of[p] = -1;
-            if (r.fir_on) {
-                const double n = (double)r.out_n;
-                const double d = (double)r.drive;
-                const double rms = sqrt(stats[2 * p] / n), share = stats[2 * p + 1] / n;
-                // the clip's slope at 0 and the peak scale of the render (MS:26-34)
-                const double M = (double)__uint_as_float(maxbits[p]);
-                double slope = 1.0, mc = M;
-                if (d > 0.0) { slope = d / tanh(d); mc = tanh(M * d) / tanh(d); }
-                const double scale = mc > 0.0 ? (double)r.peak / mc : 1.0;
-                const double pred = 5.9604644775390625e-8 * rms * sqrt(share) * slope * scale;
-                f = force || pred > FIR64_PRED;
-            }
-        }
+        const bool f = p < n_presets && flag64[p] != 0;
         const uint64_t bal = __ballot(f);
-        const int before = base + __popcll(bal & ((1ULL << lane) - 1));
-        if (f && before < cap) {
-            slot_of[p] = before;
-            slot_preset[before] = p;
+        if (f) {
+            slot_preset[base + __popcll(bal & ((1ULL << lane) - 1))] = p;
             maxbits[p] = 0u;                               // k_stereo_remax takes the float64 y's peak
         }
         base += __popcll(bal);
     }
-    if (lane == 0) *n_slots = base < cap ? base : cap;
+    if (lane == 0) *n_slots = base;
+}
+
+// slots of the window [w0, w0 + cap)
+MSG_DEV int fir64_window(const int32_t* __restrict__ n_slots, int w0, int cap) {
+    const int ns = *n_slots - w0;
+    return ns < cap ? ns : cap;
 }
 
 // h of the slots' presets (k_h_build's tile, float64 sums, float32 taps).
 __global__ void __launch_bounds__(H_T)
 k_h64(const PresetRt* __restrict__ rt, const Fir64Rt* __restrict__ fr, const int32_t* __restrict__ slot_preset,
-      const int32_t* __restrict__ n_slots, int tmax, const int32_t* __restrict__ er_off,
+      const int32_t* __restrict__ n_slots, int w0, int cap, int tmax, const int32_t* __restrict__ er_off,
       const double* __restrict__ er_gain, const double* __restrict__ ir_bank, float* __restrict__ h64,
       int64_t h_stride) {
     __shared__ float irp[H_IRMAX + 2 * H_TILE];
     __shared__ int32_t s_off[H_T];
     __shared__ double s_g[H_T];
-    const int ns = *n_slots;
+    const int ns = fir64_window(n_slots, w0, cap);
     for (int j = blockIdx.x; j < ns * tmax; j += gridDim.x) {
         const int sl = j / tmax, t = j - sl * tmax;
-        const int p = slot_preset[sl];
+        const int p = slot_preset[w0 + sl];
         if (t * H_TILE >= fr[p].h_len) continue;               // uniform
         __syncthreads();
         h_build_tile(rt[p], fr[p].h_len, t * H_TILE, er_off, er_gain, ir_bank, irp, s_off, s_g,
@@ -99,15 +90,15 @@ k_h64(const PresetRt* __restrict__ rt, const Fir64Rt* __restrict__ fr, const int
 // H_q = rfft_N(h[q P, q P + P) zero-padded) in float64, one (slot, q) per pass.
 __global__ void __launch_bounds__(FIR64_T)
 k_hspec64(const Fir64Rt* __restrict__ fr, const Real64Plan* __restrict__ plans, int plan,
-          const int32_t* __restrict__ slot_preset, const int32_t* __restrict__ n_slots, int qmax,
+          const int32_t* __restrict__ slot_preset, const int32_t* __restrict__ n_slots, int w0, int cap, int qmax,
           const float* __restrict__ h64, int64_t h_stride, double2* __restrict__ hs64, int64_t hs_stride) {
     extern __shared__ __attribute__((aligned(16))) double2 buf[];
     const Real64Plan& rp = plans[plan];
     double* d = reinterpret_cast<double*>(buf);
-    const int ns = *n_slots;
+    const int ns = fir64_window(n_slots, w0, cap);
     for (int j = blockIdx.x; j < ns * qmax; j += gridDim.x) {
         const int sl = j / qmax, q = j - sl * qmax;
-        const int p = slot_preset[sl];
+        const int p = slot_preset[w0 + sl];
         const int hl = fr[p].h_len;
         if (q >= fr[p].q) continue;
         const float* h = h64 + (int64_t)sl * h_stride + (int64_t)q * FIR64_P;
@@ -125,18 +116,18 @@ k_hspec64(const Fir64Rt* __restrict__ fr, const Real64Plan* __restrict__ plans, 
 // partitions, the spectrum sum held per thread in registers (bins tid + i T).
 __global__ void __launch_bounds__(FIR64_T)
 k_fir64(const PresetRt* __restrict__ rt, const Fir64Rt* __restrict__ fr, const Real64Plan* __restrict__ plans,
-        int plan, const int32_t* __restrict__ slot_preset, const int32_t* __restrict__ n_slots, int bmax,
+        int plan, const int32_t* __restrict__ slot_preset, const int32_t* __restrict__ n_slots, int w0, int cap, int bmax,
         const double2* __restrict__ hs64, int64_t hs_stride, const float* __restrict__ x_in,
         float* __restrict__ y_out) {
     extern __shared__ __attribute__((aligned(16))) double2 buf[];
     const Real64Plan& rp = plans[plan];
     double* d = reinterpret_cast<double*>(buf);
-    const int ns = *n_slots;
+    const int ns = fir64_window(n_slots, w0, cap);
     constexpr int NE = (FIR64_K + FIR64_T - 1) / FIR64_T;
     static_assert(NE <= FIR64_E + 1, "bins per thread");
     for (int j = blockIdx.x; j < ns * bmax; j += gridDim.x) {
         const int sl = j / bmax, b = j - sl * bmax;
-        const int p = slot_preset[sl];
+        const int p = slot_preset[w0 + sl];
         const Fir64Rt f = fr[p];
         if (b >= f.blocks) continue;
         const PresetRt& r = rt[p];

@@ -1,0 +1,606 @@
+// kernels_stereo.h — stereo diffusion (MS:423-436), tanh saturation and peak
+// normalisation (MS:26-34, 775-781) of the mono FIR output (TU: k_stereo.hip).
+//
+// Two passes over y per preset: the peak max(|L|, |R|) over every frame, then
+// the clipped, normalised (L, R) pairs.  k_stereo_fused (the render path since
+// round 5) runs both in one persistent launch: workgroups take max-pass tiles
+// in batch order from one counter and later run the output pass of the same
+// tiles, once the tile's preset is complete (the last of its tiles to finish
+// publishes the peak), so the output pass re-reads y while it is still in the
+// XCD's L2 or the Infinity Cache -- HBM moves 4 + 8 B per frame instead of the
+// 4 + 4 + 8 of two launches (C3's 537 MB of y per 341-preset sub-batch outlive
+// the 256 MB cache between two launches).
+// k_stereo_max + k_stereo_out are the two-launch form (MSGPU_STEREO_FUSED=0).
+//
+// The float64 FIR's error predictor (kernels_fir64.h) needs per preset sum y^2
+// and sum (1 + (d y)^2)^-2: each tile stores its two partial sums, and the
+// preset's last tile adds them in tile order (so the sums and the route decision
+// do not depend on which tile finished last), decides the route (flag64) and
+// marks flagged and odd-length presets deferred: their output tiles are written
+// after the float64 FIR / the odd rotation by k_stereo_out_list.
+#pragma once
+#include "rt.h"
+
+// ---------------------------------------------------------------------------
+// Tiles
+// ---------------------------------------------------------------------------
+// A block handles ST_TILE frames [t0, t0+ST_TILE) of one preset; each thread
+// owns runs of 4 consecutive frames.  The right-channel window
+// y[(t0 + dr - 24 + u) mod n], u < ST_TILE + 48, is staged in LDS with
+// coalesced loads; a run's 25-tap outputs then need 13 ds_read_b128 of the
+// window instead of 100 scalar reads (the kernels were LDS-issue bound).
+// L[t] = y[(t - dl) mod n] is staged the same way in k_stereo_out.
+constexpr int ST_RUNS = ST_TILE / (4 * ST_T);     // runs of 4 frames per thread
+static_assert(ST_TILE >= 4 * ST_T && ST_TILE % (4 * ST_T) == 0,
+              "MSG_ST_TILE must be a multiple of 4 * ST_T (every frame of a tile has a run)");
+static_assert((2 * ST_TILE + 48) * 4 <= 160 * 1024, "MSG_ST_TILE: stereo tile window exceeds the 160 KiB LDS of a CU");
+constexpr int ST_WIN = ST_TILE + 48;
+constexpr int ST_WPER = (ST_WIN + ST_T - 1) / ST_T;
+constexpr int ST_LPER = ST_TILE / ST_T;
+
+struct StereoTile {
+    int t0, cnt;             // first frame, frames in this tile
+    int lbase;               // (t0 - dl) mod n
+};
+
+MSG_DEV int mod_n(int64_t i, int64_t n) {
+    i %= n;
+    return (int)(i < 0 ? i + n : i);
+}
+
+// threadIdx.x behind an empty asm: the kernels that loop over tiles
+// (k_stereo_fused, the list kernels) would otherwise keep every tile-invariant
+// per-thread address (33 window slots, the runs' LDS and output offsets) live
+// across the loop -- 175-188 VGPRs, or spills at 128; recomputed per tile they
+// cost a few VALU and the loops fit k_stereo_out's register budget.
+MSG_DEV int st_tid() {
+    int t = (int)threadIdx.x;
+    asm volatile("" : "+v"(t));
+    return t;
+}
+
+// Stage len floats y[(b0 + u) mod n] into w[0 .. len): coalesced loads into
+// registers (stereo_load), then LDS stores (stereo_store), split so that a
+// kernel can have every global load of its tile in flight before the first
+// store waits on them.
+template <int PER>
+MSG_DEV void stereo_load(const float* __restrict__ y, int n, int b0, int len, float (&v)[PER]) {
+    const int tid = st_tid();
+    if (b0 + len <= n) {                       // no wrap (nearly every tile): one base, 32-bit offsets
+        const float* yb = y + b0;
+#pragma unroll
+        for (int i = 0; i < PER; ++i) {
+            const int u = tid + i * ST_T;
+            v[i] = u < len ? at32(yb, (uint32_t)u) : 0.f;
+        }
+    } else if (n >= len) {                     // one wrap at most
+#pragma unroll
+        for (int i = 0; i < PER; ++i) {
+            const int u = tid + i * ST_T;
+            int j = b0 + u;
+            if (j >= n) j -= n;
+            v[i] = u < len ? at32(y, (uint32_t)j) : 0.f;
+        }
+    } else {
+#pragma unroll
+        for (int i = 0; i < PER; ++i) {
+            const int u = tid + i * ST_T;
+            v[i] = u < len ? y[(b0 + u) % n] : 0.f;
+        }
+    }
+}
+template <int PER>
+MSG_DEV void stereo_store(int len, const float (&v)[PER], float* w) {
+    const int tid = st_tid();
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+        const int u = tid + i * ST_T;
+        if (u < len) w[u] = v[i];
+    }
+}
+
+MSG_DEV StereoTile stereo_tile(const PresetRt& r, int64_t t0) {
+    const int n = (int)r.out_n;
+    StereoTile st;
+    st.t0 = (int)t0;
+    st.cnt = (int)(t0 + ST_TILE < n ? ST_TILE : n - t0);
+    st.lbase = mod_n(t0 - r.dl, n);
+    return st;
+}
+
+// R[u + k] = sum_m J_m w[u + k + 2m], k < 4, u a multiple of 4 (same fma order as the
+// reference-checked scalar form: m = 0 .. 24); x receives w[u .. u + 52).
+MSG_DEV void stereo_r4(const PresetRt& r, const float* w, int u, float (&R)[4], float (&x)[52]) {
+    const float4* w4 = reinterpret_cast<const float4*>(w + u);
+#pragma unroll
+    for (int i = 0; i < 13; ++i) {
+        const float4 q = w4[i];
+        x[4 * i] = q.x; x[4 * i + 1] = q.y; x[4 * i + 2] = q.z; x[4 * i + 3] = q.w;
+    }
+    // outputs (u, u+1) and (u+2, u+3) as packed pairs: the pair (x[k+2m], x[k+1+2m])
+    // is one aligned register pair, so each tap is one v_pk_fma per pair
+    typedef float f2 __attribute__((ext_vector_type(2)));
+    f2 a01 = f2{0.f, 0.f}, a23 = f2{0.f, 0.f};
+#pragma unroll
+    for (int m = 0; m < 25; ++m) {
+        const f2 b = f2{r.bess[m], r.bess[m]};
+        a01 = __builtin_elementwise_fma(b, f2{x[2 * m], x[2 * m + 1]}, a01);
+        a23 = __builtin_elementwise_fma(b, f2{x[2 * m + 2], x[2 * m + 3]}, a23);
+    }
+    R[0] = a01.x; R[1] = a01.y; R[2] = a23.x; R[3] = a23.y;
+}
+
+// tanh from the hardware exp2 and reciprocal (two transcendentals instead of the
+// library tanhf's ~30 instructions; k_stereo_out runs two per frame):
+// 1 - 2 / (e^{2|x|} + 1), |error| <= ~2 float32 ulp of 1, and an odd Taylor
+// polynomial below |x| = 0.05 where the subtraction would lose relative digits.
+// MSG_TANH_TAYLOR = 0 (tuning only) drops the polynomial: the subtraction's
+// ~1e-7 absolute error becomes a large relative one once the peak normalisation
+// scales a quiet render (drive x peak << 1) back up, and test_feedback_imprint_chain
+// fails (profiles/r03ab_stereo_ab.json).
+#ifndef MSG_TANH_TAYLOR
+#define MSG_TANH_TAYLOR 1
+#endif
+MSG_DEV float tanh_fast(float x) {
+    const float ax = fabsf(x);
+    const float e = __builtin_amdgcn_exp2f(fminf(2.8853900817779268f * ax, 126.f));   // e^{2|x|}
+    float t = 1.0f - 2.0f * __builtin_amdgcn_rcpf(e + 1.0f);
+#if MSG_TANH_TAYLOR
+    const float x2 = ax * ax;
+    if (ax < 0.05f) t = ax * fmaf(x2, fmaf(x2, 0.13333333f, -0.33333333f), 1.0f);
+#endif
+    return copysignf(t, x);
+}
+MSG_DEV float sat(float v, float d, float inv_td) { return d > 0.f ? tanh_fast(v * d) * inv_td : v; }
+// tanh_fast of an (L, R) pair in the packed form: the arithmetic runs as
+// v_pk_* pairs, the four transcendentals stay scalar (same operations and
+// rounding as tanh_fast on each lane).
+typedef float f2p __attribute__((ext_vector_type(2)));
+MSG_DEV f2p tanh_fast2(f2p x) {
+    const f2p ax = __builtin_elementwise_abs(x);
+    const f2p a = __builtin_elementwise_min(2.8853900817779268f * ax, f2p{126.f, 126.f});
+    const f2p e1 = f2p{__builtin_amdgcn_exp2f(a.x), __builtin_amdgcn_exp2f(a.y)} + 1.0f;
+    const f2p r = f2p{__builtin_amdgcn_rcpf(e1.x), __builtin_amdgcn_rcpf(e1.y)};
+    f2p t = 1.0f - 2.0f * r;
+#if MSG_TANH_TAYLOR
+    const f2p x2 = ax * ax;
+    const f2p tp = ax * __builtin_elementwise_fma(x2, __builtin_elementwise_fma(x2, f2p{0.13333333f, 0.13333333f},
+                                                                                f2p{-0.33333333f, -0.33333333f}),
+                                                  f2p{1.0f, 1.0f});
+    t.x = ax.x < 0.05f ? tp.x : t.x;
+    t.y = ax.y < 0.05f ? tp.y : t.y;
+#endif
+    return __builtin_elementwise_copysign(t, x);
+}
+
+MSG_DEV int job_order_st() { return xcd_block(blockIdx.x, gridDim.x); }
+
+constexpr int ST_EXIT = INT32_MIN;
+
+MSG_DEV int st_rfl(int v) { return __builtin_amdgcn_readfirstlane(v); }
+
+// Cross-workgroup hand-off without agent-scope fences.  Every value another
+// workgroup reads in this launch (tile peaks, partial sums, counters, the ready
+// word) is written and read with agent-scope atomics, which gfx950 performs at
+// the coherence point past the XCDs' L2s; what orders a producer's writes
+// before its hand-off is this drain -- all of the wave's memory operations
+// acknowledged (s_waitcnt 0; the signal fences keep the compiler from moving
+// the atomics across it).  An agent-scope release / acquire fence would write
+// back / invalidate the whole XCD L2 per tile (buffer_wbl2 / buffer_inv): the
+// first build did so and ran C3's stereo pass in 486 ms instead of ~1.5.
+MSG_DEV void st_drain() {
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    __builtin_amdgcn_s_waitcnt(0);
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+}
+
+// max|L|, |R| of one tile, returned to thread 0; with part, also the tile's
+// sum y^2 and sum (1 + (d y)^2)^-2 into part[0], part[1] (the float64 FIR's
+// error predictor, kernels_fir64.h).  Consecutive calls need no barrier
+// between them (every read of w precedes the barrier before wm is read).
+MSG_DEV float stereo_max_vals(const PresetRt& r, int tile, const float* __restrict__ ybuf,
+                              const float* __restrict__ rbuf, double* __restrict__ part, bool with_r2, float* w,
+                              float* wm) {
+    const float* y = ybuf + r.y_off;
+    const int n = (int)r.out_n;
+    const StereoTile st = stereo_tile(r, (int64_t)tile * ST_TILE);
+    const int tid = st_tid();
+    // max|L| over all frames equals max|y| (L is a rotation of y).  With the
+    // Bessel FIR, the centre tap of output u + k is y[(t0 + u + k + dr) mod n]:
+    // over all tiles those cover every sample once, so max|y| comes from the
+    // staged window; otherwise read y directly (16-byte aligned regions, t0 a
+    // multiple of ST_TILE).
+    const bool fir = r.stereo_fir == 1;
+    float4 yv[ST_RUNS];
+    if (fir) {
+        float wv[ST_WPER];
+        stereo_load<ST_WPER>(y, n, mod_n((int64_t)st.t0 + r.dr - 24, n), ST_WIN, wv);
+        stereo_store<ST_WPER>(ST_WIN, wv, w);
+    } else {
+#pragma unroll
+        for (int i = 0; i < ST_RUNS; ++i) {
+            const int u = 4 * (tid + i * ST_T);
+            if (u + 4 <= st.cnt) {
+                yv[i] = *reinterpret_cast<const float4*>(y + st.t0 + u);
+            } else {
+                yv[i].x = u < st.cnt ? y[st.t0 + u] : 0.f;
+                yv[i].y = u + 1 < st.cnt ? y[st.t0 + u + 1] : 0.f;
+                yv[i].z = u + 2 < st.cnt ? y[st.t0 + u + 2] : 0.f;
+                yv[i].w = 0.f;
+            }
+        }
+    }
+    __syncthreads();
+    const float d = r.drive > 0.f ? r.drive : 0.f;
+    float m = 0.f, s2 = 0.f, sq = 0.f;
+    auto stat = [&](float v) {
+        const float u = d * v;
+        const float q = __builtin_amdgcn_rcpf(fmaf(u, u, 1.f));
+        s2 = fmaf(v, v, s2);
+        sq = fmaf(q, q, sq);
+    };
+#pragma unroll
+    for (int i = 0; i < ST_RUNS; ++i) {
+        const int u = 4 * (tid + i * ST_T);
+        if (fir) {
+            if (u < st.cnt) {
+                float R[4], x[52];
+                stereo_r4(r, w, u, R, x);
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    if (u + k < st.cnt) {
+                        m = fmaxf(m, fmaxf(fabsf(R[k]), fabsf(x[k + 24])));
+                        if (part) stat(x[k + 24]);
+                    }
+            }
+            continue;
+        }
+        m = fmaxf(m, fmaxf(fmaxf(fabsf(yv[i].x), fabsf(yv[i].y)), fmaxf(fabsf(yv[i].z), fabsf(yv[i].w))));
+        if (part) {
+            if (u < st.cnt) stat(yv[i].x);
+            if (u + 1 < st.cnt) stat(yv[i].y);
+            if (u + 2 < st.cnt) stat(yv[i].z);
+            if (u + 3 < st.cnt) stat(yv[i].w);
+        }
+        if (r.stereo_fir == 2 && with_r2) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                if (u + k < st.cnt) m = fmaxf(m, fabsf(rbuf[r.r2_off + st.t0 + u + k]));
+        }
+    }
+    for (int off = 32; off > 0; off >>= 1) m = fmaxf(m, __shfl_xor(m, off));
+    if (part)
+        for (int off = 32; off > 0; off >>= 1) { s2 += __shfl_xor(s2, off); sq += __shfl_xor(sq, off); }
+    if ((threadIdx.x & 63) == 0) {
+        wm[threadIdx.x >> 6] = m;
+        wm[ST_T / 64 + (threadIdx.x >> 6)] = s2;
+        wm[2 * (ST_T / 64) + (threadIdx.x >> 6)] = sq;
+    }
+    __syncthreads();
+    float v = 0.f;
+    if (threadIdx.x == 0) {
+        v = wm[0];
+        for (int k = 1; k < ST_T / 64; ++k) v = fmaxf(v, wm[k]);
+        if (part) {
+            double a = 0.0, b = 0.0;
+            for (int k = 0; k < ST_T / 64; ++k) { a += (double)wm[ST_T / 64 + k]; b += (double)wm[2 * (ST_T / 64) + k]; }
+            __hip_atomic_store(part, a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(part + 1, b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+    return v;
+}
+
+// max|L|, |R| of one tile of preset p into maxbits[p] (and part as above)
+MSG_DEV void stereo_max_tile(const PresetRt& r, int p, int tile, const float* __restrict__ ybuf,
+                             const float* __restrict__ rbuf, unsigned* __restrict__ maxbits, double* __restrict__ part,
+                             bool with_r2, float* w, float* wm) {
+    const float v = stereo_max_vals(r, tile, ybuf, rbuf, part, with_r2, w, wm);
+    if (threadIdx.x == 0) atomicMax(maxbits + p, __float_as_uint(v));
+}
+
+// After the max pass of `add` tiles of preset p (every thread; thread 0 holds
+// their peak run_max and stored their partials): the peak into maxbits[p],
+// then the tiles are counted; the workgroup that counts the preset's last tile
+// adds the partial sums of tiles [tile0, tile0 + cnt) in tile order, decides the
+// float64 route, resets the count and publishes the preset as ready.
+// s_last / s_red: LDS.
+MSG_DEV void stereo_run_done(const PresetRt& r, int p, int tile0, int cnt, int add, float run_max,
+                             unsigned* __restrict__ maxbits, const StereoSync& sy, int* s_last, double* s_red) {
+    if (threadIdx.x == 0) {
+        atomicMax(maxbits + p, __float_as_uint(run_max));
+        st_drain();                                        // the peak and partials before the count
+        *s_last = atomicAdd(sy.done + p, add) + add == cnt;
+    }
+    __syncthreads();
+    if (!*s_last) return;                                  // uniform
+    const bool st = sy.part != nullptr && r.fir_on;
+    double a = 0.0, b = 0.0;
+    if (st) {
+        for (int i = threadIdx.x; i < cnt; i += ST_T) {    // fixed order: tile i, i + ST_T, ...
+            a += __hip_atomic_load(sy.part + 2 * (tile0 + i), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            b += __hip_atomic_load(sy.part + 2 * (tile0 + i) + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        for (int off = 32; off > 0; off >>= 1) { a += __shfl_xor(a, off); b += __shfl_xor(b, off); }
+        if ((threadIdx.x & 63) == 0) {
+            s_red[threadIdx.x >> 6] = a;
+            s_red[ST_T / 64 + (threadIdx.x >> 6)] = b;
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        int f = 0;
+        if (st) {
+            a = s_red[0];
+            b = s_red[ST_T / 64];
+            for (int k = 1; k < ST_T / 64; ++k) { a += s_red[k]; b += s_red[ST_T / 64 + k]; }
+            sy.stats[2 * p] = a;
+            sy.stats[2 * p + 1] = b;
+            const unsigned mb = __hip_atomic_load(maxbits + p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            f = (sy.f64mode >= 2 || fir64_pred(r, a, b, mb) > FIR64_PRED) ? 1 : 0;
+        }
+        if (sy.flag64) sy.flag64[p] = f;
+        __hip_atomic_store(sy.done + p, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t defer = (f || r.stereo_fir == 2) ? 1u : 0u;
+        st_drain();                                        // stats, flag64 and the reset first
+        __hip_atomic_store(sy.ready + p, (sy.epoch << 1) | defer, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
+MSG_DEV int st_tiles_of(const int32_t* __restrict__ st_begin, int n_presets, int n_tiles, int p) {
+    return (p + 1 < n_presets ? st_begin[p + 1] : n_tiles) - st_begin[p];
+}
+
+__global__ void __launch_bounds__(ST_T)
+k_stereo_max(const PresetRt* __restrict__ rt, const int32_t* __restrict__ st_begin, int n_presets, int n_tiles,
+             const float* __restrict__ ybuf, unsigned* __restrict__ maxbits, StereoSync sy) {
+    __shared__ __attribute__((aligned(16))) float w[ST_WIN];
+    __shared__ float wm[3 * (ST_T / 64)];
+    __shared__ double s_red[2 * (ST_T / 64)];
+    __shared__ int s_last;
+    const int b = job_order_st();
+    const int p = find_preset(st_begin, n_presets, b);
+    const PresetRt& r = rt[p];
+    const float m = stereo_max_vals(r, b - st_begin[p], ybuf, nullptr,
+                                    (sy.part && r.fir_on) ? sy.part + 2 * b : nullptr, false, w, wm);
+    stereo_run_done(r, p, st_begin[p], st_tiles_of(st_begin, n_presets, n_tiles, p), 1, m, maxbits, sy, &s_last, s_red);
+}
+
+// The float64 FIR's presets again (kernels_fir64.h) and the odd-length presets
+// (R from the rotation): their peak from the final y and R.
+__global__ void __launch_bounds__(ST_T) __attribute__((amdgpu_waves_per_eu(4)))
+k_stereo_remax(const PresetRt* __restrict__ rt, const int32_t* __restrict__ st_count,
+               const int32_t* __restrict__ slot_preset, const int32_t* __restrict__ n_slots, int tmax,
+               const float* __restrict__ ybuf, const float* __restrict__ rbuf, unsigned* __restrict__ maxbits) {
+    __shared__ __attribute__((aligned(16))) float w[ST_WIN];
+    __shared__ float wm[3 * (ST_T / 64)];
+    const int ns = *n_slots;
+    for (int j = blockIdx.x; j < ns * tmax; j += gridDim.x) {
+        const int sl = j / tmax, t = j - sl * tmax;
+        const int p = st_rfl(slot_preset[sl]);
+        if (t >= st_count[p]) continue;                          // uniform
+        __syncthreads();
+        stereo_max_tile(rt[p], p, t, ybuf, rbuf, maxbits, nullptr, true, w, wm);
+    }
+}
+
+// The clipped, normalised (L, R) of one tile of preset p, peak M = the float
+// bits peak_bits (w: the R window, lw: the L window, LDS).  (L straight into
+// registers -- 16.6 KB of LDS per workgroup instead of 33 -- measured 1.64 vs
+// 1.60 ms isolated on C3: the pass is not limited by its workgroups per CU.)
+MSG_DEV void stereo_out_tile(const PresetRt& r, int tile, const float* __restrict__ ybuf, const float* __restrict__ rbuf,
+                             unsigned peak_bits, float* __restrict__ out, float* w, float* lw) {
+    const float* y = ybuf + r.y_off;
+    const int n = (int)r.out_n;
+    const StereoTile st = stereo_tile(r, (int64_t)tile * ST_TILE);
+    const int tid = st_tid();
+    {
+        float lv[ST_LPER], wv[ST_WPER];
+        stereo_load<ST_LPER>(y, n, r.stereo_fir ? st.lbase : st.t0, st.cnt, lv);
+        if (r.stereo_fir == 1) stereo_load<ST_WPER>(y, n, mod_n((int64_t)st.t0 + r.dr - 24, n), ST_WIN, wv);
+        stereo_store<ST_LPER>(st.cnt, lv, lw);
+        if (r.stereo_fir == 1) stereo_store<ST_WPER>(ST_WIN, wv, w);
+    }
+    const float d = r.drive;
+    const float inv_td = d > 0.f ? 1.0f / tanh_fast(d) : 1.f;
+    const float M = __uint_as_float(peak_bits);
+    const float mc = sat(M, d, inv_td);
+    const float scale = mc > 0.f ? r.peak / mc : 1.f;
+    const float k_out = inv_td * scale;                     // one multiply per channel after the tanh
+    float2* o = reinterpret_cast<float2*>(out) + r.out_off + st.t0;
+    const bool o16 = ((r.out_off + st.t0) & 1) == 0;      // float4 stores of two frames
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < ST_RUNS; ++i) {
+        const int u = 4 * (tid + i * ST_T);
+        if (u >= st.cnt) continue;
+        const float4 l4 = *reinterpret_cast<const float4*>(lw + u);
+        const float L[4] = {l4.x, l4.y, l4.z, l4.w};
+        float R[4];
+        if (r.stereo_fir == 1) {
+            float x[52];
+            stereo_r4(r, w, u, R, x);
+        } else {
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                R[k] = r.stereo_fir == 2 ? (u + k < st.cnt ? rbuf[r.r2_off + st.t0 + u + k] : 0.f) : L[k];
+        }
+        float2 v[4];
+        if (d > 0.f) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const f2p t = tanh_fast2(f2p{L[k], R[k]} * d) * k_out;
+                v[k] = make_float2(t.x, t.y);
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) v[k] = make_float2(L[k] * scale, R[k] * scale);
+        }
+        if (o16 && u + 4 <= st.cnt) {
+            float4* o4 = reinterpret_cast<float4*>(reinterpret_cast<char*>(o) + (uint32_t)u * 8u);   // 32-bit offset
+            o4[0] = make_float4(v[0].x, v[0].y, v[1].x, v[1].y);
+            o4[1] = make_float4(v[2].x, v[2].y, v[3].x, v[3].y);
+        } else {
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                if (u + k < st.cnt) at32(o, (uint32_t)(u + k)) = v[k];
+        }
+    }
+}
+
+__global__ void __launch_bounds__(ST_T)
+k_stereo_out(const PresetRt* __restrict__ rt, const int32_t* __restrict__ st_begin, int n_presets,
+             const float* __restrict__ ybuf, const float* __restrict__ rbuf, const unsigned* __restrict__ maxbits,
+             float* __restrict__ out) {
+    __shared__ __attribute__((aligned(16))) float w[ST_WIN];
+    __shared__ __attribute__((aligned(16))) float lw[ST_TILE];
+    const int b = job_order_st();
+    const int p = find_preset(st_begin, n_presets, b);
+    stereo_out_tile(rt[p], b - st_begin[p], ybuf, rbuf, maxbits[p], out, w, lw);
+}
+
+// The output tiles of the listed presets (the deferred ones of k_stereo_fused:
+// float64 FIR slots, odd lengths), a grid-stride walk over (entry, tile).
+__global__ void __launch_bounds__(ST_T) __attribute__((amdgpu_waves_per_eu(4)))
+k_stereo_out_list(const PresetRt* __restrict__ rt, const int32_t* __restrict__ st_count,
+                  const int32_t* __restrict__ list, const int32_t* __restrict__ n_list, int tmax,
+                  const float* __restrict__ ybuf, const float* __restrict__ rbuf, const unsigned* __restrict__ maxbits,
+                  float* __restrict__ out) {
+    __shared__ __attribute__((aligned(16))) float w[ST_WIN];
+    __shared__ __attribute__((aligned(16))) float lw[ST_TILE];
+    const int nl = *n_list;
+    for (int j = blockIdx.x; j < nl * tmax; j += gridDim.x) {
+        const int sl = j / tmax, t = j - sl * tmax;
+        const int p = st_rfl(list[sl]);
+        if (t >= st_count[p]) continue;                          // uniform
+        __syncthreads();                                         // the previous tile's LDS reads are done
+        stereo_out_tile(rt[p], t, ybuf, rbuf, maxbits[p], out, w, lw);
+    }
+}
+
+// Both passes in one persistent launch (see the header).  Jobs are chunks of
+// ST_CHUNK consecutive tiles of the batch (a chunk may span short presets): one
+// claim, one preset lookup and one count per preset run amortised over the
+// chunk (each returning atomic costs ~1 us while the chip streams,
+// MI355X_MICROARCH.md "dequeue"; per-tile jobs ran C3's pass at 3.4 ms).  A
+// workgroup owns the output pass of the chunks whose max pass it ran: wave 0
+// keeps them in a ring in LDS and picks the next job -- the oldest owned chunk
+// if the presets of its first and last tiles are ready, else the next chunk
+// from the launch's one counter, else (every chunk taken, or the ring full)
+// the oldest owned chunk, waiting for its presets.  The output pass then
+// re-reads y on the CU that just read it (its XCD's L2, else the Infinity
+// Cache).
+// Waiting cannot deadlock once every chunk is taken: each is held by a running
+// workgroup that finishes its max pass without waiting.  With the ring full,
+// all W resident workgroups could only wait together if the preset at the front
+// had 32 W ST_CHUNK claimed tiles; the host takes this launch only for presets
+// of at most ST_FUSED_MAX_TILES = 2048 tiles (C5's 8.4 M frames), so even eight
+// contexts' fused launches sharing the CUs (W >= 1024 / 8 each) cannot all
+// stall.  The last workgroup to leave resets the counters.
+constexpr int ST_RING = 32;
+#ifndef MSG_ST_CHUNK
+#define MSG_ST_CHUNK 4
+#endif
+constexpr int ST_CHUNK = MSG_ST_CHUNK;
+constexpr int ST_LDS_PRESETS = 1024;    // st_begin staged in LDS up to this many presets
+
+MSG_DEV uint32_t st_poll(const uint32_t* ready, int p) {
+    return __hip_atomic_load(ready + p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__global__ void __launch_bounds__(ST_T) __attribute__((amdgpu_waves_per_eu(4)))
+k_stereo_fused(const PresetRt* __restrict__ rt, const int32_t* __restrict__ st_begin, int n_presets, int n_tiles,
+               const float* __restrict__ ybuf, unsigned* __restrict__ maxbits, StereoSync sy,
+               int32_t* __restrict__ ctr, float* __restrict__ out) {
+    __shared__ __attribute__((aligned(16))) float w[ST_WIN];
+    __shared__ __attribute__((aligned(16))) float lw[ST_TILE];
+    __shared__ float wm[3 * (ST_T / 64)];
+    __shared__ double s_red[2 * (ST_T / 64)];
+    __shared__ int32_t s_begin[ST_LDS_PRESETS];
+    __shared__ int s_ring[ST_RING];
+    __shared__ int s_job, s_last, s_skip;
+    __shared__ unsigned s_peak;
+    const int lane = (int)(threadIdx.x & 63);
+    const bool lds_begin = n_presets <= ST_LDS_PRESETS;
+    if (lds_begin)
+        for (int i = threadIdx.x; i < n_presets; i += ST_T) s_begin[i] = st_begin[i];
+    const int32_t* beg = lds_begin ? s_begin : st_begin;
+    const int n_chunks = (n_tiles + ST_CHUNK - 1) / ST_CHUNK;
+    int head = 0, cnt = 0;                                          // wave 0's ring state (uniform)
+    bool a_done = false;
+    __syncthreads();
+    for (;;) {
+        if (threadIdx.x < 64) {
+            int job = ST_EXIT;
+            bool out_now = false;
+            if (cnt > 0) {
+                const int c = s_ring[head];
+                const int p0 = find_preset(beg, n_presets, c * ST_CHUNK);
+                const int p1 = find_preset(beg, n_presets, min(n_tiles, c * ST_CHUNK + ST_CHUNK) - 1);
+                uint32_t r0 = 0, r1 = 0;
+                if (lane == 0) {
+                    r0 = st_poll(sy.ready, p0);
+                    r1 = p1 == p0 ? r0 : st_poll(sy.ready, p1);
+                }
+                out_now = ((uint32_t)st_rfl((int)r0) >> 1) == sy.epoch && ((uint32_t)st_rfl((int)r1) >> 1) == sy.epoch;
+                out_now = out_now || cnt == ST_RING;
+            }
+            if (!out_now && !a_done) {
+                const int c = st_rfl(lane == 0 ? atomicAdd(ctr + ST_CTR_A, 1) : 0);
+                if (c < n_chunks) {
+                    job = c;
+                    if (lane == 0) s_ring[(head + cnt) & (ST_RING - 1)] = c;
+                    ++cnt;
+                } else {
+                    a_done = true;
+                }
+            }
+            if (job == ST_EXIT && cnt > 0) {                        // output pass of the oldest owned chunk
+                job = -2 - s_ring[head];
+                head = (head + 1) & (ST_RING - 1);
+                --cnt;
+            }
+            if (lane == 0) s_job = job;
+        }
+        __syncthreads();
+        const int job = st_rfl(s_job);                              // uniform: scalar registers
+        if (job == ST_EXIT) break;
+        const int c = job >= 0 ? job : -2 - job;
+        const int c1 = min(n_tiles, c * ST_CHUNK + ST_CHUNK);
+        for (int t = c * ST_CHUNK; t < c1;) {                       // one run per preset the chunk touches
+            const int p = st_rfl(find_preset(beg, n_presets, t));
+            const PresetRt& r = rt[p];
+            const int tb = beg[p];
+            const int tcnt = st_tiles_of(beg, n_presets, n_tiles, p);
+            const int te = min(c1, tb + tcnt);
+            if (job >= 0) {                                         // max pass
+                float m = 0.f;
+                for (int u = t; u < te; ++u)
+                    m = fmaxf(m, stereo_max_vals(r, u - tb, ybuf, nullptr,
+                                                 (sy.part && r.fir_on) ? sy.part + 2 * u : nullptr, false, w, wm));
+                stereo_run_done(r, p, tb, tcnt, te - t, m, maxbits, sy, &s_last, s_red);
+            } else {                                                // output pass
+                if (threadIdx.x == 0) {
+                    uint32_t rd;
+                    while (((rd = st_poll(sy.ready, p)) >> 1) != sy.epoch) __builtin_amdgcn_s_sleep(4);
+                    s_skip = (int)(rd & 1u);
+                    s_peak = __hip_atomic_load(maxbits + p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+                __syncthreads();
+                if (!st_rfl(s_skip)) {
+                    const unsigned peak = (unsigned)st_rfl((int)s_peak);
+                    for (int u = t; u < te; ++u) {
+                        stereo_out_tile(r, u - tb, ybuf, nullptr, peak, out, w, lw);
+                        __syncthreads();                            // LDS windows free for the next tile
+                    }
+                }
+            }
+            __syncthreads();                                        // s_last / s_skip / s_peak free
+            t = te;
+        }
+    }
+    if (threadIdx.x == 0 && atomicAdd(ctr + ST_CTR_E, 1) == (int)gridDim.x - 1) {
+        __hip_atomic_store(ctr + ST_CTR_A, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(ctr + ST_CTR_E, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}

@@ -41,8 +41,10 @@ hipError_t launch_spec3(unsigned grid, hipStream_t s, const msg_event* events, c
 void fir_init_attrs();
 // the float64 space FIR of heavily saturated renders (kernels_fir64.h): flag, h, H_q, blocks
 struct Fir64Launch {
-    const PresetRt* rt; int n_presets; const double* stats; unsigned* maxbits;
-    int32_t* slot_of; int32_t* slot_preset; int32_t* n_slots; int cap; int force;
+    const PresetRt* rt; int n_presets; const int32_t* flag64; unsigned* maxbits;
+    int32_t* slot_preset; int32_t* n_slots;
+    int n_cand;   // FIR presets of the batch (the most slots there can be)
+    int cap;      // slots per window (their h and H_q buffers)
     const Fir64Rt* fr; int tmax, qmax, bmax;
     const int32_t* er_off; const double* er_gain; const double* irbank;
     float* h64; int64_t h_stride; double2* hs64; int64_t hs_stride;
@@ -129,6 +131,21 @@ hipError_t launch_chain64(const G64Global* g, unsigned grid, int lds_bytes, hipS
                           const double* grain64, double* state, float* grain_pool);
 hipError_t launch_fft64_one(int lds_bytes, hipStream_t s, const Real64Plan* plans, int plan, int inverse,
                             double* io, double2* gA, double2* gB);
+
+// stereo, tanh clip and peak normalisation (kernels_stereo.h)
+hipError_t launch_stereo_max(unsigned n_tiles, hipStream_t s, const PresetRt* rt, const int32_t* st_begin, int n_presets,
+                             const float* y, unsigned* maxbits, const StereoSync& sy);
+hipError_t launch_stereo_fused(unsigned grid, unsigned n_tiles, hipStream_t s, const PresetRt* rt,
+                               const int32_t* st_begin, int n_presets, const float* y, unsigned* maxbits,
+                               const StereoSync& sy, int32_t* ctr, float* out);
+hipError_t launch_stereo_out(unsigned n_tiles, hipStream_t s, const PresetRt* rt, const int32_t* st_begin, int n_presets,
+                             const float* y, const float* r2, const unsigned* maxbits, float* out);
+hipError_t launch_stereo_remax(unsigned grid, hipStream_t s, const PresetRt* rt, const int32_t* st_count,
+                               const int32_t* list, const int32_t* n_list, int tmax, const float* y, const float* r2,
+                               unsigned* maxbits);
+hipError_t launch_stereo_out_list(unsigned grid, hipStream_t s, const PresetRt* rt, const int32_t* st_count,
+                                  const int32_t* list, const int32_t* n_list, int tmax, const float* y, const float* r2,
+                                  const unsigned* maxbits, float* out);
 
 // odd-length stereo rotation (kernels_stereo_odd.h): Bluestein through M = pow2 >= 2n-1
 void stereo_odd_init_attrs();

@@ -63,6 +63,15 @@ struct DevBuf {
     void release() { if (p) hipFree(p); p = nullptr; cap = 0; }
 };
 
+// ensure() that leaves a new allocation zeroed (counters and flags the kernels reset themselves)
+template <class T>
+static hipError_t ensure_zeroed(DevBuf<T>& b, size_t n, hipStream_t s) {
+    if (n <= b.cap && b.p) return hipSuccess;
+    hipError_t e = b.ensure(n);
+    if (e != hipSuccess) return e;
+    return hipMemsetAsync(b.p, 0, b.cap * sizeof(T), s);
+}
+
 // Pinned staging for a batch's host -> device uploads.  Every per-batch input
 // (presets, events, runtime records, job lists, IR bank ...) is packed into one
 // pinned slot and moved by ONE copy into a device arena; each input's device
@@ -252,7 +261,15 @@ struct msg_ctx {
     Slice<Fir64Rt> f64rt;
     Slice<int32_t> st_count, odd_list, odd_cnt;
     DevBuf<double> f64_stats;                   // per preset: sum y^2, sum (1 + (d y)^2)^-2
-    DevBuf<int32_t> f64_slot_of, f64_slot_preset, f64_nslots;
+    DevBuf<int32_t> f64_flag, f64_slot_preset, f64_nslots;
+    // stereo pass (kernels_stereo.h): the fused persistent launch (MSGPU_STEREO_FUSED,
+    // default 1) and its per-preset sync state, per-tile partial sums, counters
+    bool stereo_fused = false;          // measured slower than the two launches
+    int st_wgs = 4;                     // k_stereo_fused workgroups per CU (MSGPU_STEREO_WGS)
+    uint32_t st_epoch = 0;
+    DevBuf<int32_t> st_done, st_ctr;
+    DevBuf<uint32_t> st_ready;
+    DevBuf<double> st_part;
     DevBuf<int32_t> fir8_ctr;           // k_fir8p's per-XCD block counters
     DevBuf<float> f64_h;
     DevBuf<double2> f64_hs;
@@ -690,6 +707,8 @@ msg_ctx* msg_create(int device_ordinal) {
     if (const char* e = getenv("MSGPU_FIR64")) ctx->fir64 = atoi(e);
     if (const char* e = getenv("MSGPU_FIR8P")) ctx->fir8p = atoi(e);
     if (const char* e = getenv("MSGPU_FIR8P_CUS")) ctx->fir8p_cus = std::max(0, atoi(e));
+    if (const char* e = getenv("MSGPU_STEREO_FUSED")) ctx->stereo_fused = e[0] != '0';
+    if (const char* e = getenv("MSGPU_STEREO_WGS")) ctx->st_wgs = std::max(1, std::min(16, atoi(e)));
     {
         int cu = 0;
         if (hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, device_ordinal) == hipSuccess && cu >= MSG_XCDS)
@@ -763,7 +782,8 @@ void msg_destroy(msg_ctx* ctx) {
     ctx->micro.release(); ctx->grain.release();
     ctx->mono_a.release(); ctx->mono_y.release(); ctx->hspec.release();
     ctx->hscratch.release(); ctx->maxbits.release();
-    ctx->f64_stats.release(); ctx->f64_slot_of.release(); ctx->f64_slot_preset.release(); ctx->f64_nslots.release();
+    ctx->f64_stats.release(); ctx->f64_flag.release(); ctx->st_done.release(); ctx->st_ctr.release();
+    ctx->st_ready.release(); ctx->st_part.release(); ctx->f64_slot_preset.release(); ctx->f64_nslots.release();
     ctx->f64_h.release(); ctx->f64_hs.release();
     for (void* p : ctx->plans64.allocs) hipFree(p);
     ctx->plans64.dev.release();
@@ -1803,17 +1823,20 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
     HIPCHK(ctx, hipMemsetAsync(ctx->maxbits.p, 0, sizeof(unsigned) * P, s));
     // the float64 FIR chain: slots for up to FIR64_CAP flagged presets of the batch
     const bool f64_on = ctx->fir64 > 0 && f64_cand > 0;
-    const int f64_cap = std::min(f64_cand, FIR64_CAP);
     const int64_t f64_hstride = (f64_hmax + 3) & ~int64_t(3);
     const int64_t f64_hsstride = (int64_t)f64_qmax * FIR64_K;
+    // slots per window: every flagged preset is served, FIR64_WINDOW_BYTES of h and H_q at a time
+    const int64_t f64_slot_bytes = f64_hstride * (int64_t)sizeof(float) + f64_hsstride * (int64_t)sizeof(double2);
+    const int f64_cap = (int)std::max<int64_t>(1, std::min<int64_t>(std::min(f64_cand, FIR64_CAP),
+                                                                     FIR64_WINDOW_BYTES / std::max<int64_t>(1, f64_slot_bytes)));
     if (f64_on) {
         HIPCHK(ctx, ctx->f64_stats.ensure(2 * (size_t)P));
-        HIPCHK(ctx, ctx->f64_slot_of.ensure(P));
-        HIPCHK(ctx, ctx->f64_slot_preset.ensure(f64_cap));
+        HIPCHK(ctx, ctx->f64_flag.ensure(P));
+        HIPCHK(ctx, ctx->st_part.ensure(2 * (size_t)stiles));
+        HIPCHK(ctx, ctx->f64_slot_preset.ensure(f64_cand));
         HIPCHK(ctx, ctx->f64_nslots.ensure(1));
         HIPCHK(ctx, ctx->f64_h.ensure((size_t)(f64_cap * f64_hstride)));
         HIPCHK(ctx, ctx->f64_hs.ensure((size_t)(f64_cap * f64_hsstride)));
-        HIPCHK(ctx, hipMemsetAsync(ctx->f64_stats.p, 0, sizeof(double) * 2 * P, s));
         HIPCHK(ctx, h2d(&ctx->f64rt.p, f64rt.data(), sizeof(Fir64Rt) * P));
     }
     const int32_t n_odd = (int32_t)odd_presets.size();
@@ -1950,15 +1973,36 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
     }
     // ---- stereo, tanh, normalise ----
     stage_mark(ctx, 6, s);
-    // peak of L (and the float64 FIR's error predictor) over the float32 y
-    hipLaunchKernelGGL(k_stereo_max, dim3((unsigned)stiles), dim3(ST_T), 0, s, ctx->prt.p, ctx->st_begin.p, P,
-                       yb, ctx->so_r2.p, ctx->maxbits.p, f64_on ? ctx->f64_stats.p : (double*)nullptr, 0);
-    HIPCHK(ctx, hipGetLastError());
+    // peak of L (and the float64 FIR's error predictor) over the float32 y; the
+    // fused launch also writes the output of every preset it does not defer
+    // (float64 FIR slots, odd lengths: k_stereo_out_list below)
+    StereoSync sy{};
+    HIPCHK(ctx, ensure_zeroed(ctx->st_done, P, s));
+    HIPCHK(ctx, ensure_zeroed(ctx->st_ready, P, s));
+    sy.done = ctx->st_done.p;
+    sy.ready = ctx->st_ready.p;
+    sy.flag64 = f64_on ? ctx->f64_flag.p : nullptr;
+    sy.part = f64_on ? ctx->st_part.p : nullptr;
+    sy.stats = f64_on ? ctx->f64_stats.p : nullptr;
+    ctx->st_epoch = ctx->st_epoch % ((1u << 30) - 1) + 1;
+    sy.epoch = ctx->st_epoch;
+    sy.f64mode = f64_on ? ctx->fir64 : 0;
+    int st_tmax = 0;
+    for (int p = 0; p < P; ++p) st_tmax = std::max(st_tmax, st_count[p]);
+    const bool st_fused = ctx->stereo_fused && st_tmax <= ST_FUSED_MAX_TILES;
+    if (st_fused) {
+        if (!ctx->st_ctr.p) HIPCHK(ctx, ensure_zeroed(ctx->st_ctr, ST_CTR_N, s));   // every launch leaves them zero
+        const unsigned grid = (unsigned)std::max(1, std::min(stiles, ctx->n_cu * ctx->st_wgs));
+        HIPCHK(ctx, launch_stereo_fused(grid, (unsigned)stiles, s, ctx->prt.p, ctx->st_begin.p, P, yb, ctx->maxbits.p,
+                                        sy, ctx->st_ctr.p, out_dev));
+    } else {
+        HIPCHK(ctx, launch_stereo_max((unsigned)stiles, s, ctx->prt.p, ctx->st_begin.p, P, yb, ctx->maxbits.p, sy));
+    }
     if (f64_on) {   // flagged presets: the FIR again in float64, y overwritten (kernels_fir64.h)
         Fir64Launch a;
-        a.rt = ctx->prt.p; a.n_presets = P; a.stats = ctx->f64_stats.p; a.maxbits = ctx->maxbits.p;
-        a.slot_of = ctx->f64_slot_of.p; a.slot_preset = ctx->f64_slot_preset.p; a.n_slots = ctx->f64_nslots.p;
-        a.cap = f64_cap; a.force = ctx->fir64 >= 2 ? 1 : 0;
+        a.rt = ctx->prt.p; a.n_presets = P; a.flag64 = ctx->f64_flag.p; a.maxbits = ctx->maxbits.p;
+        a.slot_preset = ctx->f64_slot_preset.p; a.n_slots = ctx->f64_nslots.p;
+        a.n_cand = f64_cand; a.cap = f64_cap;
         a.fr = ctx->f64rt.p; a.tmax = (int)((f64_hmax + H_BUILD_TILE - 1) / H_BUILD_TILE); a.qmax = f64_qmax;
         a.bmax = f64_bmax;
         a.er_off = ctx->er_off.p; a.er_gain = ctx->er_gain.p; a.irbank = ctx->irbank.p;
@@ -2000,21 +2044,29 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
         HIPCHK(ctx, launch_stereo_odd(n, ctx->so_row, ctx->so_col, prt[p].dr, w, yb + prt[p].y_off, it->second.p, ctx->so_A.p,
                                       ctx->so_r2.p + prt[p].r2_off, s));
     }
+    int odd_tmax = 0;
+    for (int p : odd_presets) odd_tmax = std::max(odd_tmax, st_count[p]);
     if (f64_on)   // the float64 presets' peak from their new y (and R)
-        hipLaunchKernelGGL(k_stereo_remax, dim3((unsigned)std::min(f64_cap * f64_stmax, 256)), dim3(ST_T), 0, s,
-                           ctx->prt.p, ctx->st_count.p, ctx->f64_slot_preset.p, ctx->f64_nslots.p, f64_stmax, yb,
-                           ctx->so_r2.p, ctx->maxbits.p);
-    if (n_odd > 0) {   // odd lengths: the peak of the rotated R
-        int tmax = 0;
-        for (int p : odd_presets) tmax = std::max(tmax, st_count[p]);
-        hipLaunchKernelGGL(k_stereo_remax, dim3((unsigned)std::min<int64_t>((int64_t)n_odd * tmax, 4096)), dim3(ST_T),
-                           0, s, ctx->prt.p, ctx->st_count.p, ctx->odd_list.p, ctx->odd_cnt.p, tmax, yb,
-                           ctx->so_r2.p, ctx->maxbits.p);
+        HIPCHK(ctx, launch_stereo_remax((unsigned)std::min(f64_cand * f64_stmax, 256), s, ctx->prt.p, ctx->st_count.p,
+                                        ctx->f64_slot_preset.p, ctx->f64_nslots.p, f64_stmax, yb, ctx->so_r2.p,
+                                        ctx->maxbits.p));
+    if (n_odd > 0)   // odd lengths: the peak of the rotated R
+        HIPCHK(ctx, launch_stereo_remax((unsigned)std::min<int64_t>((int64_t)n_odd * odd_tmax, 4096), s, ctx->prt.p,
+                                        ctx->st_count.p, ctx->odd_list.p, ctx->odd_cnt.p, odd_tmax, yb, ctx->so_r2.p,
+                                        ctx->maxbits.p));
+    if (st_fused) {   // the deferred presets' output
+        if (f64_on)
+            HIPCHK(ctx, launch_stereo_out_list((unsigned)std::min(f64_cand * f64_stmax, 1024), s, ctx->prt.p,
+                                               ctx->st_count.p, ctx->f64_slot_preset.p, ctx->f64_nslots.p, f64_stmax,
+                                               yb, ctx->so_r2.p, ctx->maxbits.p, out_dev));
+        if (n_odd > 0)
+            HIPCHK(ctx, launch_stereo_out_list((unsigned)std::min<int64_t>((int64_t)n_odd * odd_tmax, 4096), s,
+                                               ctx->prt.p, ctx->st_count.p, ctx->odd_list.p, ctx->odd_cnt.p, odd_tmax,
+                                               yb, ctx->so_r2.p, ctx->maxbits.p, out_dev));
+    } else {
+        HIPCHK(ctx, launch_stereo_out((unsigned)stiles, s, ctx->prt.p, ctx->st_begin.p, P, yb, ctx->so_r2.p,
+                                      ctx->maxbits.p, out_dev));
     }
-    HIPCHK(ctx, hipGetLastError());
-    hipLaunchKernelGGL(k_stereo_out, dim3((unsigned)stiles), dim3(ST_T), 0, s, ctx->prt.p, ctx->st_begin.p, P,
-                       yb, ctx->so_r2.p, ctx->maxbits.p, out_dev);
-    HIPCHK(ctx, hipGetLastError());
     stage_mark(ctx, 7, s);
     HIPCHK(ctx, done.finish());
     ctx->h_info = info;

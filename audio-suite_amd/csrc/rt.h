@@ -116,13 +116,35 @@ struct Chain64 {
 // The float64 space FIR of heavily saturated renders (kernels_fir64.h): one
 // record per FIR preset, the shape of its float64 overlap-save.
 constexpr int FIR64_N = 16384, FIR64_P = FIR64_N / 2, FIR64_B = FIR64_N - FIR64_P + 1, FIR64_K = FIR64_N / 2 + 1;
-constexpr int FIR64_CAP = 128;     // presets per batch that can take it (slots, in batch order)
+// float64 slots buffered per window of the chain (h and H_q of every slot of a
+// window are resident at once): all flagged presets of a batch are processed,
+// in windows of this many slots when the slots' buffers would exceed
+// FIR64_WINDOW_BYTES
+constexpr int FIR64_CAP = 1024;
+constexpr int64_t FIR64_WINDOW_BYTES = (int64_t)1 << 30;
+constexpr double FIR64_PRED = 5e-7;   // predicted float32 error above which a preset takes float64
 struct Fir64Rt {
     int32_t h_len;                 // taps of h (<= out_n)
     int32_t q;                     // partitions of FIR64_P taps
     int32_t blocks;                // output blocks of FIR64_B frames
     int32_t st_tiles;              // stereo tiles (k_stereo_remax)
 };
+
+// Cross-workgroup state of the max pass (per context, reused launch to launch).
+struct StereoSync {
+    int32_t* done;       // per preset: max-pass tiles finished (the preset's last tile resets it to 0)
+    uint32_t* ready;     // per preset: (epoch << 1) | deferred once every max-pass tile is done
+    int32_t* flag64;     // per preset: 1 = takes the float64 FIR (null when the route is off)
+    double* part;        // per stereo tile: the tile's sum y^2, sum q^2 (null when the route is off)
+    double* stats;       // per preset: the same sums over the preset, added in tile order
+    uint32_t epoch;      // this launch's tag, 1 .. 2^30
+    int f64mode;         // 0 route off, 1 predicted, 2 every FIR preset (MSGPU_FIR64)
+};
+constexpr int ST_CTR_A = 0, ST_CTR_E = 32, ST_CTR_N = 64;   // k_stereo_fused counters, 128 B apart
+// the fused stereo launch takes batches whose presets have at most this many
+// stereo tiles (kernels_stereo.h: its deadlock-freedom bound); longer ones run
+// k_stereo_max + k_stereo_out
+constexpr int ST_FUSED_MAX_TILES = 2048;
 
 constexpr int GEN_T = 64;          // one wave per event
 constexpr int OLA_T = 256;
@@ -168,6 +190,22 @@ __device__ __forceinline__ int find_preset(const int32_t* __restrict__ begin, in
     }
     return lo;
 }
+
+#if defined(__HIPCC__)
+// The float64 FIR's error predictor (kernels_fir64.h): eps32 rms(y) x sqrt(the
+// clip's linear share) x the clip's slope at 0 x the peak scale (MS:26-34),
+// from sum y^2 (sy2), sum (1 + (d y)^2)^-2 (sq) and the float32 peak bits.
+MSG_DEV double fir64_pred(const PresetRt& r, double sy2, double sq, unsigned peak_bits) {
+    const double n = (double)r.out_n;
+    const double d = (double)r.drive;
+    const double rms = sqrt(sy2 / n), share = sq / n;
+    const double M = (double)__uint_as_float(peak_bits);
+    double slope = 1.0, mc = M;
+    if (d > 0.0) { slope = d / tanh(d); mc = tanh(M * d) / tanh(d); }
+    const double scale = mc > 0.0 ? (double)r.peak / mc : 1.0;
+    return 5.9604644775390625e-8 * rms * sqrt(share) * slope * scale;
+}
+#endif
 
 MSG_DEV float fade_w(int j, int n, int fade) {
     double w = 1.0;

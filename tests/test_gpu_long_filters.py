@@ -276,3 +276,46 @@ def test_fir8_persistent_bit_identical(msgpu, irs, full_renders):
     assert np.array_equal(outs["0"], outs["1"])
     packed, _ = _render_env(params[:1], {})
     assert rms(outs["1"][:int(packed.out_n[0])], full_renders["C3_audio"]) <= RMS_TOL
+
+
+def test_fir64_serves_every_flagged_preset(msgpu, irs):
+    """the float64 FIR had 128 slots per batch and left flagged
+    presets beyond them on float32, so a preset's output depended on the batch
+    it shared.  Every flagged preset is now served (in windows of slots): 140
+    copies of one saturated ER + IR preset in one batch all match the preset
+    rendered alone, bit for bit, and the oracle within FIR_TOL."""
+    from oracle import msound_oracle as O
+    p = msgpu.merged(gen_mode="Resonant strike", event_process="Poisson", _ir_audio=irs["tiny_room_ir"],
+                     base_sr=48000, out_dur_s=0.3, space_ir_on=True, seed=22, er_cloud_on=True,
+                     space_ir_max_samps=8192, stereo_width=0.3)
+    packed1, one = _render_env([p], {})
+    packedN, many = _render_env([p] * 140, {})
+    n = int(packed1.out_n[0])
+    for i in (0, 127, 128, 139):
+        off = int(packedN.offsets[i])
+        assert np.array_equal(many[off:off + n], one[:n]), i
+    e = rms(one[:n], O.render(p)[0])
+    _, f32 = _render_env([p], {"MSGPU_FIR64": "0"})
+    e32 = rms(f32[:n], O.render(p)[0])
+    print(f"saturated preset: rms err {e:.3e} (float32 FIR alone: {e32:.3e})")
+    assert e <= FIR_TOL and not np.array_equal(one[:n], f32[:n])   # the float64 route did run
+
+
+def test_stereo_fused_matches_two_launches(msgpu, irs):
+    """k_stereo_fused (MSGPU_STEREO_FUSED=1: max and output passes in one
+    persistent launch, deferred float64-FIR and odd-length presets) writes the
+    same bits as k_stereo_max + k_stereo_out, and the float64 FIR's per-preset
+    sums are added in tile order, so two renders are identical."""
+    base = dict(gen_mode="Resonant strike", event_process="Poisson", _ir_audio=irs["tiny_room_ir"])
+    params = [msgpu.config_params("C3", seed=1000 + s, irs=irs, out_dur_s=0.3) for s in range(3)]
+    params += [msgpu.merged(base, base_sr=48000, out_dur_s=0.3, space_ir_on=True, seed=22, er_cloud_on=True,
+                            space_ir_max_samps=8192, stereo_width=0.3),          # float64 FIR (deferred)
+               msgpu.merged(out_dur_s=0.2, seed=5),                             # no filter
+               msgpu.merged(out_dur_s=0.2000208, seed=6, base_sr=48000),        # odd length (deferred)
+               msgpu.config_params("C2", seed=1000, irs=irs, out_dur_s=0.25)]
+    _, two = _render_env(params, {"MSGPU_STEREO_FUSED": "0"})
+    _, two_again = _render_env(params, {"MSGPU_STEREO_FUSED": "0"})
+    packed, fused = _render_env(params, {"MSGPU_STEREO_FUSED": "1"})
+    assert int(packed.out_n[5]) % 2 == 1
+    assert np.array_equal(two, two_again)
+    assert np.array_equal(two, fused)
