@@ -314,7 +314,7 @@ template <int UNUSED = 0>
 __global__ void __launch_bounds__(fir8::T)
 k_fir8p(const PresetRt* __restrict__ rt, const int2* __restrict__ jobs, int n_jobs, const float2* __restrict__ tables,
         const float2* __restrict__ hspec, const float* __restrict__ x_in, float* __restrict__ y_out,
-        int32_t* __restrict__ ctr) {
+        int32_t* __restrict__ ctr, int stagger) {
     using namespace fir8;
     extern __shared__ __attribute__((aligned(16))) float2 lds[];
     __shared__ int s_take[2];
@@ -322,6 +322,14 @@ k_fir8p(const PresetRt* __restrict__ rt, const int2* __restrict__ jobs, int n_jo
     float2* buf = lds + G::TAB;
     const int t = otid();
     { TabCopy<G::TAB_USED, T> tc; tc.fetch(tables); tc.put(tab); }
+    // Stagger (MSGPU_FIR8P_STAGGER wall-clock ticks of 10 ns): every other
+    // workgroup of an XCD starts its first block that much later, so the two
+    // halves of the chip load their 256 KB segments and store their outputs
+    // out of phase instead of all together.
+    if (stagger > 0 && ((blockIdx.x / MSG_XCDS) & 1)) {
+        const long long t_end = wall_clock64() + stagger;
+        while (wall_clock64() < t_end) __builtin_amdgcn_s_sleep(16);
+    }
     // ctr[x * FIR8P_CTR]: XCD x's next block; ctr[MSG_XCDS * FIR8P_CTR]: workgroups
     // done.  The last workgroup to finish zeroes them for the next launch (no
     // memset kernel: one would queue for a CU behind the other streams' work).
@@ -345,6 +353,7 @@ k_fir8p(const PresetRt* __restrict__ rt, const int2* __restrict__ jobs, int n_jo
         }
         if (k == MSG_XCDS) break;
         const int xr = (x0 + k) % MSG_XCDS;
+        FIR_STAMP_INIT;
         const int2 job = jobs[lo + cur];
         const PresetRt& pr = rt[job.x];
         const int P = pr.fir_P;                   // Q == 1
@@ -354,16 +363,23 @@ k_fir8p(const PresetRt* __restrict__ rt, const int2* __restrict__ jobs, int n_jo
         load_halves(x_in + pr.y_off, n, t0 - (P - 1), a, b);
         if (t == 0) s_take[par] = atomicAdd(ctr + xr * FIR8P_CTR, 1);   // the block after this one
         dif_split(tab, a, b);
+        FIR_STAMP(0);
         const float2* He = hspec + pr.h_off;
         const float2* Ho = He + (MH + 1);
         float2 v[2][R4], acc[2][R4], A[R1];
         fwd_half<false>(buf, tab, a, v);
+        FIR_STAMP(1);
         even_mac_pre(tab, v, He, acc);
+        FIR_STAMP(2);
         inv_half<false>(buf, tab, acc, A);
+        FIR_STAMP(3);
         fwd_half<true>(buf, tab, b, v);
+        FIR_STAMP(4);
         odd_mac_pre(tab, v, Ho, acc);
+        FIR_STAMP(5);
         float2 (&B)[R1] = a;                      // a is dead: its registers take B
         inv_half<true>(buf, tab, acc, B);
+        FIR_STAMP(6);
         const int nxt = s_take[par];              // written before this block's first barrier
         // F[m] = A + W_M^m B, F[m + MH] = A - W_M^m B; z'[m] = conj(F[m]) / M
         const float2 wt = fir4_wM(tab, G::OFF_PLO, G::OFF_PHI, t);
@@ -378,6 +394,7 @@ k_fir8p(const PresetRt* __restrict__ rt, const int2* __restrict__ jobs, int n_jo
             for (int h = 0; h < 2; ++h)
                 so.put((uint32_t)(d0 + 2 * (r * NB1 + h * MH)), make_float2(f[h].x * s, -f[h].y * s));
         }
+        FIR_STAMP(7);
         cur = nxt;
         par ^= 1;
     }

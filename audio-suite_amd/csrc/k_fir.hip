@@ -133,9 +133,10 @@ hipError_t launch_fir8(unsigned grid, hipStream_t s, const PresetRt* rt, const i
 // per-XCD counters (ctr: (MSG_XCDS + 1) x FIR8P_CTR int32, zero before the first
 // launch; each launch leaves them zero)
 hipError_t launch_fir8p(unsigned n_jobs, unsigned grid, hipStream_t s, const PresetRt* rt, const int2* jobs,
-                        const float2* tables, const float2* hspec, const float* x_in, float* y_out, int32_t* ctr) {
+                        const float2* tables, const float2* hspec, const float* x_in, float* y_out, int32_t* ctr,
+                        int stagger) {
     hipLaunchKernelGGL((k_fir8p<0>), dim3(grid), dim3(fir8::T), Fir4Geo<16384>::LDS_BYTES, s, rt, jobs, (int)n_jobs,
-                       tables, hspec, x_in, y_out, ctr);
+                       tables, hspec, x_in, y_out, ctr, stagger);
     return hipGetLastError();
 }
 

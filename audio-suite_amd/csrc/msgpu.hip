@@ -216,6 +216,7 @@ struct msg_ctx {
     int fir8p = 1;
     int n_cu = 256;              // compute units (persistent grids)
     int fir8p_cus = 0;           // persistent FIR workgroups (MSGPU_FIR8P_CUS, A/B; 0: one per CU)
+    int fir8p_stagger = 0;       // k_fir8p: every other workgroup starts this many 10-ns ticks later (MSGPU_FIR8P_STAGGER)
     // Q <= 2 presets on the streaming k_fir4s (MSGPU_FIR4S=1; off by default: at
     // C3's 24 blocks per preset its H re-reads miss L2 and cancel the saved transforms)
     bool fir4s = false;
@@ -707,6 +708,7 @@ msg_ctx* msg_create(int device_ordinal) {
     if (const char* e = getenv("MSGPU_FIR64")) ctx->fir64 = atoi(e);
     if (const char* e = getenv("MSGPU_FIR8P")) ctx->fir8p = atoi(e);
     if (const char* e = getenv("MSGPU_FIR8P_CUS")) ctx->fir8p_cus = std::max(0, atoi(e));
+    if (const char* e = getenv("MSGPU_FIR8P_STAGGER")) ctx->fir8p_stagger = std::max(0, atoi(e));
     if (const char* e = getenv("MSGPU_STEREO_FUSED")) ctx->stereo_fused = e[0] != '0';
     if (const char* e = getenv("MSGPU_STEREO_WGS")) ctx->st_wgs = std::max(1, std::min(16, atoi(e)));
     {
@@ -1949,7 +1951,8 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
                     HIPCHK(ctx, hipMemsetAsync(ctx->fir8_ctr.p, 0, sizeof(int32_t) * ctx->fir8_ctr.cap, s));
                 }
                 HIPCHK(ctx, launch_fir8p(nj, grid, s, ctx->prt.p, ctx->fir_jobs.p + fjob_off[i],
-                                         ctx->d_fir4tab, ctx->hspec.p, ctx->mono_a.p, ctx->mono_y.p, ctx->fir8_ctr.p));
+                                         ctx->d_fir4tab, ctx->hspec.p, ctx->mono_a.p, ctx->mono_y.p, ctx->fir8_ctr.p,
+                                         ctx->fir8p_stagger));
             } else if (i == 6)
                 HIPCHK(ctx, launch_fir8(nj, s, ctx->prt.p, ctx->fir_jobs.p + fjob_off[i], ctx->d_fir4tab, ctx->hspec.p,
                                         ctx->mono_a.p, ctx->mono_y.p));

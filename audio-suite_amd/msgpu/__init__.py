@@ -16,16 +16,19 @@ def render(params, progress=None, device: int = 0):
     return _render(params, progress, device)
 
 
-def render_batch(params_list, device: int = 0, devices=None):
+def render_batch(params_list, device: int = 0, devices=None, results: str = "audio"):
     """Render many presets; ``devices`` (e.g. range(8)) shards them across GPUs,
-    one worker process per GPU (multi.py; call before this process touches the GPU)."""
+    one worker process per GPU (multi.py; call before this process touches the GPU).
+    ``results``: "audio" ((out_n, 2) float32 arrays), "stats" (a summary per
+    preset, multi.audio_stats) or "device" (the renders stay in HBM: device
+    tensors on one GPU, multi.DeviceResult handles across several)."""
     if devices is not None and len(list(devices)) > 1:
         from .multi import pool_for
-        return pool_for(devices).render_batch(params_list)
+        return pool_for(devices).render_batch(params_list, results=results)
     if devices is not None:
         device = int(list(devices)[0])
     from .dropin import render_batch as _rb
-    return _rb(params_list, device)
+    return _rb(params_list, device, results)
 
 
 def DevicePool(devices, stub: bool = False, share_devices: bool = False):

@@ -56,6 +56,15 @@ STAGE_NAMES = ["plan", "host_prep", "generate", "spectral", "overlap_add", "fir"
                "fir_kernel", "fir_h", "host_plan_wall", "host_records_wall", "host_upload_wall",
                "host_plan_sizes", "host_plan_events", "host_preset_records", "host_event_records", "host_lists"]
 KERNEL_STAGES = ["generate", "spectral", "overlap_add", "fir_kernel", "stereo"]
+# the line's roofline kernel per config: the stage of the config's rocprof-dominant
+# kernel (largest share of GPU time in profiles/r04h_*kernel_stats.csv: k_spec3 for
+# C3 and C4, k_fir8p for C5), fixed so that roofline.frac is one kernel's series
+# across rounds; other configs: the longest window of the run
+DOMINANT_STAGE = {"C3": "spectral", "C4": "spectral", "C5": "fir_kernel"}
+# the north star's "FIR + rFFT stage": the band-pruned / compile-time spectral
+# kernels (rFFT -> band limit -> stretch -> irFFT), the filter spectra and the
+# overlap-save FIR
+FIR_RFFT_STAGES = ("spectral", "fir_h", "fir_kernel")
 # host cores one GPU's rank uses at most (the GPU box's CPU share per GPU; nproc
 # shows the whole machine).  The rank's actual set is its slice of the process
 # affinity (pin_rank_cpus).
@@ -476,7 +485,8 @@ def measure(runner, cfg, seeds, sub, steps, warmup, comm, irs, golden, iso_steps
     nsub = len(w.subs)
     sb = stage_bytes(infos)
     sb_launch = {k: v / nsub for k, v in sb.items()}
-    dom = max(KERNEL_STAGES, key=lambda k: stages[k])
+    longest = max(KERNEL_STAGES, key=lambda k: stages[k])
+    dom = DOMINANT_STAGE.get(cfg, longest)
     achieved = sb_launch[dom] / (stages[dom] * 1e-3) / 1e9
     launch_batch = len(seeds) // nsub
     sum_n = sum(int(i.pool_len) for i in infos)
@@ -492,6 +502,10 @@ def measure(runner, cfg, seeds, sub, steps, warmup, comm, irs, golden, iso_steps
                      "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": measured_traffic(STAGE_KERNEL[dom], cfg, launch_batch),
                      "algorithmic_bytes": sb_launch[dom], "kernel_ms": stages[dom],
+                     "kernel_choice": "the config's rocprof-dominant kernel (DOMINANT_STAGE)" if cfg in DOMINANT_STAGE
+                                      else "the longest window of this run",
+                     "longest_window_stage": longest,
+                     "fir_rfft_stage": {"timed": fir_rfft(sb_launch, stages, "per launch in the timed region")},
                      "note": f"per launch in the timed region ({nsub} sub-batches of ~{launch_batch} presets "
                              f"on {len(runner.engs)} streams sharing the GPU)"},
         "stage_ms": stages,
@@ -509,8 +523,23 @@ def measure(runner, cfg, seeds, sub, steps, warmup, comm, irs, golden, iso_steps
                              "note": "packing of every sub-batch's param dicts inside the timed step"}
     if iso_steps > 0:
         rec["roofline_isolated"] = isolated(runner, w, iso_steps, sb, cfg)
+        rec["roofline"]["fir_rfft_stage"]["isolated"] = rec["roofline_isolated"]["fir_rfft_stage"]
     runner.free(w)
     return rec
+
+
+def fir_rfft(sbytes, st_ms, where):
+    """The north star's FIR + rFFT stage (FIR_RFFT_STAGES): the spectral and FIR
+    kernels' algorithmic bytes (grain read + write, mono read + write; the filter
+    spectra's own writes, 8 B x 32 769 per preset, are not counted) over the sum
+    of the three stages' windows (h spectra included)."""
+    b = sbytes["spectral"] + sbytes["fir_kernel"]
+    ms = sum(st_ms.get(k, 0.0) for k in FIR_RFFT_STAGES)
+    ach = b / (ms * 1e-3) / 1e9 if ms > 0 else 0.0
+    return {"kernels": "k_spec3 / k_spectral_ct + k_fir8_hconv / k_fir8_spec + k_fir8p",
+            "algorithmic_bytes": b, "ms": round(ms, 4), "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
+            "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
+            "stage_ms": {k: st_ms.get(k) for k in FIR_RFFT_STAGES}, "note": where}
 
 
 def pack_ms(w, reps=5):
@@ -544,7 +573,7 @@ def isolated(runner, w, iso_steps, sb, cfg):
     iso = {n: round(float(v), 4) for n, v in zip(STAGE_NAMES, e.stage_times())}
     if not whole:
         sb = stage_bytes(e.last_plan())
-    dom = max(KERNEL_STAGES, key=lambda k: iso[k])
+    dom = DOMINANT_STAGE.get(cfg, max(KERNEL_STAGES, key=lambda k: iso[k]))
     ach = sb[dom] / (iso[dom] * 1e-3) / 1e9
     kern = [k for k in KERNEL_STAGES if iso.get(k, 0) > 0]
     tot_bytes = sum(sb[k] for k in kern)
@@ -556,6 +585,7 @@ def isolated(runner, w, iso_steps, sb, cfg):
             "stage_ms": iso,
             "stage_frac": {k: round(sb[k] / (iso[k] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) for k in kern},
             "kernels_frac": round(tot_bytes / (tot_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+            "fir_rfft_stage": fir_rfft(sb, iso, "whole batch (or one sub-batch) alone on one stream"),
             "presets": packed.n,
             "note": (f"whole batch on one stream, {iso_steps} renders after the timed region" if whole else
                      f"one sub-batch of {packed.n} presets alone on one stream, {iso_steps} renders after the "

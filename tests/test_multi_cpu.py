@@ -112,3 +112,83 @@ def test_shared_device_rehearsal(irs):
         assert [split[0]["presets"][0], split[0]["presets"][1], split[1]["presets"][1]] == balance(plan_costs(params), 2)
     finally:
         p.close()
+
+
+def test_stats_mode(pool2, irs):
+    """results="stats": one summary per preset in the caller's order, equal to a
+    host computation on the worker's fill (the stub writes (index, device))."""
+    from msgpu.multi import audio_stats
+    params = mixed(irs)
+    stats = pool2.render_batch(params, results="stats")
+    out_n = PackedBatch(params).out_n
+    cut = pool2.last_split[0]["presets"][1]
+    assert len(stats) == len(params)
+    for i, (s, n) in enumerate(zip(stats, out_n)):
+        a = np.empty((n, 2), np.float32)
+        a[:, 0] = i
+        a[:, 1] = 0 if i < cut else 1
+        assert s == audio_stats(a)
+        assert s["out_n"] == n and s["sum_l"] == i * n
+
+
+def test_device_mode_fetch_and_release(pool2, irs):
+    """results="device": handles in the caller's order; fetch copies one render
+    back, release frees it (a fetch after that raises)."""
+    params = mixed(irs)[:5]
+    hs = pool2.render_batch(params, results="device")
+    out_n = PackedBatch(params).out_n
+    assert [h.index for h in hs] == list(range(5))
+    for h, n in zip(hs, out_n):
+        a = pool2.fetch(h)
+        assert a.shape == (n, 2) and np.all(a[:, 0] == h.index) and np.all(a[:, 1] == h.device)
+    pool2.release(hs[:2])
+    with pytest.raises(KeyError):
+        pool2.fetch(hs[0])
+    assert np.all(pool2.fetch(hs[2])[:, 0] == 2)
+    pool2.release(hs[2:])
+
+
+def test_interrupted_call_closes_the_pool(monkeypatch, irs):
+    """an interrupted call must not leave replies in the pipes for
+    the next one.  The interrupted pool is closed and dropped from pool_for's
+    cache; a new pool renders the next call correctly."""
+    from msgpu import multi
+    p = DevicePool([0, 1], stub=True)
+    monkeypatch.setitem(multi._POOLS, (7, 8), p)
+    params = mixed(irs)[:6]
+    real = p._recv_checked
+    calls = {"n": 0}
+
+    def flaky(*a):
+        calls["n"] += 1
+        if calls["n"] == 1:
+            raise KeyboardInterrupt
+        return real(*a)
+    monkeypatch.setattr(p, "_recv_checked", flaky)
+    with pytest.raises(KeyboardInterrupt):
+        p.render_batch(params)
+    assert p._closed and (7, 8) not in multi._POOLS
+    with pytest.raises(RuntimeError, match="closed"):
+        p.render_batch(params)
+    q = DevicePool([0, 1], stub=True)
+    try:
+        outs = q.render_batch(params)
+        assert [int(a[0, 0]) for a in outs] == list(range(6))
+    finally:
+        q.close()
+
+
+def test_stale_reply_is_detected(irs):
+    """A reply that belongs to another job (sequence number, shared block or
+    preset range) is refused and closes the pool instead of being paired with
+    the current job."""
+    p = DevicePool([0, 1], stub=True)
+    try:
+        params = mixed(irs)[:4]
+        # a stray job whose reply will sit in worker 0's pipe ahead of the real one
+        p._conns[0].send(("job", 10_000, "stats", None, [0], params[:1], [0], [int(PackedBatch(params[:1]).out_n[0])]))
+        with pytest.raises(RuntimeError, match="out of step"):
+            p.render_batch(params, results="stats")
+        assert p._closed
+    finally:
+        p.close()

@@ -8,6 +8,12 @@ pool.render_batch, then the same batch renders in this process with
 msgpu.render_batch(device=0) and the two are compared preset by preset.
 
     python tools/multi_rehearsal.py [W]     # prints one JSON line
+
+``stats W N``: N C5 presets (seeds 1000..) through pool.render_batch(...,
+results="stats") -- the C5-scale mode that never brings the outputs (67 MB per
+preset) to the host; records the parent's and the workers' peak RSS, checks
+preset 0 against the reference's C5 summary and the first presets' summaries
+against the same presets rendered in this process afterwards.
 """
 import json
 import os
@@ -20,7 +26,43 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(REPO, "audio-suite_amd"))
 
 
+def stats_main(w, n):
+    import resource
+    import msgpu
+    z = np.load(os.path.join(REPO, "tests", "golden", "irs.npz"))
+    irs = {k: z[k] for k in z.files}
+    with open(os.path.join(REPO, "tests", "golden", "golden_info.json")) as f:
+        golden = json.load(f)["summaries"]
+    params = [msgpu.config_params("C5", seed=1000 + i, irs=irs) for i in range(n)]
+    rss0 = resource.getrusage(resource.RUSAGE_SELF).ru_maxrss
+    pool = msgpu.DevicePool([0] * w, share_devices=True)     # before any GPU call here
+    t0 = time.perf_counter()
+    stats = pool.render_batch(params, results="stats")
+    t_pool = time.perf_counter() - t0
+    split = pool.last_split
+    pool.close()
+    rss_parent = resource.getrusage(resource.RUSAGE_SELF).ru_maxrss
+    rss_workers = resource.getrusage(resource.RUSAGE_CHILDREN).ru_maxrss
+    ref = golden.get("C5_1000")
+    d0 = {"rms": abs(stats[0]["rms"] - ref["rms"]), "sum_l": abs(stats[0]["sum_l"] - ref["sum_l"]) / stats[0]["out_n"],
+          "sum_r": abs(stats[0]["sum_r"] - ref["sum_r"]) / stats[0]["out_n"]} if ref else None
+    k = min(4, n)
+    again = msgpu.render_batch(params[:k], device=0, results="stats")
+    same = all(a == b for a, b in zip(stats[:k], again))
+    out_bytes = 8 * sum(s["out_n"] for s in stats)
+    ok = len(stats) == n and same and (d0 is None or max(d0.values()) <= 1e-5)
+    print(json.dumps({"mode": "stats", "workers": w, "presets": n, "split": split, "pool_s": round(t_pool, 2),
+                      "output_bytes_not_copied": out_bytes, "parent_maxrss_mb": round(rss_parent / 1024, 1),
+                      "parent_maxrss_before_mb": round(rss0 / 1024, 1),
+                      "workers_maxrss_mb": round(rss_workers / 1024, 1),
+                      "preset0_vs_reference": d0, "first_presets_equal_in_process": same,
+                      "stats0": stats[0], "ok": ok}), flush=True)
+    sys.exit(0 if ok else 1)
+
+
 def main():
+    if len(sys.argv) > 1 and sys.argv[1] == "stats":
+        return stats_main(int(sys.argv[2]) if len(sys.argv) > 2 else 2, int(sys.argv[3]) if len(sys.argv) > 3 else 1024)
     w = int(sys.argv[1]) if len(sys.argv) > 1 else 2
     import msgpu
     z = np.load(os.path.join(REPO, "tests", "golden", "irs.npz"))
