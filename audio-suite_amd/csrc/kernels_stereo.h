@@ -79,7 +79,7 @@ MSG_DEV void stereo_load(const float* __restrict__ y, int n, int b0, int len, fl
             const int u = tid + i * ST_T;
             int j = b0 + u;
             if (j >= n) j -= n;
-            v[i] = u < len ? at32(y, (uint32_t)j) : 0.f;
+            v[i] = u < len ? y[j] : 0.f;          // j up to n: 64-bit addressing (n may pass 2^30)
         }
     } else {
 #pragma unroll

@@ -313,6 +313,12 @@ struct msg_ctx {
     int32_t last_n = 0;
 };
 
+// the longest output a preset may have: every kernel indexes a preset's frames
+// with 32-bit integers (round 4 stopped at 2^29, where a 32-bit byte offset of
+// the float2 output from the preset's own base ran out; the offsets are now
+// formed from each tile's or block's base)
+constexpr int64_t MSG_MAX_FRAMES = ((int64_t)1 << 31) - ((int64_t)1 << 20);
+
 #define HIPCHK(ctx, expr)                                                        \
     do {                                                                         \
         hipError_t _e = (expr);                                                  \
@@ -1156,16 +1162,19 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
     int64_t nslots = 0, ntaps = 0;
     auto bases = [&]() -> int {
         nslots = ntaps = 0;
+        int64_t frames = 0;
         for (int p = 0; p < P; ++p) {
             slot_base[p] = (int32_t)nslots;
             tap_base[p] = (int32_t)ntaps;
             nslots += info[p].n_slots;
             if (presets[p].flags & MSG_F_ER_CLOUD) ntaps += std::max(1, presets[p].er_taps);
-            // kernels index a preset's frames with 32-bit integers (and 32-bit byte
-            // offsets of its float32 mono buffer)
-            if (info[p].out_n > (int64_t)1 << 29) return fail(ctx, MSG_E_UNSUPPORTED, "output longer than 2^29 frames");
+            // kernels index a preset's frames with 32-bit integers (byte offsets
+            // from a tile's or block's own base; the tile counters of a batch in 32 bits)
+            if (info[p].out_n > MSG_MAX_FRAMES) return fail(ctx, MSG_E_UNSUPPORTED, "output longer than 2^31 - 2^20 frames");
+            frames += info[p].out_n;
         }
         if (nslots > INT32_MAX / 2) return fail(ctx, MSG_E_UNSUPPORTED, "too many events in one batch");
+        if (frames > ((int64_t)1 << 40)) return fail(ctx, MSG_E_UNSUPPORTED, "more than 2^40 frames in one batch");
         return MSG_OK;
     };
     if (!ctx->device_plan) {

@@ -1,0 +1,56 @@
+"""An output longer than 2^29 frames (VERDICT r04 missing #1: round 4 raised
+NotImplementedError there).  The reference computes out_n = round(out_dur *
+base_sr) with no limit (MS:591); a hand-written params dict at 384 kHz passes
+2^29 frames after 23.3 minutes.  One preset of 2^29 + 2^18 frames (no ER / IR,
+Poisson events at 2 / s, so grains land on both sides of frame 2^29) is
+rendered on the device and its summary checked against the NumPy restatement's
+render of the same dict, computed in the container (tools/gen_golden_r5.py,
+tests/golden/long_2e29.json: the render itself is 8.6 GB)."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def device_summary(torch, out, seg):
+    """tools/gen_golden_r5.summary of a device (n, 2) float32 tensor, reduced on the device in float64."""
+    n = int(out.shape[0])
+    d = out.to(torch.float64)
+    b = d[: n - n % seg].abs().reshape(seg, -1, 2).sum(dim=1)
+    return {"out_n": n, "rms": float(torch.sqrt(torch.mean(d * d))), "peak": float(d.abs().max()),
+            "sum_l": float(d[:, 0].sum()), "sum_r": float(d[:, 1].sum()),
+            "rows_every_2e20": d[:: 1 << 20].cpu().numpy(), "seg_abs_sums": b.cpu().numpy()}
+
+
+@pytest.mark.gpu
+def test_output_beyond_2e29_frames():
+    import torch
+    import msgpu
+    from msgpu.engine import default_engine
+    from msgpu.pack import PackedBatch
+    with open(os.path.join(HERE, "golden", "long_2e29.json")) as f:
+        ref = json.load(f)
+    p = msgpu.merged(**ref["params"])
+    packed = PackedBatch([p])
+    n = int(packed.out_n[0])
+    assert n == ref["out_n"] and n > (1 << 29)
+    eng = default_engine(0)
+    out = eng.render_packed(packed)
+    torch.cuda.synchronize(0)
+    s = device_summary(torch, out[:n], ref["seg"])
+    del out
+    rows_ref = np.asarray(ref["rows_every_2e20"])
+    seg_ref = np.asarray(ref["seg_abs_sums"])
+    d = {"rms": abs(s["rms"] - ref["rms"]), "sum_l": abs(s["sum_l"] - ref["sum_l"]) / n,
+         "sum_r": abs(s["sum_r"] - ref["sum_r"]) / n, "peak": abs(s["peak"] - ref["peak"]),
+         "rows": float(np.max(np.abs(s["rows_every_2e20"] - rows_ref))),
+         "seg_rel": float(np.max(np.abs(s["seg_abs_sums"] - seg_ref)) / max(1e-30, float(seg_ref.max())))}
+    active = [i for i, v in enumerate(s["seg_abs_sums"]) if v[0] > 0]
+    print(f"out_n {n}: {d}; active segments device {len(active)} / reference {len(ref['active_segments'])}")
+    assert active == ref["active_segments"]
+    assert max(i for i in active) * (n // ref["seg"]) > (1 << 29)       # grains beyond frame 2^29
+    assert d["rms"] <= 1e-5 and d["sum_l"] <= 1e-5 and d["sum_r"] <= 1e-5 and d["peak"] <= 1e-5
+    assert d["rows"] <= 1e-4 and d["seg_rel"] <= 1e-4
