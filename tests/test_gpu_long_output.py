@@ -51,6 +51,8 @@ def test_output_beyond_2e29_frames():
     active = [i for i, v in enumerate(s["seg_abs_sums"]) if v[0] > 0]
     print(f"out_n {n}: {d}; active segments device {len(active)} / reference {len(ref['active_segments'])}")
     assert active == ref["active_segments"]
-    assert max(i for i in active) * (n // ref["seg"]) > (1 << 29)       # grains beyond frame 2^29
+    seg_len = n // ref["seg"]
+    assert (max(active) + 1) * seg_len > (1 << 29)                        # grains beyond frame 2^29
+    assert float(s["seg_abs_sums"][-1][0]) > 0.0
     assert d["rms"] <= 1e-5 and d["sum_l"] <= 1e-5 and d["sum_r"] <= 1e-5 and d["peak"] <= 1e-5
     assert d["rows"] <= 1e-4 and d["seg_rel"] <= 1e-4
