@@ -648,6 +648,89 @@ k_fir4_hpart(const PresetRt* __restrict__ rt, const int2* __restrict__ jobs, con
     }
 }
 
+// One-partition spectra at N = 2M straight from the taps, the k_fir8_hconv
+// recipe on the k_fir4 engine (round 5; H48's 48 kHz filters: k_h_build's
+// float64 time-domain h was 0.21 of the h stage's 0.26 ms per 1024 presets):
+//   k_fir4_irspec  S = rfft_N(IR) of each IR of the batch (float64 bank, the
+//                  8192-tap cap), jobs (src offset, length, spectrum offset, -);
+//   k_fir4_hconv   H = rfft_N(delta + ER taps) . S for a preset whose h =
+//                  (delta + ER) * IR fits the transform (h_len <= N: the circular
+//                  product is the linear convolution), one workgroup per preset;
+//                  the taps are scattered into LDS as the packed input.
+// Spectra in natural bin order, M + 1 float2 (k_fir4's hspec layout).
+template <int M>
+MSG_DEV void fir4_store_spec(const float2 (&v)[2][Fir4Geo<M>::R4], const float2* __restrict__ S, float2* __restrict__ H) {
+    constexpr int R4 = Fir4Geo<M>::R4, NB4 = Fir4Geo<M>::NB4;
+    const int t = otid();
+    auto put = [&](int k, float2 x) { at32(H, (uint32_t)k) = S ? cmul(x, at32(S, (uint32_t)k)) : x; };
+    if (t != 0) {
+#pragma unroll
+        for (int k = 0; k < R4; ++k) {
+            const int kA = t + k * NB4;
+            put(kA, v[0][k]);
+            put(M - kA, v[1][R4 - 1 - k]);
+        }
+    } else {   // thread 0's slot layout (fir4s_forward): (X[0], X[M]) packed, X[M/2]
+#pragma unroll
+        for (int k = 0; k < R4 - 1; ++k) {
+            const int kA = fir_k0<M, R4>(k);
+            put(kA, v[0][k]);
+            put(M - kA, v[1][R4 - 1 - k]);
+        }
+        put(0, make_float2(v[0][R4 - 1].x, 0.f));
+        put(M, make_float2(v[0][R4 - 1].y, 0.f));
+        put(M / 2, v[1][0]);
+    }
+}
+
+template <int M>
+__global__ void __launch_bounds__(Fir4Geo<M>::T)
+k_fir4_irspec(const int64_t* __restrict__ jobs, const float2* __restrict__ tables, const double* __restrict__ src,
+              float2* __restrict__ hspec) {
+    using G = Fir4Geo<M>;
+    constexpr int T = G::T;
+    extern __shared__ __attribute__((aligned(16))) float2 lds[];
+    float2* tab = lds;
+    float2* buf = lds + G::TAB;
+    const int64_t* j = jobs + 4 * blockIdx.x;
+    const double* x = src + j[0];
+    const int64_t len = j[1];
+    { TabCopy<G::TAB_USED, T> tc; tc.fetch(tables); tc.put(tab); }
+    for (int m = threadIdx.x; m < M; m += T) {                 // packed z[m] = x[2m] + i x[2m + 1], zero-padded
+        const int64_t i = 2 * (int64_t)m;
+        buf[m] = make_float2(i < len ? (float)x[i] : 0.f, i + 1 < len ? (float)x[i + 1] : 0.f);
+    }
+    __syncthreads();
+    float2 v[2][G::R4];
+    fir4s_forward<M, true>(buf, tab, nullptr, 0, 0, v);
+    fir4_store_spec<M>(v, nullptr, hspec + j[2]);
+}
+
+template <int M>
+__global__ void __launch_bounds__(Fir4Geo<M>::T)
+k_fir4_hconv(const PresetRt* __restrict__ rt, const int32_t* __restrict__ list, const float2* __restrict__ tables,
+             const int32_t* __restrict__ er_off, const double* __restrict__ er_gain, float2* __restrict__ hspec) {
+    using G = Fir4Geo<M>;
+    constexpr int T = G::T;
+    extern __shared__ __attribute__((aligned(16))) float2 lds[];
+    float2* tab = lds;
+    float2* buf = lds + G::TAB;
+    const PresetRt& r = rt[list[blockIdx.x]];
+    { TabCopy<G::TAB_USED, T> tc; tc.fetch(tables); tc.put(tab); }
+    for (int m = threadIdx.x; m < M; m += T) buf[m] = make_float2(0.f, 0.f);
+    __syncthreads();
+    // e = delta + taps at real index o (the host merged equal offsets: a slot holds the
+    // delta and at most one tap, and two float adds give the same sum in either order)
+    float* e = reinterpret_cast<float*>(buf);
+    if (threadIdx.x == 0) atomicAdd(e, 1.0f);
+    for (int k = threadIdx.x; k < r.n_taps; k += T)
+        atomicAdd(e + er_off[r.er_base + k], (float)er_gain[r.er_base + k]);
+    __syncthreads();
+    float2 v[2][G::R4];
+    fir4s_forward<M, true>(buf, tab, nullptr, 0, 0, v);
+    fir4_store_spec<M>(v, r.ir_len > 0 ? hspec + r.irs_off : nullptr, hspec + r.h_off);
+}
+
 // Host: the twiddle tables of Fir4Geo<M> (float64-built, rounded once).
 template <int M>
 inline void fir4_tables(std::vector<float>& out) {

@@ -29,6 +29,7 @@
 // per half so the MAC reads are unit-stride.
 #pragma once
 #include "fir4_fft.h"
+#include "ola.h"
 
 // Phase timing (debug builds with -DMSG_STAMPS, tools/fir8_stamps.py): block-summed
 // wall-clock deltas per phase of k_fir8, read back with msg_debug_stamps_fir.
@@ -214,6 +215,89 @@ MSG_DEV void load_halves(const float* __restrict__ x, int64_t n, int64_t s0, flo
     }
 }
 
+// ---------------------------------------------------------------------------
+// The overlap-add fused into the segment load (PresetRt::ola_fir): x[s0, s0 + N)
+// is summed from the placed grains (MS:742-764) instead of read from a mono
+// buffer k_ola_env wrote, one half of the segment at a time through buf.  The
+// arithmetic is ola_tile's (kernels_core.h): per frame, fmaf over the events in
+// event order from 0.f, times the ADSR, so the FIR's input is the same bits.
+// Wave w owns frames [w OLA_CHUNK, (w + 1) OLA_CHUNK) of each half, lane l the
+// frames l + 64 j: a grain's reads are coalesced over the wave, and one event
+// puts up to OLA_J loads per lane in flight.
+// ---------------------------------------------------------------------------
+constexpr int OLA_J = M / T;                  // frames per lane per half (32)
+constexpr int OLA_CHUNK = 64 * OLA_J;         // frames per wave per half
+
+// the half [c0, c0 + M) of the segment (absolute frames) into xf[0, M)
+MSG_DEV void ola_half(const msg_event* __restrict__ ev, const PresetRt& pr, const float* __restrict__ grain_pool,
+                      int lo, int64_t c0, float* xf) {
+    const int t = otid();
+    const int lane = t & 63, w = t >> 6;
+    const int64_t w0 = c0 + (int64_t)w * OLA_CHUNK, w1 = w0 + OLA_CHUNK;
+    const int ne = pr.n_events;
+    float acc[OLA_J];
+#pragma unroll
+    for (int j = 0; j < OLA_J; ++j) acc[j] = 0.f;
+    for (int k0 = lo; k0 < ne; k0 += 64) {
+        const int k = k0 + lane;
+        int s = INT32_MAX, L = 0;
+        float amp = 0.f;
+        int64_t goff = 0;
+        if (k < ne) {
+            const msg_event& e = ev[k];
+            s = e.start; L = e.len; amp = (float)e.amp;
+            goff = pr.pool_base + e.pool_off + e.offset;
+        }
+        const uint64_t before = __ballot(s < w1);           // sorted: a prefix of the lanes
+        uint64_t live = before & __ballot(L > 0 && (int64_t)s + L > w0);
+        while (live) {                                      // in event order
+            const int i = __builtin_ctzll(live);
+            live &= live - 1;
+            const int si = __builtin_amdgcn_readlane(s, i);
+            const uint32_t Li = (uint32_t)__builtin_amdgcn_readlane(L, i);
+            const float av = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(amp), i));
+            const int64_t gi = ((int64_t)__builtin_amdgcn_readlane((int)(goff >> 32), i) << 32) |
+                               (uint32_t)__builtin_amdgcn_readlane((int)goff, i);
+            const float* g = grain_pool + gi;
+            const int q0 = (int)(w0 - si) + lane;           // in (-OLA_CHUNK, L): the event meets the chunk
+            float gv[OLA_J];
+#pragma unroll
+            for (int j = 0; j < OLA_J; ++j) {
+                const int q = q0 + 64 * j;
+                gv[j] = (uint32_t)q < Li ? g[q] : 0.f;
+            }
+#pragma unroll
+            for (int j = 0; j < OLA_J; ++j)
+                if ((uint32_t)(q0 + 64 * j) < Li) acc[j] = fmaf(av, gv[j], acc[j]);
+        }
+        if (before != ~0ull) break;
+    }
+    const int64_t n = pr.out_n;
+#pragma unroll
+    for (int j = 0; j < OLA_J; ++j) {
+        const int64_t f = w0 + lane + 64 * j;
+        xf[w * OLA_CHUNK + lane + 64 * j] = (f >= 0 && f < n) ? acc[j] * adsr_at(pr, (int)f) : 0.f;
+    }
+}
+
+// load_halves for an ola_fir preset: the segment x[s0, s0 + N) summed in buf
+MSG_DEV void ola_halves(const msg_event* __restrict__ ev, const PresetRt& pr, const float* __restrict__ grain_pool,
+                        int64_t s0, float2* buf, float2 (&a)[R1], float2 (&b)[R1]) {
+    const int t = otid();
+    // events that can reach s0 start after s0 - max_n (every wave finds the same lo)
+    const int lo = events_starting_by(ev, pr.n_events, s0 - (int64_t)pr.max_n);
+    float* xf = reinterpret_cast<float*>(buf);        // free: inv_half ends on a barrier
+    ola_half(ev, pr, grain_pool, lo, s0, xf);
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < R1; ++r) a[r] = buf[t + r * NB1];
+    __syncthreads();
+    ola_half(ev, pr, grain_pool, lo, s0 + M, xf);
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < R1; ++r) b[r] = buf[t + r * NB1];
+}
+
 // (a, b) <- (a + b, (a - b) W_M^(t + r NB1))
 MSG_DEV void dif_split(const float2* tab, float2 (&a)[R1], float2 (&b)[R1]) {
     const float2 wt = fir4_wM(tab, G::OFF_PLO, G::OFF_PHI, otid());   // W_M^t (PLO/PHI: W_{2 MH} = W_M)
@@ -314,7 +398,8 @@ template <int UNUSED = 0>
 __global__ void __launch_bounds__(fir8::T)
 k_fir8p(const PresetRt* __restrict__ rt, const int2* __restrict__ jobs, int n_jobs, const float2* __restrict__ tables,
         const float2* __restrict__ hspec, const float* __restrict__ x_in, float* __restrict__ y_out,
-        int32_t* __restrict__ ctr, int stagger) {
+        int32_t* __restrict__ ctr, int stagger, const msg_event* __restrict__ events,
+        const float* __restrict__ grain_pool) {
     using namespace fir8;
     extern __shared__ __attribute__((aligned(16))) float2 lds[];
     __shared__ int s_take[2];
@@ -360,7 +445,10 @@ k_fir8p(const PresetRt* __restrict__ rt, const int2* __restrict__ jobs, int n_jo
         const int64_t n = pr.out_n;
         const int64_t t0 = (int64_t)job.y * pr.fir_B;
         float2 a[R1], b[R1];
-        load_halves(x_in + pr.y_off, n, t0 - (P - 1), a, b);
+        if (__builtin_amdgcn_readfirstlane(pr.ola_fir))
+            ola_halves(events + pr.ev_begin, pr, grain_pool, t0 - (P - 1), buf, a, b);
+        else
+            load_halves(x_in + pr.y_off, n, t0 - (P - 1), a, b);
         if (t == 0) s_take[par] = atomicAdd(ctr + xr * FIR8P_CTR, 1);   // the block after this one
         dif_split(tab, a, b);
         FIR_STAMP(0);

@@ -21,6 +21,10 @@ void fir_init_attrs() {
                               Fir4Geo<16384>::LDS_BYTES);
     (void)hipFuncSetAttribute((const void*)k_fir4s<16384>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               Fir4Geo<16384>::LDS_BYTES);
+    (void)hipFuncSetAttribute((const void*)k_fir4_hconv<16384>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              Fir4Geo<16384>::LDS_BYTES);
+    (void)hipFuncSetAttribute((const void*)k_fir4_irspec<16384>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              Fir4Geo<16384>::LDS_BYTES);
     (void)hipFuncSetAttribute((const void*)k_fir4_hpart<16384>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               Fir4Geo<16384>::LDS_BYTES);
     (void)hipFuncSetAttribute((const void*)k_fir8<0>, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -122,6 +126,20 @@ hipError_t launch_fir4_hpart(int M, unsigned n_parts, hipStream_t s, const Prese
     return hipGetLastError();
 }
 
+hipError_t launch_fir4_hconv(unsigned n_presets, hipStream_t s, const PresetRt* rt, const int32_t* list,
+                             const float2* tables, const int32_t* er_off, const double* er_gain, float2* hspec) {
+    hipLaunchKernelGGL((k_fir4_hconv<16384>), dim3(n_presets), dim3(Fir4Geo<16384>::T), Fir4Geo<16384>::LDS_BYTES, s,
+                       rt, list, tables, er_off, er_gain, hspec);
+    return hipGetLastError();
+}
+
+hipError_t launch_fir4_irspec(unsigned n_jobs, hipStream_t s, const int64_t* jobs, const float2* tables,
+                              const double* src, float2* hspec) {
+    hipLaunchKernelGGL((k_fir4_irspec<16384>), dim3(n_jobs), dim3(Fir4Geo<16384>::T), Fir4Geo<16384>::LDS_BYTES, s,
+                       jobs, tables, src, hspec);
+    return hipGetLastError();
+}
+
 hipError_t launch_fir8(unsigned grid, hipStream_t s, const PresetRt* rt, const int2* jobs, const float2* tables,
                        const float2* hspec, const float* x_in, float* y_out) {
     hipLaunchKernelGGL((k_fir8<0>), dim3(grid), dim3(fir8::T), Fir4Geo<16384>::LDS_BYTES, s, rt, jobs, tables, hspec,
@@ -134,9 +152,9 @@ hipError_t launch_fir8(unsigned grid, hipStream_t s, const PresetRt* rt, const i
 // launch; each launch leaves them zero)
 hipError_t launch_fir8p(unsigned n_jobs, unsigned grid, hipStream_t s, const PresetRt* rt, const int2* jobs,
                         const float2* tables, const float2* hspec, const float* x_in, float* y_out, int32_t* ctr,
-                        int stagger) {
+                        int stagger, const msg_event* events, const float* grain_pool) {
     hipLaunchKernelGGL((k_fir8p<0>), dim3(grid), dim3(fir8::T), Fir4Geo<16384>::LDS_BYTES, s, rt, jobs, (int)n_jobs,
-                       tables, hspec, x_in, y_out, ctr, stagger);
+                       tables, hspec, x_in, y_out, ctr, stagger, events, grain_pool);
     return hipGetLastError();
 }
 

@@ -7,9 +7,13 @@ void fir64_init_attrs() {
     (void)hipFuncSetAttribute((const void*)k_fir64, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
 }
 
-hipError_t launch_fir64(const Fir64Launch& a, hipStream_t s) {
+hipError_t launch_fir64_flag(const Fir64Launch& a, hipStream_t s) {
     hipLaunchKernelGGL(k_fir64_flag, dim3(1), dim3(64), 0, s, a.n_presets, a.flag64, a.maxbits, a.slot_preset,
                        a.n_slots);
+    return hipGetLastError();
+}
+
+hipError_t launch_fir64(const Fir64Launch& a, hipStream_t s) {
     // small persistent grids: with no flagged preset every workgroup exits at once,
     // and one waiting for a CU held by another stream's kernel delays little
     for (int w0 = 0; w0 < a.n_cand; w0 += a.cap) {

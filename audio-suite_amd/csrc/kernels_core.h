@@ -1,6 +1,7 @@
 // kernels_core.h — planner, generator, overlap-add and stereo kernels (TU: msgpu.hip).
 #pragma once
 #include "rt.h"
+#include "ola.h"
 #include <type_traits>
 
 // ---------------------------------------------------------------------------
@@ -624,40 +625,6 @@ k_gen_normal(const msg_preset* __restrict__ presets, const msg_event* __restrict
 // ---------------------------------------------------------------------------
 // Overlap-add of placed grains (event order) x ADSR -> mono a[t].
 // ---------------------------------------------------------------------------
-// x^c for x in [0, 1] (hardware log2/exp2; exact at 0 and 1)
-MSG_DEV float env_pow(float x, float c) { return x > 0.f ? exp2f(c * __log2f(x)) : 0.f; }
-
-// make_adsr (MS:172-195) at frame t < n; region bounds and reciprocals precomputed on the host
-MSG_DEV float adsr_at(const PresetRt& r, int t) {
-    const float c = r.envC, S = r.envS;
-    if (t < r.envA) return env_pow((float)t * r.envInvA, c);
-    if (t < r.envJ) return 1.0f - (1.0f - S) * env_pow((float)(t - r.envA) * r.envInvD, c);
-    if (t < r.envS1) return S;
-    const int n = (int)r.out_n;
-    const float u = (n - r.envS1 == 1) ? 0.f : (t == n - 1 ? 1.f : (float)(t - r.envS1) * r.envInvR);
-    return S * (1.0f - env_pow(u, c));
-}
-
-// Number of events (sorted by start) with start <= lim: a 64-ary ballot search,
-// one dependent load for up to 64 events instead of a log2 n binary search.
-// Call from every lane of a wave.
-MSG_DEV int events_starting_by(const msg_event* __restrict__ ev, int n, int64_t lim) {
-    const int lane = (int)(threadIdx.x & 63);
-    int lo = 0, len = n;
-    while (len > 0) {
-        const int step = (len + 63) >> 6;
-        const int nseg = (len + step - 1) / step;
-        const int last = min((lane + 1) * step, len) - 1;       // last element of this lane's segment
-        const bool ok = lane < nseg && (int64_t)ev[lo + last].start <= lim;
-        const int c = __popcll(__ballot(ok));                   // sorted: a prefix of the segments
-        if (c == nseg) { lo += len; break; }
-        lo += c * step;
-        if (step == 1) break;
-        len = min(step, len - c * step) - 1;                    // segment c ends above lim
-    }
-    return lo;
-}
-
 // Traversal order against the Infinity Cache (tuning A/B): MSG_OLA_REV = 1
 // walks each XCD's job range backwards, so overlap-add starts on the most
 // recently written end of the spectral kernel's grains (measured neutral,
@@ -670,14 +637,10 @@ MSG_DEV int job_order(int rev) {
     return rev ? (int)gridDim.x - 1 - b : b;
 }
 
-__global__ void __launch_bounds__(OLA_T)
-k_ola_env(const msg_event* __restrict__ events, const PresetRt* __restrict__ rt,
-          const int32_t* __restrict__ tile_begin, int n_presets,
-          const float* __restrict__ grain_pool, float* __restrict__ mono) {
-    const int b = job_order(MSG_OLA_REV);
-    const int p = find_preset(tile_begin, n_presets, b);
-    const PresetRt& r = rt[p];
-    const int64_t t0 = (int64_t)(b - r.tile_begin) * OLA_TILE;
+// One OLA_TILE tile [t0, t0 + OLA_TILE) of preset r: the placed grains in event
+// order times the ADSR (MS:742-764), into its mono buffer.
+MSG_DEV void ola_tile(const msg_event* __restrict__ events, const PresetRt& r, int64_t t0,
+                      const float* __restrict__ grain_pool, float* __restrict__ mono) {
     const int64_t t1 = t0 + OLA_TILE < r.out_n ? t0 + OLA_TILE : r.out_n;
     constexpr int PER = OLA_TILE / OLA_T;
     const int lane = threadIdx.x & 63;
@@ -738,5 +701,31 @@ k_ola_env(const msg_event* __restrict__ events, const PresetRt* __restrict__ rt,
     for (int u = 0; u < PER; ++u) {
         const int t = (int)t0 + (int)threadIdx.x + u * OLA_T;
         if (t < t1) y[t] = acc[u] * adsr_at(r, t);
+    }
+}
+
+__global__ void __launch_bounds__(OLA_T)
+k_ola_env(const msg_event* __restrict__ events, const PresetRt* __restrict__ rt,
+          const int32_t* __restrict__ tile_begin, int n_presets,
+          const float* __restrict__ grain_pool, float* __restrict__ mono) {
+    const int b = job_order(MSG_OLA_REV);
+    const int p = find_preset(tile_begin, n_presets, b);
+    const PresetRt& r = rt[p];
+    ola_tile(events, r, (int64_t)(b - r.tile_begin) * OLA_TILE, grain_pool, mono);
+}
+
+// The overlap-add of the float64 FIR's slots (kernels_fir64.h) among the presets
+// whose overlap-add runs inside k_fir8p (ola_fir): the float64 FIR reads their
+// mono a, which k_fir8p never writes.  A grid-stride walk over (slot, tile).
+__global__ void __launch_bounds__(OLA_T)
+k_ola_slots(const msg_event* __restrict__ events, const PresetRt* __restrict__ rt,
+            const int32_t* __restrict__ slot_preset, const int32_t* __restrict__ n_slots, int tmax,
+            const float* __restrict__ grain_pool, float* __restrict__ mono) {
+    const int ns = *n_slots;
+    for (int j = blockIdx.x; j < ns * tmax; j += gridDim.x) {
+        const int sl = j / tmax, t = j - sl * tmax;
+        const PresetRt& r = rt[__builtin_amdgcn_readfirstlane(slot_preset[sl])];
+        if (!r.ola_fir || (int64_t)t * OLA_TILE >= r.out_n) continue;   // uniform
+        ola_tile(events, r, (int64_t)t * OLA_TILE, grain_pool, mono);
     }
 }

@@ -52,6 +52,8 @@ struct Fir64Launch {
     const float* x; float* y;
 };
 void fir64_init_attrs();
+// k_fir64_flag: the flagged presets into slot_preset / n_slots; then the windows
+hipError_t launch_fir64_flag(const Fir64Launch& a, hipStream_t s);
 hipError_t launch_fir64(const Fir64Launch& a, hipStream_t s);
 hipError_t launch_ir_spec(unsigned grid, int lds_bytes, hipStream_t s, const int64_t* jobs, int n_jobs,
                           const RealPlan* fir_plans, const double* ir_bank, float2* ir_spec);
@@ -79,6 +81,12 @@ constexpr int FIR4S_P = 16384;
 // partition spectra on the k_fir4 engine (fir4_fft.h): k_fir4_hpart over the (preset, q) jobs
 hipError_t launch_fir4_hpart(int M, unsigned n_parts, hipStream_t s, const PresetRt* rt, const int2* part_jobs,
                              const float2* tables, const float* hs, float2* hspec);
+// one-partition spectra at N = 32768 from the taps (fir4_fft.h): S = rfft(IR) per job
+// [src off, len, spec off, 0] of the float64 bank; H = rfft(delta + ER taps) . S per listed preset
+hipError_t launch_fir4_hconv(unsigned n_presets, hipStream_t s, const PresetRt* rt, const int32_t* list,
+                             const float2* tables, const int32_t* er_off, const double* er_gain, float2* hspec);
+hipError_t launch_fir4_irspec(unsigned n_jobs, hipStream_t s, const int64_t* jobs, const float2* tables,
+                              const double* src, float2* hspec);
 // N = 65536 overlap-save, one partition (fir8_fft.h): blocks on the k_fir4 engine in
 // two halves.  Spectra (even/odd bin layout, N/2 + 1 float2): k_fir8_hconv per listed
 // ER preset (rfft(delta + taps) . S_IR), k_fir8_spec per job [src off, len, spec off, 0]
@@ -88,7 +96,7 @@ hipError_t launch_fir8(unsigned grid, hipStream_t s, const PresetRt* rt, const i
                        const float2* hspec, const float* x_in, float* y_out);
 hipError_t launch_fir8p(unsigned n_jobs, unsigned grid, hipStream_t s, const PresetRt* rt, const int2* jobs,
                         const float2* tables, const float2* hspec, const float* x_in, float* y_out, int32_t* ctr,
-                        int stagger);
+                        int stagger, const msg_event* events, const float* grain_pool);
 hipError_t launch_fir8_hconv(unsigned n_presets, hipStream_t s, const PresetRt* rt, const int32_t* list,
                              const float2* tables, const int32_t* er_off, const double* er_gain, float2* hspec);
 hipError_t launch_fir8_spec64(unsigned n_jobs, hipStream_t s, const int64_t* jobs, const float2* tables,

@@ -191,6 +191,7 @@ struct msg_ctx {
     // msg_stage_times -- profiling never makes the host wait for the last batch
     bool pending[2] = {false, false};
     bool pending_fir[2] = {false, false};
+    bool pending_h_early[2] = {false, false};
     int ev_cur = 0;
     double stage_sum[10] = {0};   // accumulated stage times since msg_set_profiling(ctx, 1)
     int64_t stage_cnt = 0;
@@ -198,7 +199,7 @@ struct msg_ctx {
     // plan sizes, plan events + tap merge, preset records, event records, lists + buffers
     double host_sum[8] = {0};
     int64_t host_cnt = 0;
-    hipEvent_t ev[2][10] = {};
+    hipEvent_t ev[2][12] = {};
     bool device_plan = false;     // MSGPU_DEVICE_PLAN=1: plan on the device (k_plan_*), read back
     Staging staging;              // pinned uploads of a batch
     // constant tables
@@ -208,6 +209,8 @@ struct msg_ctx {
     float2* d_fir2tab[5] = {};   // k_fir2 twiddle tables, M = 1024 << i
     float2* d_fir4tab = nullptr; // k_fir4 twiddle tables (M = 16384)
     bool fir4 = true;            // M = 16384 blocks on k_fir4 (MSGPU_FIR4=0: k_fir2, A/B and tests)
+    // one-partition k_fir4 spectra from the taps (k_fir4_hconv; MSGPU_FIR4C=0: k_h_build + k_fir4_hpart)
+    bool fir4c = true;
     bool fir8 = true;            // N = 65536 one-partition filters on k_fir8 (MSGPU_FIR8=0: off, A/B and tests)
     int fir64 = 1;               // float64 FIR of saturated renders: 0 off, 1 predicted, 2 every FIR preset (MSGPU_FIR64)
     // k_fir8 blocks (MSGPU_FIR8P): 0 one workgroup per block, 1 persistent workgroups
@@ -217,6 +220,14 @@ struct msg_ctx {
     int n_cu = 256;              // compute units (persistent grids)
     int fir8p_cus = 0;           // persistent FIR workgroups (MSGPU_FIR8P_CUS, A/B; 0: one per CU)
     int fir8p_stagger = 0;       // k_fir8p: every other workgroup starts this many 10-ns ticks later (MSGPU_FIR8P_STAGGER)
+    // overlap-add inside k_fir8p's loads (PresetRt::ola_fir) for presets whose
+    // placed grains total at most ola_fir_density x out_n frames (MSGPU_OLA_FIR=0: never)
+    bool ola_fir = true;
+    // filter spectra before the generator (MSGPU_H_EARLY): 0 at the FIR stage, 1 always,
+    // 2 (default) for batches with an output of at least 2^22 frames, whose FIR
+    // holds every CU for milliseconds (C5 -2.5 %); shorter ones lose by it (C3 +2 %)
+    int h_early = 2;
+    double ola_fir_density = 1.25;
     // Q <= 2 presets on the streaming k_fir4s (MSGPU_FIR4S=1; off by default: at
     // C3's 24 blocks per preset its H re-reads miss L2 and cancel the saved transforms)
     bool fir4s = false;
@@ -253,6 +264,8 @@ struct msg_ctx {
     DevBuf<float> hscratch;                     // h of every FIR preset (k_h_build -> k_fir_h / k_fir4_hpart)
     Slice<int32_t> h_tile_begin, fir8_list;
     Slice<int64_t> ir8_jobs;
+    Slice<int32_t> fir4c_list;                  // k_fir4_hconv presets (one partition at N = 32768)
+    Slice<int64_t> ir4_jobs;                    // k_fir4_irspec jobs
     Slice<int2> hpart_jobs;
     Slice<int2> fir_jobs;
     Slice<int32_t> spec_ct_list;
@@ -710,11 +723,15 @@ msg_ctx* msg_create(int device_ordinal) {
         }
     }
     if (const char* e = getenv("MSGPU_FIR4")) ctx->fir4 = e[0] != '0';
+    if (const char* e = getenv("MSGPU_FIR4C")) ctx->fir4c = e[0] != '0';
     if (const char* e = getenv("MSGPU_FIR8")) ctx->fir8 = e[0] != '0';
     if (const char* e = getenv("MSGPU_FIR64")) ctx->fir64 = atoi(e);
     if (const char* e = getenv("MSGPU_FIR8P")) ctx->fir8p = atoi(e);
     if (const char* e = getenv("MSGPU_FIR8P_CUS")) ctx->fir8p_cus = std::max(0, atoi(e));
     if (const char* e = getenv("MSGPU_FIR8P_STAGGER")) ctx->fir8p_stagger = std::max(0, atoi(e));
+    if (const char* e = getenv("MSGPU_OLA_FIR")) ctx->ola_fir = e[0] != '0';
+    if (const char* e = getenv("MSGPU_H_EARLY")) ctx->h_early = atoi(e);
+    if (const char* e = getenv("MSGPU_OLA_FIR_DENSITY")) ctx->ola_fir_density = atof(e);
     if (const char* e = getenv("MSGPU_STEREO_FUSED")) ctx->stereo_fused = e[0] != '0';
     if (const char* e = getenv("MSGPU_STEREO_WGS")) ctx->st_wgs = std::max(1, std::min(16, atoi(e)));
     {
@@ -812,9 +829,14 @@ static void collect_stage_set(msg_ctx* ctx, int k) {
     float ms[10] = {0};
     for (int i = 0; i < 7; ++i) hipEventElapsedTime(&ms[i], ev[i], ev[i + 1]);
     hipEventElapsedTime(&ms[7], ev[0], ev[7]);
-    if (ctx->pending_fir[k]) {   // the FIR kernel alone, and the h build before it
+    if (ctx->pending_fir[k]) {   // the FIR kernel alone, and the filter spectra
         hipEventElapsedTime(&ms[8], ev[8], ev[9]);
-        hipEventElapsedTime(&ms[9], ev[5], ev[8]);
+        if (ctx->pending_h_early[k]) {   // launched before the generator: out of host_prep
+            hipEventElapsedTime(&ms[9], ev[10], ev[11]);
+            hipEventElapsedTime(&ms[1], ev[1], ev[10]);
+        } else {
+            hipEventElapsedTime(&ms[9], ev[5], ev[8]);
+        }
     }
     for (int i = 0; i < 10; ++i) ctx->stage_sum[i] += ms[i];
     ++ctx->stage_cnt;
@@ -1326,6 +1348,8 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
     }
     int64_t pool = 0, ysum = 0, hsum = 0;
     int32_t tiles = 0, fblocks = 0, hblocks = 0, stiles = 0;
+    int n_ola_fir = 0;                               // presets with PresetRt::ola_fir
+    int64_t ola_fir_nmax = 0;                        // their longest output
     std::vector<int2> hpart_jobs;                  // (preset, q) of the presets on the k_fir4 engine
     std::vector<int32_t> h_tile_begin(P, 0);       // k_h_build tiles per preset (prefix)
     int32_t htiles = 0;
@@ -1349,6 +1373,11 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
     std::map<int, int64_t> ir8_spec_of;                   // IR index -> spectrum offset (before relocation)
     std::vector<int64_t> ir8_jobs;                        // k_fir8_spec jobs: [ir_off, len, spec_off, 0]
     int64_t ir8_sum = 0;
+    // the same at N = 32768 on the k_fir4 engine (k_fir4_hconv / k_fir4_irspec, MSGPU_FIR4C)
+    std::vector<int32_t> fir4c_list, ir_only4;
+    std::map<int, int64_t> ir4_spec_of;
+    std::vector<int64_t> ir4_jobs;
+    int64_t ir4_sum = 0;
     std::vector<int2> fir4s_presets;                      // (preset, blocks) on the streaming FIR
     // float64 grain chain records
     std::vector<Ev64> ev64;
@@ -1512,6 +1541,28 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
                     r.h_off = irs;                 // relocated past the per-preset spectra below
                     ir_only8.push_back(p);
                 }
+            } else if (N == 2 * 16384 && ctx->fir4 && ctx->fir4c && Q == 1 && M <= N) {
+                // one partition on k_fir4: the k_fir8_hconv recipe at N = 32768 (fir4_fft.h),
+                // H = rfft(delta + ER taps) . S_IR, or S_IR itself for an IR-only preset
+                r.h_fir4 = 3;
+                const bool er = (pr.flags & MSG_F_ER_CLOUD) != 0;
+                int64_t irs = -1;
+                if (r.ir_len > 0) {
+                    auto it = ir4_spec_of.find(pr.ir_conv);
+                    if (it == ir4_spec_of.end()) {
+                        it = ir4_spec_of.emplace(pr.ir_conv, ir4_sum).first;
+                        ir4_jobs.insert(ir4_jobs.end(), {r.ir_off, (int64_t)r.ir_len, ir4_sum, 0});
+                        ir4_sum += N / 2 + 1;
+                    }
+                    irs = it->second;
+                }
+                if (er) {
+                    r.irs_off = irs;
+                    fir4c_list.push_back(p);
+                } else {
+                    r.h_off = irs;                 // relocated past the per-preset spectra below
+                    ir_only4.push_back(p);
+                }
             } else {                               // h in the time domain (k_h_build), cut into partitions
                 r.hs_off = hs_sum;
                 hs_sum += (M + 3) & ~int64_t(3);    // 16-byte aligned h regions
@@ -1522,6 +1573,14 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
                 }
             }
             const int32_t nblk = (int32_t)((inf.out_n + r.fir_B - 1) / r.fir_B);
+            // the overlap-add in k_fir8p's segment loads: each segment sums its grains
+            // again (N / B ~ 1.6 times per frame), worth it while the grains are sparse
+            if (N == FIR8_N && !stream && ctx->fir8p > 0 && ctx->ola_fir &&
+                (double)inf.pool_len <= ctx->ola_fir_density * (double)inf.out_n) {
+                r.ola_fir = 1;
+                n_ola_fir++;
+                ola_fir_nmax = std::max<int64_t>(ola_fir_nmax, inf.out_n);
+            }
             if (stream) {
                 fir4s_presets.push_back(make_int2(p, nblk));   // jobs cut once the batch's total is known
             } else {
@@ -1531,7 +1590,7 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
             fblocks += nblk;
             hblocks += Q;
             if (!r.h_fir4) hblocks_gen += Q;
-            if (!(N == FIR8_N && r.ir_len > 0 && !(pr.flags & MSG_F_ER_CLOUD)))
+            if (!((N == FIR8_N || r.h_fir4 == 3) && r.ir_len > 0 && !(pr.flags & MSG_F_ER_CLOUD)))
                 hsum += (int64_t)Q * (N / 2 + 1);
         } else {
             h_tile_begin[p] = htiles;
@@ -1574,7 +1633,7 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
                 f64_stmax = std::max(f64_stmax, f.st_tiles);
             }
         }
-        tiles += (int32_t)((inf.out_n + OLA_TILE - 1) / OLA_TILE);
+        if (!r.ola_fir) tiles += (int32_t)((inf.out_n + OLA_TILE - 1) / OLA_TILE);
         pool += (inf.pool_len + 3) & ~int64_t(3);   // 16-byte aligned grain regions (float4 loads)
         ysum += (inf.out_n + 3) & ~int64_t(3);   // keep every mono region 16-byte aligned
         // events
@@ -1798,7 +1857,12 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
         if (prt[p].ir_len > 0) prt[p].irs_off += hsum;
     for (int p : ir_only8) prt[p].h_off += hsum;
     for (size_t j = 0; j < ir8_jobs.size(); j += 4) ir8_jobs[j + 2] += hsum;
-    HIPCHK(ctx, ctx->hspec.ensure(hsum + ir8_sum));
+    // then the k_fir4_hconv presets' IR spectra
+    for (int p : fir4c_list)
+        if (prt[p].ir_len > 0) prt[p].irs_off += hsum + ir8_sum;
+    for (int p : ir_only4) prt[p].h_off += hsum + ir8_sum;
+    for (size_t j = 0; j < ir4_jobs.size(); j += 4) ir4_jobs[j + 2] += hsum + ir8_sum;
+    HIPCHK(ctx, ctx->hspec.ensure(hsum + ir8_sum + ir4_sum));
     HIPCHK(ctx, ctx->hscratch.ensure(hs_sum));
     HIPCHK(ctx, ctx->maxbits.ensure(P));
     auto h2d = [&](auto** dst, const auto* src, size_t bytes) -> hipError_t {
@@ -1830,6 +1894,8 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
     HIPCHK(ctx, h2d(&ctx->h_tile_begin.p, h_tile_begin.data(), sizeof(int32_t) * P));
     HIPCHK(ctx, h2d(&ctx->fir8_list.p, fir8_list.data(), sizeof(int32_t) * fir8_list.size()));
     HIPCHK(ctx, h2d(&ctx->ir8_jobs.p, ir8_jobs.data(), sizeof(int64_t) * ir8_jobs.size()));
+    HIPCHK(ctx, h2d(&ctx->fir4c_list.p, fir4c_list.data(), sizeof(int32_t) * fir4c_list.size()));
+    HIPCHK(ctx, h2d(&ctx->ir4_jobs.p, ir4_jobs.data(), sizeof(int64_t) * ir4_jobs.size()));
     HIPCHK(ctx, h2d(&ctx->hpart_jobs.p, hpart_jobs.data(), sizeof(int2) * hpart_jobs.size()));
     HIPCHK(ctx, hipMemsetAsync(ctx->maxbits.p, 0, sizeof(unsigned) * P, s));
     // the float64 FIR chain: slots for up to FIR64_CAP flagged presets of the batch
@@ -1875,6 +1941,44 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
         ++ctx->host_cnt;
     }
 
+    // The filter spectra depend on the presets' taps and IRs only, not on the
+    // audio: launched before the generator (h_early), they run while
+    // the GPU holds the other streams' earlier stages, instead of queueing
+    // behind a persistent k_fir8p of another stream that holds every CU
+    // (C5's fir_h window had been ~100x its isolated time).
+    auto launch_h_spectra = [&]() -> int {
+        if (htiles > 0)
+            HIPCHK(ctx, launch_h_build((unsigned)htiles, s, ctx->prt.p, ctx->h_tile_begin.p, P, ctx->er_off.p,
+                                       ctx->er_gain.p, ctx->irbank.p, ctx->hscratch.p));
+        if (!ir8_jobs.empty())
+            HIPCHK(ctx, launch_fir8_spec64((unsigned)(ir8_jobs.size() / 4), s, ctx->ir8_jobs.p, ctx->d_fir4tab,
+                                           ctx->irbank.p, ctx->hspec.p));
+        if (!hpart_jobs.empty())
+            HIPCHK(ctx, launch_fir4_hpart(16384, (unsigned)hpart_jobs.size(), s, ctx->prt.p, ctx->hpart_jobs.p,
+                                          ctx->d_fir4tab, ctx->hscratch.p, ctx->hspec.p));
+        if (!fir8_list.empty())
+            HIPCHK(ctx, launch_fir8_hconv((unsigned)fir8_list.size(), s, ctx->prt.p, ctx->fir8_list.p, ctx->d_fir4tab,
+                                          ctx->er_off.p, ctx->er_gain.p, ctx->hspec.p));
+        if (!ir4_jobs.empty())
+            HIPCHK(ctx, launch_fir4_irspec((unsigned)(ir4_jobs.size() / 4), s, ctx->ir4_jobs.p, ctx->d_fir4tab,
+                                           ctx->irbank.p, ctx->hspec.p));
+        if (!fir4c_list.empty())
+            HIPCHK(ctx, launch_fir4_hconv((unsigned)fir4c_list.size(), s, ctx->prt.p, ctx->fir4c_list.p, ctx->d_fir4tab,
+                                          ctx->er_off.p, ctx->er_gain.p, ctx->hspec.p));
+        if (hblocks_gen > 0)   // blocks of k_fir4/k_fir8-engine presets return at once
+            HIPCHK(ctx, launch_fir_h((unsigned)hblocks, fir_lds, s, ctx->prt.p, ctx->h_begin.p, P,
+                                     ctx->fir_plans.dev.p, ctx->fir_plan_of.p, ctx->hscratch.p, ctx->hspec.p));
+        return MSG_OK;
+    };
+    int64_t fir_nmax = 0;
+    for (int p = 0; p < P; ++p)
+        if (prt[p].fir_on) fir_nmax = std::max<int64_t>(fir_nmax, prt[p].out_n);
+    const bool h_early = hblocks > 0 && (ctx->h_early == 1 || (ctx->h_early == 2 && fir_nmax >= ((int64_t)1 << 22)));
+    if (h_early) {
+        stage_mark(ctx, 10, s);
+        if (const int rc = launch_h_spectra()) return rc;
+        stage_mark(ctx, 11, s);
+    }
     // ---- generate ----
     stage_mark(ctx, 2, s);
     if (!gen_list.empty())
@@ -1925,28 +2029,17 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
                                    ctx->grain.p));
     // ---- overlap-add x ADSR ----
     stage_mark(ctx, 4, s);
-    hipLaunchKernelGGL(k_ola_env, dim3((unsigned)tiles), dim3(OLA_T), 0, s, ctx->events.p, ctx->prt.p,
-                       ctx->tile_begin.p, P, ctx->grain.p, ctx->mono_a.p);
-    HIPCHK(ctx, hipGetLastError());
+    if (tiles > 0) {
+        hipLaunchKernelGGL(k_ola_env, dim3((unsigned)tiles), dim3(OLA_T), 0, s, ctx->events.p, ctx->prt.p,
+                           ctx->tile_begin.p, P, ctx->grain.p, ctx->mono_a.p);
+        HIPCHK(ctx, hipGetLastError());
+    }
     // ---- FIR (presets without ER/IR pass a through) ----
     stage_mark(ctx, 5, s);
     float* yb = ctx->mono_a.p;
     if (hblocks > 0) {
-        if (htiles > 0)
-            HIPCHK(ctx, launch_h_build((unsigned)htiles, s, ctx->prt.p, ctx->h_tile_begin.p, P, ctx->er_off.p,
-                                       ctx->er_gain.p, ctx->irbank.p, ctx->hscratch.p));
-        if (!ir8_jobs.empty())
-            HIPCHK(ctx, launch_fir8_spec64((unsigned)(ir8_jobs.size() / 4), s, ctx->ir8_jobs.p, ctx->d_fir4tab,
-                                           ctx->irbank.p, ctx->hspec.p));
-        if (!hpart_jobs.empty())
-            HIPCHK(ctx, launch_fir4_hpart(16384, (unsigned)hpart_jobs.size(), s, ctx->prt.p, ctx->hpart_jobs.p,
-                                          ctx->d_fir4tab, ctx->hscratch.p, ctx->hspec.p));
-        if (!fir8_list.empty())
-            HIPCHK(ctx, launch_fir8_hconv((unsigned)fir8_list.size(), s, ctx->prt.p, ctx->fir8_list.p, ctx->d_fir4tab,
-                                          ctx->er_off.p, ctx->er_gain.p, ctx->hspec.p));
-        if (hblocks_gen > 0)   // blocks of k_fir4/k_fir8-engine presets return at once
-            HIPCHK(ctx, launch_fir_h((unsigned)hblocks, fir_lds, s, ctx->prt.p, ctx->h_begin.p, P,
-                                     ctx->fir_plans.dev.p, ctx->fir_plan_of.p, ctx->hscratch.p, ctx->hspec.p));
+        if (!h_early)
+            if (const int rc = launch_h_spectra()) return rc;
         stage_mark(ctx, 8, s);
         for (int i = 0; i < 7; ++i) {
             if (fjob_off[i + 1] <= fjob_off[i]) continue;
@@ -1961,7 +2054,7 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
                 }
                 HIPCHK(ctx, launch_fir8p(nj, grid, s, ctx->prt.p, ctx->fir_jobs.p + fjob_off[i],
                                          ctx->d_fir4tab, ctx->hspec.p, ctx->mono_a.p, ctx->mono_y.p, ctx->fir8_ctr.p,
-                                         ctx->fir8p_stagger));
+                                         ctx->fir8p_stagger, ctx->events.p, ctx->grain.p));
             } else if (i == 6)
                 HIPCHK(ctx, launch_fir8(nj, s, ctx->prt.p, ctx->fir_jobs.p + fjob_off[i], ctx->d_fir4tab, ctx->hspec.p,
                                         ctx->mono_a.p, ctx->mono_y.p));
@@ -2022,6 +2115,14 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
         a.plans = ctx->plans64.dev.p; a.plan = f64_plan;
         a.lds_bytes = FIR64_K * (int)sizeof(double2);   // the packed transform and its Nyquist slot
         a.x = ctx->mono_a.p; a.y = yb;
+        HIPCHK(ctx, launch_fir64_flag(a, s));
+        if (n_ola_fir > 0) {   // the flagged ola_fir presets' mono a, which k_fir8p never wrote
+            const int tmax = (int)((ola_fir_nmax + OLA_TILE - 1) / OLA_TILE);
+            hipLaunchKernelGGL(k_ola_slots, dim3((unsigned)std::min<int64_t>((int64_t)f64_cand * tmax, 1024)),
+                               dim3(OLA_T), 0, s, ctx->events.p, ctx->prt.p, ctx->f64_slot_preset.p,
+                               ctx->f64_nslots.p, tmax, ctx->grain.p, ctx->mono_a.p);
+            HIPCHK(ctx, hipGetLastError());
+        }
         HIPCHK(ctx, launch_fir64(a, s));
     }
     ++ctx->batch_serial;
@@ -2090,6 +2191,7 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
     if (ctx->profiling) {
         ctx->pending[ctx->ev_cur] = true;
         ctx->pending_fir[ctx->ev_cur] = hblocks > 0;
+        ctx->pending_h_early[ctx->ev_cur] = h_early;
         ctx->ev_cur ^= 1;
     }
     return MSG_OK;

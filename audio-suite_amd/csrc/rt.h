@@ -7,6 +7,7 @@
 //   k_h_build / k_fir_h            h = (delta + ER) * IR, its partition spectra      MS:409-445
 //   k_fir2<M>                      register-resident FFT overlap-save FIR           MS:766-773
 //   k_stereo_max / k_stereo_out    25-tap Bessel stereo, tanh, peak normalise       MS:423-436, 775-781
+//   k_fir8p (ola_fir)              overlap-add x ADSR fused into the FIR's loads    MS:742-773
 #pragma once
 #include "msg_common.h"
 #include "nprng.h"
@@ -49,13 +50,13 @@ struct PresetRt {
     int64_t ir_off;        // offset of the IR in the device IR bank (float64)
     int64_t h_off;         // offset of the Q partition spectra (float2)
     int32_t h_len;         // taps of h = (delta + ER) * IR (k_h_build), <= out_n
-    int32_t h_pad;
+    int32_t ola_fir;       // 1: the overlap-add runs inside k_fir8p's segment loads (fir8_fft.h), no mono a
     // stereo / saturation / normalisation
     int32_t stereo_fir;    // 1: 25-tap Bessel FIR (even n), 2: precomputed R (odd n), 0: L = R = y
     int32_t dl, dr;
     float bess[25];        // J_m(0.9 w), m = -12..12
     float drive, peak;
-    int32_t h_fir4;        // 1: partition spectra built on the k_fir4 engine (k_fir4_hpart)
+    int32_t h_fir4;        // spectra: 1 k_fir4_hpart, 2 k_fir8_hconv / IR spectrum, 3 k_fir4_hconv / IR spectrum
     // generator sources: IR fragment (float64 IR bank) and image (uint8 bank)
     int64_t frag_off, frag_len;
     int64_t img_off;

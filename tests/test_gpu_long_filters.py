@@ -319,3 +319,58 @@ def test_stereo_fused_matches_two_launches(msgpu, irs):
     assert int(packed.out_n[5]) % 2 == 1
     assert np.array_equal(two, two_again)
     assert np.array_equal(two, fused)
+
+
+def test_fir4_spectra_from_taps(msgpu, irs):
+    """One-partition filters at N = 32 768 (H48's 48 kHz ER + 4096-tap IR, an
+    IR-only one, an ER-only one): the spectra straight from the taps
+    (k_fir4_hconv / k_fir4_irspec, MSGPU_FIR4C=1, the default) against the
+    time-domain float64 h cut into one partition (k_h_build + k_fir4_hpart,
+    MSGPU_FIR4C=0): both match the oracle within the tolerance."""
+    from oracle import msound_oracle as O
+    params = [msgpu.config_params("H48", seed=1000 + s, irs=irs, out_dur_s=0.5) for s in range(2)]
+    params += [msgpu.merged(msgpu.config_params("H48", seed=1010, irs=irs, out_dur_s=0.5), er_cloud_on=False),
+               msgpu.merged(msgpu.config_params("H48", seed=1011, irs=irs, out_dur_s=0.5), space_ir_on=False)]
+    outs = {m: _render_env(params, {"MSGPU_FIR4C": m}) for m in ("0", "1")}
+    for i, p in enumerate(params):
+        ref, _ = O.render(p)
+        for m, (packed, o) in outs.items():
+            off, n = int(packed.offsets[i]), int(packed.out_n[i])
+            e = rms(o[off:off + n], ref)
+            print(f"case {i} [MSGPU_FIR4C={m}]: rms err vs oracle {e:.3e}")
+            assert e <= RMS_TOL, (i, m)
+
+
+def test_ola_fused_matches_ola_kernel(msgpu, irs):
+    """The overlap-add inside k_fir8p's segment loads (PresetRt::ola_fir) sums
+    the same events in the same order as k_ola_env, so the renders are the same
+    bits: C3 / C5 presets forced onto the fused path (MSGPU_OLA_FIR_DENSITY
+    raised past their grain density), short outputs (one block, first and last
+    blocks partial), and a float64-FIR preset whose mono a k_ola_slots writes."""
+    base = dict(gen_mode="Resonant strike", event_process="Poisson", _ir_audio=irs["tiny_room_ir"])
+    params = [msgpu.config_params("C3", seed=1200 + s, irs=irs, out_dur_s=d) for s, d in enumerate((1.3, 0.2))]
+    params += [msgpu.config_params("C5", seed=1300 + s, irs=irs, out_dur_s=d) for s, d in enumerate((200.0, 9.0))]
+    params += [msgpu.merged(base, base_sr=48000, out_dur_s=0.9, space_ir_on=True, seed=22, er_cloud_on=True,
+                            space_ir_max_samps=8192, stereo_width=0.3, sat_drive=6.0)]
+    fused_env = {"MSGPU_OLA_FIR": "1", "MSGPU_OLA_FIR_DENSITY": "1e9"}
+    _, ref = _render_env(params, {"MSGPU_OLA_FIR": "0"})
+    _, fused = _render_env(params, fused_env)
+    _, default = _render_env(params, {})
+    assert np.array_equal(ref, fused)
+    assert np.array_equal(ref, default)
+    # every FIR preset on the float64 FIR: k_ola_slots writes the fused presets' mono a
+    _, ref64 = _render_env(params, {"MSGPU_OLA_FIR": "0", "MSGPU_FIR64": "2"})
+    _, fused64 = _render_env(params, dict(fused_env, MSGPU_FIR64="2"))
+    assert np.array_equal(ref64, fused64)
+
+
+def test_filter_spectra_early_same_bits(msgpu, irs):
+    """The filter spectra launched before the generator (MSGPU_H_EARLY=1, the
+    default) or at the FIR stage: the same kernels on the same inputs, so the
+    same bits, for the k_fir8 / k_fir4 one-partition and the partitioned paths."""
+    params = [msgpu.config_params("C3", seed=1400, irs=irs, out_dur_s=0.4),
+              msgpu.config_params("H48", seed=1401, irs=irs, out_dur_s=0.5),
+              msgpu.config_params("C2", seed=1402, irs=irs, out_dur_s=0.25)]
+    _, late = _render_env(params, {"MSGPU_H_EARLY": "0"})
+    _, early = _render_env(params, {"MSGPU_H_EARLY": "1"})
+    assert np.array_equal(late, early)
