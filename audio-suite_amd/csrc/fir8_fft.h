@@ -218,24 +218,28 @@ MSG_DEV void load_halves(const float* __restrict__ x, int64_t n, int64_t s0, flo
 // ---------------------------------------------------------------------------
 // The overlap-add fused into the segment load (PresetRt::ola_fir): x[s0, s0 + N)
 // is summed from the placed grains (MS:742-764) instead of read from a mono
-// buffer k_ola_env wrote, one half of the segment at a time through buf.  The
-// arithmetic is ola_tile's (kernels_core.h): per frame, fmaf over the events in
-// event order from 0.f, times the ADSR, so the FIR's input is the same bits.
-// Wave w owns frames [w OLA_CHUNK, (w + 1) OLA_CHUNK) of each half, lane l the
-// frames l + 64 j: a grain's reads are coalesced over the wave, and one event
-// puts up to OLA_J loads per lane in flight.
+// buffer k_ola_env wrote.  The arithmetic is ola_tile's (kernels_core.h): per
+// frame, fmaf over the events in event order from 0.f, times the ADSR, so the
+// FIR's input is the same bits.  Wave w owns frames [w OLA_CHUNK, (w + 1)
+// OLA_CHUNK) of each half, lane l the frames l + 64 j: a grain's reads are
+// coalesced over the wave, and one event puts up to OLA_J loads per lane in
+// flight.  The DIF split is folded in: half 0 goes to LDS, each lane combines
+// its half-1 frames with its own half-0 frames (x0 + x1 in place, x0 - x1 kept),
+// and the sums, then the differences, leave LDS in the a / b layout -- so no
+// half is held in registers while the other is gathered (the first form held
+// a[] there: 128 VGPRs and scratch spills inside the transform passes).
 // ---------------------------------------------------------------------------
 constexpr int OLA_J = M / T;                  // frames per lane per half (32)
 constexpr int OLA_CHUNK = 64 * OLA_J;         // frames per wave per half
 
-// the half [c0, c0 + M) of the segment (absolute frames) into xf[0, M)
-MSG_DEV void ola_half(const msg_event* __restrict__ ev, const PresetRt& pr, const float* __restrict__ grain_pool,
-                      int lo, int64_t c0, float* xf) {
+// this lane's frames c0 + w OLA_CHUNK + lane + 64 j of the half starting at c0
+// (absolute), times the ADSR, zero outside [0, n)
+MSG_DEV void ola_sum(const msg_event* __restrict__ ev, const PresetRt& pr, const float* __restrict__ grain_pool,
+                     int lo, int64_t c0, float (&acc)[OLA_J]) {
     const int t = otid();
     const int lane = t & 63, w = t >> 6;
     const int64_t w0 = c0 + (int64_t)w * OLA_CHUNK, w1 = w0 + OLA_CHUNK;
     const int ne = pr.n_events;
-    float acc[OLA_J];
 #pragma unroll
     for (int j = 0; j < OLA_J; ++j) acc[j] = 0.f;
     for (int k0 = lo; k0 < ne; k0 += 64) {
@@ -276,26 +280,50 @@ MSG_DEV void ola_half(const msg_event* __restrict__ ev, const PresetRt& pr, cons
 #pragma unroll
     for (int j = 0; j < OLA_J; ++j) {
         const int64_t f = w0 + lane + 64 * j;
-        xf[w * OLA_CHUNK + lane + 64 * j] = (f >= 0 && f < n) ? acc[j] * adsr_at(pr, (int)f) : 0.f;
+        acc[j] = (f >= 0 && f < n) ? acc[j] * adsr_at(pr, (int)f) : 0.f;
     }
 }
 
-// load_halves for an ola_fir preset: the segment x[s0, s0 + N) summed in buf
-MSG_DEV void ola_halves(const msg_event* __restrict__ ev, const PresetRt& pr, const float* __restrict__ grain_pool,
-                        int64_t s0, float2* buf, float2 (&a)[R1], float2 (&b)[R1]) {
+// load_halves + dif_split for an ola_fir preset: (a, b) = (z0 + z1, (z0 - z1) W)
+// of the segment x[s0, s0 + N) summed from its grains (the same float adds and
+// products as dif_split on the loaded halves)
+MSG_DEV void ola_split(const msg_event* __restrict__ ev, const PresetRt& pr, const float* __restrict__ grain_pool,
+                       int64_t s0, float2* buf, const float2* tab, float2 (&a)[R1], float2 (&b)[R1]) {
     const int t = otid();
+    const int lane = t & 63, w = t >> 6;
     // events that can reach s0 start after s0 - max_n (every wave finds the same lo)
     const int lo = events_starting_by(ev, pr.n_events, s0 - (int64_t)pr.max_n);
-    float* xf = reinterpret_cast<float*>(buf);        // free: inv_half ends on a barrier
-    ola_half(ev, pr, grain_pool, lo, s0, xf);
+    float* xf = reinterpret_cast<float*>(buf) + w * OLA_CHUNK + lane;   // buf is free: inv_half ends on a barrier
+    {
+        float x0[OLA_J];
+        ola_sum(ev, pr, grain_pool, lo, s0, x0);
+#pragma unroll
+        for (int j = 0; j < OLA_J; ++j) xf[64 * j] = x0[j];             // read back by this lane only
+    }
+    float d[OLA_J];
+    {
+        float x1[OLA_J];
+        ola_sum(ev, pr, grain_pool, lo, s0 + M, x1);
+#pragma unroll
+        for (int j = 0; j < OLA_J; ++j) {
+            const float x0 = xf[64 * j];
+            d[j] = x0 - x1[j];
+            xf[64 * j] = x0 + x1[j];
+        }
+    }
     __syncthreads();
 #pragma unroll
     for (int r = 0; r < R1; ++r) a[r] = buf[t + r * NB1];
     __syncthreads();
-    ola_half(ev, pr, grain_pool, lo, s0 + M, xf);
-    __syncthreads();
 #pragma unroll
-    for (int r = 0; r < R1; ++r) b[r] = buf[t + r * NB1];
+    for (int j = 0; j < OLA_J; ++j) xf[64 * j] = d[j];
+    __syncthreads();
+    const float2 wt = fir4_wM(tab, G::OFF_PLO, G::OFF_PHI, t);
+#pragma unroll
+    for (int r = 0; r < R1; ++r) {
+        const float2 dd = buf[t + r * NB1];
+        b[r] = r == 0 ? cmul(dd, wt) : cmul(dd, cmul_k(wt, w32<R1>(r)));
+    }
 }
 
 // (a, b) <- (a + b, (a - b) W_M^(t + r NB1))
@@ -394,7 +422,11 @@ MSG_DEV void xcd_range(int n, int x, int& lo, int& cnt) {
 }
 }  // namespace fir8
 
-template <int UNUSED = 0>
+// OLA: the instantiation with the fused overlap-add (PresetRt::ola_fir) -- its
+// extra live state pushed the plain path to 128 VGPRs with spills in the
+// transform passes (C3 isolated FIR 1.94 -> 2.11 ms), so batches without an
+// ola_fir preset run the plain instantiation.
+template <bool OLA>
 __global__ void __launch_bounds__(fir8::T)
 k_fir8p(const PresetRt* __restrict__ rt, const int2* __restrict__ jobs, int n_jobs, const float2* __restrict__ tables,
         const float2* __restrict__ hspec, const float* __restrict__ x_in, float* __restrict__ y_out,
@@ -445,12 +477,13 @@ k_fir8p(const PresetRt* __restrict__ rt, const int2* __restrict__ jobs, int n_jo
         const int64_t n = pr.out_n;
         const int64_t t0 = (int64_t)job.y * pr.fir_B;
         float2 a[R1], b[R1];
-        if (__builtin_amdgcn_readfirstlane(pr.ola_fir))
-            ola_halves(events + pr.ev_begin, pr, grain_pool, t0 - (P - 1), buf, a, b);
+        const bool ola = OLA && __builtin_amdgcn_readfirstlane(pr.ola_fir);
+        if (ola)
+            ola_split(events + pr.ev_begin, pr, grain_pool, t0 - (P - 1), buf, tab, a, b);
         else
             load_halves(x_in + pr.y_off, n, t0 - (P - 1), a, b);
         if (t == 0) s_take[par] = atomicAdd(ctr + xr * FIR8P_CTR, 1);   // the block after this one
-        dif_split(tab, a, b);
+        if (!ola) dif_split(tab, a, b);
         FIR_STAMP(0);
         const float2* He = hspec + pr.h_off;
         const float2* Ho = He + (MH + 1);

@@ -29,7 +29,9 @@ void fir_init_attrs() {
                               Fir4Geo<16384>::LDS_BYTES);
     (void)hipFuncSetAttribute((const void*)k_fir8<0>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               Fir4Geo<16384>::LDS_BYTES);
-    (void)hipFuncSetAttribute((const void*)k_fir8p<0>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    (void)hipFuncSetAttribute((const void*)k_fir8p<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              Fir4Geo<16384>::LDS_BYTES);
+    (void)hipFuncSetAttribute((const void*)k_fir8p<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               Fir4Geo<16384>::LDS_BYTES);
     (void)hipFuncSetAttribute((const void*)k_fir8_hconv<0>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               Fir4Geo<16384>::LDS_BYTES);
@@ -153,8 +155,12 @@ hipError_t launch_fir8(unsigned grid, hipStream_t s, const PresetRt* rt, const i
 hipError_t launch_fir8p(unsigned n_jobs, unsigned grid, hipStream_t s, const PresetRt* rt, const int2* jobs,
                         const float2* tables, const float2* hspec, const float* x_in, float* y_out, int32_t* ctr,
                         int stagger, const msg_event* events, const float* grain_pool) {
-    hipLaunchKernelGGL((k_fir8p<0>), dim3(grid), dim3(fir8::T), Fir4Geo<16384>::LDS_BYTES, s, rt, jobs, (int)n_jobs,
-                       tables, hspec, x_in, y_out, ctr, stagger, events, grain_pool);
+    if (events)
+        hipLaunchKernelGGL((k_fir8p<true>), dim3(grid), dim3(fir8::T), Fir4Geo<16384>::LDS_BYTES, s, rt, jobs,
+                           (int)n_jobs, tables, hspec, x_in, y_out, ctr, stagger, events, grain_pool);
+    else
+        hipLaunchKernelGGL((k_fir8p<false>), dim3(grid), dim3(fir8::T), Fir4Geo<16384>::LDS_BYTES, s, rt, jobs,
+                           (int)n_jobs, tables, hspec, x_in, y_out, ctr, stagger, events, grain_pool);
     return hipGetLastError();
 }
 

@@ -2,15 +2,16 @@
 // normalisation (MS:26-34, 775-781) of the mono FIR output (TU: k_stereo.hip).
 //
 // Two passes over y per preset: the peak max(|L|, |R|) over every frame, then
-// the clipped, normalised (L, R) pairs.  k_stereo_fused (the render path since
-// round 5) runs both in one persistent launch: workgroups take max-pass tiles
-// in batch order from one counter and later run the output pass of the same
-// tiles, once the tile's preset is complete (the last of its tiles to finish
-// publishes the peak), so the output pass re-reads y while it is still in the
-// XCD's L2 or the Infinity Cache -- HBM moves 4 + 8 B per frame instead of the
-// 4 + 4 + 8 of two launches (C3's 537 MB of y per 341-preset sub-batch outlive
-// the 256 MB cache between two launches).
-// k_stereo_max + k_stereo_out are the two-launch form (MSGPU_STEREO_FUSED=0).
+// the clipped, normalised (L, R) pairs: k_stereo_max + k_stereo_out, two
+// launches (the render path).  k_stereo_fused (MSGPU_STEREO_FUSED=1, an option)
+// runs both in one persistent launch: workgroups take max-pass tiles in batch
+// order from one counter and later run the output pass of the same tiles, once
+// the tile's preset is complete (the last of its tiles to finish publishes the
+// peak), so the output pass can re-read y from the XCD's L2 or the Infinity
+// Cache -- 4 + 8 B of HBM per frame instead of 4 + 4 + 8.  Measured slower
+// (C3 isolated stereo 1.79 vs 1.60 ms, C5 7.35 vs 5.59 ms per sub-batch, DESIGN
+// §4): the chunk claims and the waits for a preset's last tile cost more than
+// the re-read saves.
 //
 // The float64 FIR's error predictor (kernels_fir64.h) needs per preset sum y^2
 // and sum (1 + (d y)^2)^-2: each tile stores its two partial sums, and the

@@ -220,8 +220,8 @@ struct msg_ctx {
     int n_cu = 256;              // compute units (persistent grids)
     int fir8p_cus = 0;           // persistent FIR workgroups (MSGPU_FIR8P_CUS, A/B; 0: one per CU)
     int fir8p_stagger = 0;       // k_fir8p: every other workgroup starts this many 10-ns ticks later (MSGPU_FIR8P_STAGGER)
-    // overlap-add inside k_fir8p's loads (PresetRt::ola_fir) for presets whose
-    // placed grains total at most ola_fir_density x out_n frames (MSGPU_OLA_FIR=0: never)
+    // overlap-add inside k_fir8p's loads (PresetRt::ola_fir) for batches whose k_fir8p
+    // presets' grains total at most ola_fir_density x their frames (MSGPU_OLA_FIR=0: never)
     bool ola_fir = true;
     // filter spectra before the generator (MSGPU_H_EARLY): 0 at the FIR stage, 1 always,
     // 2 (default) for batches with an output of at least 2^22 frames, whose FIR
@@ -1447,6 +1447,21 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
             f.bess[m + 12] = (float)((m < 0 && (m & 1)) ? -j : j);
         }
     });
+    // The overlap-add inside k_fir8p, decided for the batch as a whole: all of its
+    // k_fir8p presets or none, by their grains against their outputs.  A batch
+    // with any ola_fir preset runs the fused instantiation for all of its blocks,
+    // and that kernel's extra live state costs the plain blocks ~10 % (C3: a few
+    // sparse seeds had put every C3 batch on it, isolated FIR 1.88 -> 2.13 ms).
+    bool batch_ola = false;
+    if (ctx->ola_fir && ctx->fir8p > 0) {
+        double grains = 0.0, frames = 0.0;
+        for (int p = 0; p < P; ++p)
+            if (pick[p].M > 0 && pick[p].N == FIR8_N && !pick[p].stream) {
+                grains += (double)info[p].pool_len;
+                frames += (double)info[p].out_n;
+            }
+        batch_ola = frames > 0.0 && grains <= ctx->ola_fir_density * frames;
+    }
     for (int p = 0; p < P; ++p) {
         const msg_preset& pr = presets[p];
         const msg_plan_info& inf = info[p];
@@ -1575,8 +1590,7 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
             const int32_t nblk = (int32_t)((inf.out_n + r.fir_B - 1) / r.fir_B);
             // the overlap-add in k_fir8p's segment loads: each segment sums its grains
             // again (N / B ~ 1.6 times per frame), worth it while the grains are sparse
-            if (N == FIR8_N && !stream && ctx->fir8p > 0 && ctx->ola_fir &&
-                (double)inf.pool_len <= ctx->ola_fir_density * (double)inf.out_n) {
+            if (N == FIR8_N && !stream && batch_ola) {
                 r.ola_fir = 1;
                 n_ola_fir++;
                 ola_fir_nmax = std::max<int64_t>(ola_fir_nmax, inf.out_n);
@@ -2054,7 +2068,8 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
                 }
                 HIPCHK(ctx, launch_fir8p(nj, grid, s, ctx->prt.p, ctx->fir_jobs.p + fjob_off[i],
                                          ctx->d_fir4tab, ctx->hspec.p, ctx->mono_a.p, ctx->mono_y.p, ctx->fir8_ctr.p,
-                                         ctx->fir8p_stagger, ctx->events.p, ctx->grain.p));
+                                         ctx->fir8p_stagger,
+                                         n_ola_fir > 0 ? ctx->events.p : nullptr, ctx->grain.p));
             } else if (i == 6)
                 HIPCHK(ctx, launch_fir8(nj, s, ctx->prt.p, ctx->fir_jobs.p + fjob_off[i], ctx->d_fir4tab, ctx->hspec.p,
                                         ctx->mono_a.p, ctx->mono_y.p));
