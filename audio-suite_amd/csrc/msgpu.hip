@@ -198,6 +198,7 @@ struct msg_ctx {
     // host wall clock per batch: plan, records, pinned upload, then the splits
     // plan sizes, plan events + tap merge, preset records, event records, lists + buffers
     double host_sum[8] = {0};
+    double ola_fir_sum = 0.0;    // presets whose overlap-add ran inside k_fir8p, summed over profiled batches
     int64_t host_cnt = 0;
     hipEvent_t ev[2][12] = {};
     bool device_plan = false;     // MSGPU_DEVICE_PLAN=1: plan on the device (k_plan_*), read back
@@ -855,6 +856,7 @@ int msg_set_profiling(msg_ctx* ctx, int32_t on) {
     if (ctx->profiling) {
         for (double& v : ctx->stage_sum) v = 0.0;
         for (double& v : ctx->host_sum) v = 0.0;
+        ctx->ola_fir_sum = 0.0;
         ctx->stage_cnt = 0;
         ctx->host_cnt = 0;
     }
@@ -889,6 +891,7 @@ int msg_stage_times(msg_ctx* ctx, float* ms, int32_t n) {
         ms[i] = ctx->host_cnt ? (float)(ctx->host_sum[i - 10] / (double)ctx->host_cnt) : 0.f;
     for (int i = 13; i < n && i < 18; ++i)
         ms[i] = ctx->host_cnt ? (float)(ctx->host_sum[i - 10] / (double)ctx->host_cnt) : 0.f;
+    if (n > 18) ms[18] = ctx->host_cnt ? (float)(ctx->ola_fir_sum / (double)ctx->host_cnt) : 0.f;
     return MSG_OK;
 }
 
@@ -1952,6 +1955,7 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
         ctx->host_sum[5] += std::chrono::duration<double, std::milli>(hB - h1).count();
         ctx->host_sum[6] += std::chrono::duration<double, std::milli>(hC - hB).count();
         ctx->host_sum[7] += std::chrono::duration<double, std::milli>(h2 - hC).count();
+        ctx->ola_fir_sum += n_ola_fir;
         ++ctx->host_cnt;
     }
 

@@ -58,8 +58,8 @@ class Engine:
         self._gate_peer = peer      # the peer context stays alive while this one gates on it
 
     def stage_times(self):
-        arr = (C.c_float * 18)()
-        L.check(L.lib().msg_stage_times(self._ctx, arr, 18), self._ctx)
+        arr = (C.c_float * 19)()
+        L.check(L.lib().msg_stage_times(self._ctx, arr, 19), self._ctx)
         return list(arr)
 
     def alloc_output(self, packed: PackedBatch):

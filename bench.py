@@ -54,7 +54,8 @@ STAGE_KERNEL = {"generate": ("k_gen_normal",), "spectral": ("k_spec3", "k_spectr
                 "fir_h": ("k_fir8_hconv", "k_fir8_spec", "k_h_build", "k_fir4_hpart", "k_fir_h", "k_ir_spec")}
 STAGE_NAMES = ["plan", "host_prep", "generate", "spectral", "overlap_add", "fir", "stereo", "total",
                "fir_kernel", "fir_h", "host_plan_wall", "host_records_wall", "host_upload_wall",
-               "host_plan_sizes", "host_plan_events", "host_preset_records", "host_event_records", "host_lists"]
+               "host_plan_sizes", "host_plan_events", "host_preset_records", "host_event_records", "host_lists",
+               "ola_fir_presets"]
 KERNEL_STAGES = ["generate", "spectral", "overlap_add", "fir_kernel", "stereo"]
 # the line's roofline kernel per config: the stage of the config's rocprof-dominant
 # kernel (largest share of GPU time in profiles/r04h_*kernel_stats.csv: k_spec3 for
@@ -101,17 +102,24 @@ def load_irs():
     return {k: z[k] for k in z.files}
 
 
-def stage_bytes(infos):
+def stage_bytes(infos, fused=0.0):
     """Algorithmic (compulsory) HBM bytes per stage for the presets in ``infos``
-    (DESIGN.md section 4)."""
+    (DESIGN.md section 4).  ``fused``: the share of them whose overlap-add ran
+    inside the FIR kernel (stage time "ola_fir_presets" over the presets per
+    batch): their grain reads move from the overlap-add to the FIR, and the
+    mono buffer between the two is neither written nor read."""
     sum_n = sum(int(i.pool_len) for i in infos)
     out_n = sum(int(i.out_n) for i in infos)
+    f = min(max(float(fused), 0.0), 1.0)
+    ola = 4 * sum_n + 4 * out_n                # placed grains read + mono written (upper bound)
+    fir = 8 * out_n                            # mono read + y written
+    fir_fused = 4 * sum_n + 4 * out_n          # placed grains read + y written
     return {
         "generate": 4 * sum_n,                 # grain samples written once
         "spectral": 8 * sum_n,                 # grain read + grain written (one LDS round trip)
-        "overlap_add": 4 * sum_n + 4 * out_n,  # placed grains read + mono written (upper bound)
-        "fir": 8 * out_n,                      # mono read + mono written
-        "fir_kernel": 8 * out_n,               # k_fir alone: same compulsory bytes
+        "overlap_add": (1 - f) * ola,
+        "fir": (1 - f) * fir + f * fir_fused,
+        "fir_kernel": (1 - f) * fir + f * fir_fused,   # k_fir alone: same compulsory bytes
         "stereo": 16 * out_n,                  # max pass reads y; output pass reads y, writes L/R
     }
 
@@ -483,7 +491,7 @@ def measure(runner, cfg, seeds, sub, steps, warmup, comm, irs, golden, iso_steps
     check = runner.check(w, golden) if comm.rank == 0 else None
     infos = runner.infos(w)
     nsub = len(w.subs)
-    sb = stage_bytes(infos)
+    sb = stage_bytes(infos, stages.get("ola_fir_presets", 0.0) * nsub / max(1, len(seeds)))
     sb_launch = {k: v / nsub for k, v in sb.items()}
     longest = max(KERNEL_STAGES, key=lambda k: stages[k])
     dom = DOMINANT_STAGE.get(cfg, longest)
@@ -571,8 +579,8 @@ def isolated(runner, w, iso_steps, sb, cfg):
     runner.sync()
     e.set_profiling(False)
     iso = {n: round(float(v), 4) for n, v in zip(STAGE_NAMES, e.stage_times())}
-    if not whole:
-        sb = stage_bytes(e.last_plan())
+    infos = e.last_plan()
+    sb = stage_bytes(infos, iso.get("ola_fir_presets", 0.0) / max(1, len(infos)))
     dom = DOMINANT_STAGE.get(cfg, max(KERNEL_STAGES, key=lambda k: iso[k]))
     ach = sb[dom] / (iso[dom] * 1e-3) / 1e9
     kern = [k for k in KERNEL_STAGES if iso.get(k, 0) > 0]

@@ -171,7 +171,8 @@ int msg_last_grain64(msg_ctx* ctx, int32_t preset, int32_t k, double* grain, int
  * with n >= 13 also the host wall clock per batch: [10] plan (host pool),
  * [11] runtime records, [12] pinned staging + upload enqueue; host splits:
  * [13] plan sizes, [14] plan events + ER tap merge, [15] preset records,
- * [16] event records, [17] lists, buffers and staging adds.
+ * [16] event records, [17] lists, buffers and staging adds; with n >= 19,
+ * [18] the presets per batch whose overlap-add ran inside the FIR kernel.
  * Events are read lazily, so profiling does not block the host.             */
 int msg_set_profiling(msg_ctx* ctx, int32_t on);
 int msg_stage_times(msg_ctx* ctx, float* ms, int32_t n);
