@@ -232,36 +232,46 @@ MSG_DEV void load_halves(const float* __restrict__ x, int64_t n, int64_t s0, flo
 constexpr int OLA_J = M / T;                  // frames per lane per half (32)
 constexpr int OLA_CHUNK = 64 * OLA_J;         // frames per wave per half
 
+// lane k's event of a 64-event round (start INT32_MAX past the preset's last)
+struct OlaEv {
+    int s, L;
+    float amp;
+    int64_t goff;
+};
+MSG_DEV OlaEv ola_ev(const msg_event* __restrict__ ev, const PresetRt& pr, int k) {
+    OlaEv o{INT32_MAX, 0, 0.f, 0};
+    if (k < pr.n_events) {
+        const msg_event& e = ev[k];
+        o.s = e.start; o.L = e.len; o.amp = (float)e.amp;
+        o.goff = pr.pool_base + e.pool_off + e.offset;
+    }
+    return o;
+}
+
 // this lane's frames c0 + w OLA_CHUNK + lane + 64 j of the half starting at c0
-// (absolute), times the ADSR, zero outside [0, n)
+// (absolute), times the ADSR, zero outside [0, n).  first: the lanes' events
+// lo + lane (fetched once per segment, for both halves).  (Two events per
+// iteration, both grains' loads in flight before the first FMA, ran slower:
+// 146 SGPR spills, C5's FIR 5.84 -> 6.10 ms per sub-batch.)
 MSG_DEV void ola_sum(const msg_event* __restrict__ ev, const PresetRt& pr, const float* __restrict__ grain_pool,
-                     int lo, int64_t c0, float (&acc)[OLA_J]) {
+                     int lo, const OlaEv& first, int64_t c0, float (&acc)[OLA_J]) {
     const int t = otid();
     const int lane = t & 63, w = t >> 6;
     const int64_t w0 = c0 + (int64_t)w * OLA_CHUNK, w1 = w0 + OLA_CHUNK;
-    const int ne = pr.n_events;
 #pragma unroll
     for (int j = 0; j < OLA_J; ++j) acc[j] = 0.f;
-    for (int k0 = lo; k0 < ne; k0 += 64) {
-        const int k = k0 + lane;
-        int s = INT32_MAX, L = 0;
-        float amp = 0.f;
-        int64_t goff = 0;
-        if (k < ne) {
-            const msg_event& e = ev[k];
-            s = e.start; L = e.len; amp = (float)e.amp;
-            goff = pr.pool_base + e.pool_off + e.offset;
-        }
-        const uint64_t before = __ballot(s < w1);           // sorted: a prefix of the lanes
-        uint64_t live = before & __ballot(L > 0 && (int64_t)s + L > w0);
+    OlaEv e = first;
+    for (int k0 = lo;;) {
+        const uint64_t before = __ballot(e.s < w1);         // sorted: a prefix of the lanes
+        uint64_t live = before & __ballot(e.L > 0 && (int64_t)e.s + e.L > w0);
         while (live) {                                      // in event order
             const int i = __builtin_ctzll(live);
             live &= live - 1;
-            const int si = __builtin_amdgcn_readlane(s, i);
-            const uint32_t Li = (uint32_t)__builtin_amdgcn_readlane(L, i);
-            const float av = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(amp), i));
-            const int64_t gi = ((int64_t)__builtin_amdgcn_readlane((int)(goff >> 32), i) << 32) |
-                               (uint32_t)__builtin_amdgcn_readlane((int)goff, i);
+            const int si = __builtin_amdgcn_readlane(e.s, i);
+            const uint32_t Li = (uint32_t)__builtin_amdgcn_readlane(e.L, i);
+            const float av = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(e.amp), i));
+            const int64_t gi = ((int64_t)__builtin_amdgcn_readlane((int)(e.goff >> 32), i) << 32) |
+                               (uint32_t)__builtin_amdgcn_readlane((int)e.goff, i);
             const float* g = grain_pool + gi;
             const int q0 = (int)(w0 - si) + lane;           // in (-OLA_CHUNK, L): the event meets the chunk
             float gv[OLA_J];
@@ -275,6 +285,9 @@ MSG_DEV void ola_sum(const msg_event* __restrict__ ev, const PresetRt& pr, const
                 if ((uint32_t)(q0 + 64 * j) < Li) acc[j] = fmaf(av, gv[j], acc[j]);
         }
         if (before != ~0ull) break;
+        k0 += 64;
+        if (k0 >= pr.n_events) break;
+        e = ola_ev(ev, pr, k0 + lane);
     }
     const int64_t n = pr.out_n;
 #pragma unroll
@@ -287,23 +300,24 @@ MSG_DEV void ola_sum(const msg_event* __restrict__ ev, const PresetRt& pr, const
 // load_halves + dif_split for an ola_fir preset: (a, b) = (z0 + z1, (z0 - z1) W)
 // of the segment x[s0, s0 + N) summed from its grains (the same float adds and
 // products as dif_split on the loaded halves)
+// lo: the first event that can reach s0 (its start after s0 - max_n; the host
+// computes it per block, fir_lo)
 MSG_DEV void ola_split(const msg_event* __restrict__ ev, const PresetRt& pr, const float* __restrict__ grain_pool,
-                       int64_t s0, float2* buf, const float2* tab, float2 (&a)[R1], float2 (&b)[R1]) {
+                       int64_t s0, int lo, float2* buf, const float2* tab, float2 (&a)[R1], float2 (&b)[R1]) {
     const int t = otid();
     const int lane = t & 63, w = t >> 6;
-    // events that can reach s0 start after s0 - max_n (every wave finds the same lo)
-    const int lo = events_starting_by(ev, pr.n_events, s0 - (int64_t)pr.max_n);
+    const OlaEv first = ola_ev(ev, pr, lo + lane);
     float* xf = reinterpret_cast<float*>(buf) + w * OLA_CHUNK + lane;   // buf is free: inv_half ends on a barrier
     {
         float x0[OLA_J];
-        ola_sum(ev, pr, grain_pool, lo, s0, x0);
+        ola_sum(ev, pr, grain_pool, lo, first, s0, x0);
 #pragma unroll
         for (int j = 0; j < OLA_J; ++j) xf[64 * j] = x0[j];             // read back by this lane only
     }
     float d[OLA_J];
     {
         float x1[OLA_J];
-        ola_sum(ev, pr, grain_pool, lo, s0 + M, x1);
+        ola_sum(ev, pr, grain_pool, lo, first, s0 + M, x1);
 #pragma unroll
         for (int j = 0; j < OLA_J; ++j) {
             const float x0 = xf[64 * j];
@@ -431,7 +445,7 @@ __global__ void __launch_bounds__(fir8::T)
 k_fir8p(const PresetRt* __restrict__ rt, const int2* __restrict__ jobs, int n_jobs, const float2* __restrict__ tables,
         const float2* __restrict__ hspec, const float* __restrict__ x_in, float* __restrict__ y_out,
         int32_t* __restrict__ ctr, int stagger, const msg_event* __restrict__ events,
-        const float* __restrict__ grain_pool) {
+        const float* __restrict__ grain_pool, const int32_t* __restrict__ ev_lo) {
     using namespace fir8;
     extern __shared__ __attribute__((aligned(16))) float2 lds[];
     __shared__ int s_take[2];
@@ -479,7 +493,7 @@ k_fir8p(const PresetRt* __restrict__ rt, const int2* __restrict__ jobs, int n_jo
         float2 a[R1], b[R1];
         const bool ola = OLA && __builtin_amdgcn_readfirstlane(pr.ola_fir);
         if (ola)
-            ola_split(events + pr.ev_begin, pr, grain_pool, t0 - (P - 1), buf, tab, a, b);
+            ola_split(events + pr.ev_begin, pr, grain_pool, t0 - (P - 1), ev_lo[lo + cur], buf, tab, a, b);
         else
             load_halves(x_in + pr.y_off, n, t0 - (P - 1), a, b);
         if (t == 0) s_take[par] = atomicAdd(ctr + xr * FIR8P_CTR, 1);   // the block after this one

@@ -154,13 +154,13 @@ hipError_t launch_fir8(unsigned grid, hipStream_t s, const PresetRt* rt, const i
 // launch; each launch leaves them zero)
 hipError_t launch_fir8p(unsigned n_jobs, unsigned grid, hipStream_t s, const PresetRt* rt, const int2* jobs,
                         const float2* tables, const float2* hspec, const float* x_in, float* y_out, int32_t* ctr,
-                        int stagger, const msg_event* events, const float* grain_pool) {
+                        int stagger, const msg_event* events, const float* grain_pool, const int32_t* ev_lo) {
     if (events)
         hipLaunchKernelGGL((k_fir8p<true>), dim3(grid), dim3(fir8::T), Fir4Geo<16384>::LDS_BYTES, s, rt, jobs,
-                           (int)n_jobs, tables, hspec, x_in, y_out, ctr, stagger, events, grain_pool);
+                           (int)n_jobs, tables, hspec, x_in, y_out, ctr, stagger, events, grain_pool, ev_lo);
     else
         hipLaunchKernelGGL((k_fir8p<false>), dim3(grid), dim3(fir8::T), Fir4Geo<16384>::LDS_BYTES, s, rt, jobs,
-                           (int)n_jobs, tables, hspec, x_in, y_out, ctr, stagger, events, grain_pool);
+                           (int)n_jobs, tables, hspec, x_in, y_out, ctr, stagger, events, grain_pool, ev_lo);
     return hipGetLastError();
 }
 

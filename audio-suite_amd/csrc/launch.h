@@ -96,7 +96,9 @@ hipError_t launch_fir8(unsigned grid, hipStream_t s, const PresetRt* rt, const i
                        const float2* hspec, const float* x_in, float* y_out);
 hipError_t launch_fir8p(unsigned n_jobs, unsigned grid, hipStream_t s, const PresetRt* rt, const int2* jobs,
                         const float2* tables, const float2* hspec, const float* x_in, float* y_out, int32_t* ctr,
-                        int stagger, const msg_event* events, const float* grain_pool);   // events: null if no ola_fir preset
+                        int stagger, const msg_event* events, const float* grain_pool,
+                        const int32_t* ev_lo);   // events: null if no ola_fir preset; ev_lo: per job, the
+                                                 // first event reaching its segment
 hipError_t launch_fir8_hconv(unsigned n_presets, hipStream_t s, const PresetRt* rt, const int32_t* list,
                              const float2* tables, const int32_t* er_off, const double* er_gain, float2* hspec);
 hipError_t launch_fir8_spec64(unsigned n_jobs, hipStream_t s, const int64_t* jobs, const float2* tables,

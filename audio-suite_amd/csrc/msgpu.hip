@@ -263,7 +263,7 @@ struct msg_ctx {
     DevBuf<float> micro, grain, mono_a, mono_y;
     DevBuf<float2> hspec;
     DevBuf<float> hscratch;                     // h of every FIR preset (k_h_build -> k_fir_h / k_fir4_hpart)
-    Slice<int32_t> h_tile_begin, fir8_list;
+    Slice<int32_t> h_tile_begin, fir8_list, fir_lo;
     Slice<int64_t> ir8_jobs;
     Slice<int32_t> fir4c_list;                  // k_fir4_hconv presets (one partition at N = 32768)
     Slice<int64_t> ir4_jobs;                    // k_fir4_irspec jobs
@@ -1865,6 +1865,25 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
         fir_jobs.insert(fir_jobs.end(), fjobs_by[i].begin(), fjobs_by[i].end());
     }
     fjob_off[7] = (int32_t)fir_jobs.size();
+    // the fused overlap-add's first event per k_fir8p block: the events of a
+    // preset are sorted by start, so one moving index per preset finds, block by
+    // block, the first event starting after the segment's start - max_n
+    std::vector<int32_t> fir_lo;
+    if (n_ola_fir > 0) {
+        const std::vector<int2>& fj = fjobs_by[6];
+        fir_lo.resize(fj.size());
+        int cur_p = -1, k = 0;
+        for (size_t j = 0; j < fj.size(); ++j) {
+            const int p = fj[j].x;
+            if (p != cur_p) { cur_p = p; k = 0; }
+            const PresetRt& r = prt[p];
+            const int64_t lim = (int64_t)fj[j].y * r.fir_B - (r.fir_P - 1) - (int64_t)r.max_n;
+            const msg_event* ev = ctx->h_events.data() + r.ev_begin;
+            if (fj[j].y == 0) k = 0;
+            while (k < r.n_events && (int64_t)ev[k].start <= lim) ++k;
+            fir_lo[j] = k;
+        }
+    }
     HIPCHK(ctx, ctx->micro.ensure(pool));
     HIPCHK(ctx, ctx->grain.ensure(pool));
     HIPCHK(ctx, ctx->mono_a.ensure(ysum));
@@ -1904,6 +1923,7 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
     HIPCHK(ctx, h2d(&ctx->tile_begin.p, tile_begin.data(), sizeof(int32_t) * P));
     HIPCHK(ctx, h2d(&ctx->fir_begin.p, fir_begin.data(), sizeof(int32_t) * P));
     HIPCHK(ctx, h2d(&ctx->fir_jobs.p, fir_jobs.data(), sizeof(int2) * fir_jobs.size()));
+    HIPCHK(ctx, h2d(&ctx->fir_lo.p, fir_lo.data(), sizeof(int32_t) * fir_lo.size()));
     HIPCHK(ctx, h2d(&ctx->h_begin.p, h_begin.data(), sizeof(int32_t) * P));
     HIPCHK(ctx, h2d(&ctx->st_begin.p, st_begin.data(), sizeof(int32_t) * P));
     HIPCHK(ctx, h2d(&ctx->fir_plan_of.p, fir_plan_of.data(), sizeof(int32_t) * P));
@@ -2073,7 +2093,7 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
                 HIPCHK(ctx, launch_fir8p(nj, grid, s, ctx->prt.p, ctx->fir_jobs.p + fjob_off[i],
                                          ctx->d_fir4tab, ctx->hspec.p, ctx->mono_a.p, ctx->mono_y.p, ctx->fir8_ctr.p,
                                          ctx->fir8p_stagger,
-                                         n_ola_fir > 0 ? ctx->events.p : nullptr, ctx->grain.p));
+                                         n_ola_fir > 0 ? ctx->events.p : nullptr, ctx->grain.p, ctx->fir_lo.p));
             } else if (i == 6)
                 HIPCHK(ctx, launch_fir8(nj, s, ctx->prt.p, ctx->fir_jobs.p + fjob_off[i], ctx->d_fir4tab, ctx->hspec.p,
                                         ctx->mono_a.p, ctx->mono_y.p));
