@@ -2083,8 +2083,13 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
             if (fjob_off[i + 1] <= fjob_off[i]) continue;
             const unsigned nj = (unsigned)(fjob_off[i + 1] - fjob_off[i]);
             if (i == 6 && ctx->fir8p > 0) {
-                // persistent: one workgroup per CU (at most one per block), a multiple of the XCD count
-                const int cus = ctx->fir8p_cus > 0 ? std::min(ctx->fir8p_cus, ctx->n_cu) : ctx->n_cu;
+                // persistent: one workgroup per CU (at most one per block), a multiple of the XCD
+                // count.  Long outputs (h_early: milliseconds per launch) leave one CU in eight
+                // to the other streams' small kernels, which cannot start beside a k_fir8p
+                // workgroup (its VGPRs fill the CU): C5 118.4 - 119.4 ms with 224 of 256 CUs
+                // against 118.8 - 124.0 with all of them; C3 keeps every CU
+                const int cus = ctx->fir8p_cus > 0 ? std::min(ctx->fir8p_cus, ctx->n_cu)
+                                                   : (h_early ? ctx->n_cu - ctx->n_cu / 8 : ctx->n_cu);
                 const unsigned grid = (unsigned)std::max(MSG_XCDS, (std::min((int)nj, cus) / MSG_XCDS) * MSG_XCDS);
                 if (!ctx->fir8_ctr.p) {   // zeroed once; every launch leaves the counters zero
                     HIPCHK(ctx, ctx->fir8_ctr.ensure((size_t)(MSG_XCDS + 1) * FIR8P_CTR));
