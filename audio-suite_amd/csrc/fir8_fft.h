@@ -27,6 +27,10 @@
 // H layout (k_fir8_hpart): He[kappa] = H[2 kappa] (kappa <= MH), then
 // Ho[kappa] = H[2 kappa + 1] (kappa < MH): M + 1 float2 per preset, contiguous
 // per half so the MAC reads are unit-stride.
+//
+// k_fir8p<true> (round 5) also serves presets whose overlap-add runs in its
+// load phase (PresetRt::ola_fir, ola_split below): the segment is summed from
+// the placed grains instead of read from the mono buffer k_ola_env writes.
 #pragma once
 #include "fir4_fft.h"
 #include "ola.h"
