@@ -228,6 +228,7 @@ struct msg_ctx {
     // 2 (default) for batches with an output of at least 2^22 frames, whose FIR
     // holds every CU for milliseconds (C5 -2.5 %); shorter ones lose by it (C3 +2 %)
     int h_early = 2;
+    bool er_dev = true;          // ER gains drawn on the device (k_er_gains; MSGPU_ER_DEV=0: on the host plan)
     double ola_fir_density = 1.25;
     // Q <= 2 presets on the streaming k_fir4s (MSGPU_FIR4S=1; off by default: at
     // C3's 24 blocks per preset its H re-reads miss L2 and cancel the saved transforms)
@@ -257,6 +258,8 @@ struct msg_ctx {
     Slice<msg_event> events;
     Slice<int32_t> er_off;
     Slice<double> er_gain;
+    Slice<int32_t> er_key, er_first, er_cnt;
+    DevBuf<double> er_gain_d;           // k_er_gains' output (host batch path)
     Slice<EventRt> ert;
     Slice<PresetRt> prt;
     Slice<int32_t> gen_list, spec_small, spec_big, tile_begin, fir_begin, h_begin, st_begin, fir_plan_of;
@@ -320,6 +323,9 @@ struct msg_ctx {
     size_t h_ert_cap = 0;
     std::vector<int32_t> h_er_off;
     std::vector<double> h_er_gain;
+    // the host batch path's merged ER taps: per live slot its first key and
+    // key count, the keys' tap indices (k_er_gains draws the gains on the device)
+    std::vector<int32_t> h_er_key, h_er_first, h_er_cnt;
     std::vector<PresetRt> h_prt;
     std::vector<int32_t> h_slot_base;
     std::vector<Ev64> h_ev64;
@@ -732,6 +738,7 @@ msg_ctx* msg_create(int device_ordinal) {
     if (const char* e = getenv("MSGPU_FIR8P_STAGGER")) ctx->fir8p_stagger = std::max(0, atoi(e));
     if (const char* e = getenv("MSGPU_OLA_FIR")) ctx->ola_fir = e[0] != '0';
     if (const char* e = getenv("MSGPU_H_EARLY")) ctx->h_early = atoi(e);
+    if (const char* e = getenv("MSGPU_ER_DEV")) ctx->er_dev = e[0] != '0';
     if (const char* e = getenv("MSGPU_OLA_FIR_DENSITY")) ctx->ola_fir_density = atof(e);
     if (const char* e = getenv("MSGPU_STEREO_FUSED")) ctx->stereo_fused = e[0] != '0';
     if (const char* e = getenv("MSGPU_STEREO_WGS")) ctx->st_wgs = std::max(1, std::min(16, atoi(e)));
@@ -1211,12 +1218,20 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
         if (int st = bases()) return st;
         ctx->h_events.resize(nslots);
         ctx->h_er_off.resize(ntaps);
-        ctx->h_er_gain.resize(ntaps);
+        if (ctx->er_dev) {
+            ctx->h_er_key.resize(ntaps);
+            ctx->h_er_first.resize(ntaps);
+            ctx->h_er_cnt.resize(ntaps);
+        } else {
+            ctx->h_er_gain.resize(ntaps);
+        }
+        // offsets only: the gains (two thirds of the host plan of a 320-tap preset,
+        // a float64 exp each) are drawn on the device by k_er_gains
         pool.run(P, [&](int p) {
             const bool er = (presets[p].flags & MSG_F_ER_CLOUD) != 0;
             msgplan::plan_events(presets[p], bp_bank, kHostZig, flen[p], p, info[p], ctx->h_events.data() + slot_base[p],
                                  er ? ctx->h_er_off.data() + tap_base[p] : nullptr,
-                                 er ? ctx->h_er_gain.data() + tap_base[p] : nullptr, true);
+                                 (er && !ctx->er_dev) ? ctx->h_er_gain.data() + tap_base[p] : nullptr, true);
         });
 
     } else {
@@ -1276,13 +1291,14 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
             if (!(presets[p].flags & MSG_F_ER_CLOUD)) return;
             const int nt = std::max(1, presets[p].er_taps);
             int32_t* off = ctx->h_er_off.data() + tap_base[p];
-            double* g = ctx->h_er_gain.data() + tap_base[p];
+            const bool dev_gain = !ctx->device_plan && ctx->er_dev;
+            double* g = dev_gain ? nullptr : ctx->h_er_gain.data() + tap_base[p];
             // (offset, tap index) packed in one key, sorted stably by offset (tap_sort.h)
             thread_local std::vector<uint64_t> keybuf, tmpbuf;
             thread_local std::vector<double> g0;
             keybuf.resize(nt);
             tmpbuf.resize(nt);
-            g0.assign(g, g + nt);
+            if (!dev_gain) g0.assign(g, g + nt);
             const int64_t n = info[p].out_n;
             int m = 0;
             uint32_t omax = 0;
@@ -1298,15 +1314,32 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
             const uint64_t* key = keybuf.data();
 #endif
             int live = 0;
-            for (int i = 0; i < m;) {
-                const uint32_t o = (uint32_t)(key[i] >> 32);
-                double acc = g0[(uint32_t)key[i]];
-                int j = i + 1;
-                for (; j < m && (uint32_t)(key[j] >> 32) == o; ++j) acc += g0[(uint32_t)key[j]];
-                off[live] = (int32_t)o;
-                g[live] = acc;
-                ++live;
-                i = j;
+            if (dev_gain) {                              // slots -> key ranges, summed by k_er_gains
+                int32_t* kx = ctx->h_er_key.data() + tap_base[p];
+                int32_t* first = ctx->h_er_first.data() + tap_base[p];
+                int32_t* cnt = ctx->h_er_cnt.data() + tap_base[p];
+                for (int i = 0; i < m; ++i) kx[i] = (int32_t)(uint32_t)key[i];
+                for (int i = 0; i < m;) {
+                    const uint32_t o = (uint32_t)(key[i] >> 32);
+                    int j = i + 1;
+                    while (j < m && (uint32_t)(key[j] >> 32) == o) ++j;
+                    off[live] = (int32_t)o;
+                    first[live] = i;
+                    cnt[live] = j - i;
+                    ++live;
+                    i = j;
+                }
+            } else {
+                for (int i = 0; i < m;) {
+                    const uint32_t o = (uint32_t)(key[i] >> 32);
+                    double acc = g0[(uint32_t)key[i]];
+                    int j = i + 1;
+                    for (; j < m && (uint32_t)(key[j] >> 32) == o; ++j) acc += g0[(uint32_t)key[j]];
+                    off[live] = (int32_t)o;
+                    g[live] = acc;
+                    ++live;
+                    i = j;
+                }
             }
             n_taps_live[p] = live;
             tap_max[p] = live ? off[live - 1] : 0;
@@ -1319,7 +1352,14 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
     ctx->staging.add(&ctx->presets.p, presets, sizeof(msg_preset) * P);
     ctx->staging.add(&ctx->events.p, ctx->h_events.data(), sizeof(msg_event) * nslots);
     ctx->staging.add(&ctx->er_off.p, ctx->h_er_off.data(), sizeof(int32_t) * ntaps);
-    ctx->staging.add(&ctx->er_gain.p, ctx->h_er_gain.data(), sizeof(double) * ntaps);
+    const bool er_dev = !ctx->device_plan && ctx->er_dev;
+    if (!er_dev) {
+        ctx->staging.add(&ctx->er_gain.p, ctx->h_er_gain.data(), sizeof(double) * ntaps);
+    } else {
+        ctx->staging.add(&ctx->er_key.p, ctx->h_er_key.data(), sizeof(int32_t) * ntaps);
+        ctx->staging.add(&ctx->er_first.p, ctx->h_er_first.data(), sizeof(int32_t) * ntaps);
+        ctx->staging.add(&ctx->er_cnt.p, ctx->h_er_cnt.data(), sizeof(int32_t) * ntaps);
+    }
 
     // ---- host: runtime records ----
     std::vector<PresetRt> prt(P);
@@ -1965,6 +2005,17 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
     HIPCHK(ctx, h2d(&ctx->imgbank.p, imgbank.data(), imgbank.size()));
     const auto h2 = hclock::now();
     HIPCHK(ctx, ctx->staging.flush(s));
+    // the merged ER gains (host batch path), before any filter kernel reads them
+    const double* erg = ctx->er_gain.p;
+    if (er_dev) {
+        HIPCHK(ctx, ctx->er_gain_d.ensure((size_t)std::max<int64_t>(1, ntaps)));
+        erg = ctx->er_gain_d.p;
+        if (ntaps > 0) {
+            hipLaunchKernelGGL(k_er_gains, dim3((unsigned)P), dim3(64), 0, s, ctx->presets.p, ctx->prt.p, P,
+                               ctx->er_key.p, ctx->er_first.p, ctx->er_cnt.p, ctx->er_gain_d.p);
+            HIPCHK(ctx, hipGetLastError());
+        }
+    }
     if (ctx->profiling) {
         const auto h3 = hclock::now();
         ctx->host_sum[0] += std::chrono::duration<double, std::milli>(h1 - h0).count();
@@ -1987,7 +2038,7 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
     auto launch_h_spectra = [&]() -> int {
         if (htiles > 0)
             HIPCHK(ctx, launch_h_build((unsigned)htiles, s, ctx->prt.p, ctx->h_tile_begin.p, P, ctx->er_off.p,
-                                       ctx->er_gain.p, ctx->irbank.p, ctx->hscratch.p));
+                                       erg, ctx->irbank.p, ctx->hscratch.p));
         if (!ir8_jobs.empty())
             HIPCHK(ctx, launch_fir8_spec64((unsigned)(ir8_jobs.size() / 4), s, ctx->ir8_jobs.p, ctx->d_fir4tab,
                                            ctx->irbank.p, ctx->hspec.p));
@@ -1996,13 +2047,13 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
                                           ctx->d_fir4tab, ctx->hscratch.p, ctx->hspec.p));
         if (!fir8_list.empty())
             HIPCHK(ctx, launch_fir8_hconv((unsigned)fir8_list.size(), s, ctx->prt.p, ctx->fir8_list.p, ctx->d_fir4tab,
-                                          ctx->er_off.p, ctx->er_gain.p, ctx->hspec.p));
+                                          ctx->er_off.p, erg, ctx->hspec.p));
         if (!ir4_jobs.empty())
             HIPCHK(ctx, launch_fir4_irspec((unsigned)(ir4_jobs.size() / 4), s, ctx->ir4_jobs.p, ctx->d_fir4tab,
                                            ctx->irbank.p, ctx->hspec.p));
         if (!fir4c_list.empty())
             HIPCHK(ctx, launch_fir4_hconv((unsigned)fir4c_list.size(), s, ctx->prt.p, ctx->fir4c_list.p, ctx->d_fir4tab,
-                                          ctx->er_off.p, ctx->er_gain.p, ctx->hspec.p));
+                                          ctx->er_off.p, erg, ctx->hspec.p));
         if (hblocks_gen > 0)   // blocks of k_fir4/k_fir8-engine presets return at once
             HIPCHK(ctx, launch_fir_h((unsigned)hblocks, fir_lds, s, ctx->prt.p, ctx->h_begin.p, P,
                                      ctx->fir_plans.dev.p, ctx->fir_plan_of.p, ctx->hscratch.p, ctx->hspec.p));
@@ -2154,7 +2205,7 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
         a.n_cand = f64_cand; a.cap = f64_cap;
         a.fr = ctx->f64rt.p; a.tmax = (int)((f64_hmax + H_BUILD_TILE - 1) / H_BUILD_TILE); a.qmax = f64_qmax;
         a.bmax = f64_bmax;
-        a.er_off = ctx->er_off.p; a.er_gain = ctx->er_gain.p; a.irbank = ctx->irbank.p;
+        a.er_off = ctx->er_off.p; a.er_gain = erg; a.irbank = ctx->irbank.p;
         a.h64 = ctx->f64_h.p; a.h_stride = f64_hstride; a.hs64 = ctx->f64_hs.p; a.hs_stride = f64_hsstride;
         a.plans = ctx->plans64.dev.p; a.plan = f64_plan;
         a.lds_bytes = FIR64_K * (int)sizeof(double2);   // the packed transform and its Nyquist slot

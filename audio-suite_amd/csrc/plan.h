@@ -255,7 +255,17 @@ MSG_HD void plan_events(const msg_preset& p, const double* bp, const Zig& z, int
     }
     info.pool_len = pool;
     info.max_n = max_n;
-    // early reflections (MS:410-417): uniform delays, then uniform gains, same stream
+    // early reflections (MS:410-417): uniform delays, then uniform gains, same stream.
+    // er_gain null: the offsets only (the host batch path; k_er_gains draws the
+    // gains on the device from the same stream positions)
+    if (er_off && !er_gain) {
+        Pcg64 ge = nprng::default_rng((uint64_t)(p.seed + 202));
+        const int32_t ntap = p.er_taps > 1 ? p.er_taps : 1;
+        for (int32_t j = 0; j < ntap; ++j) {
+            const double d = nprng::uniform(ge, 0.3, p.er_max_ms) / 1000.0;
+            er_off[j] = (int32_t)rint(d * (double)p.base_sr);
+        }
+    }
     if (er_off && er_gain) {
         Pcg64 ge = nprng::default_rng((uint64_t)(p.seed + 202));
         const int32_t ntap = p.er_taps > 1 ? p.er_taps : 1;

@@ -374,3 +374,23 @@ def test_filter_spectra_early_same_bits(msgpu, irs):
     _, late = _render_env(params, {"MSGPU_H_EARLY": "0"})
     _, early = _render_env(params, {"MSGPU_H_EARLY": "1"})
     assert np.array_equal(late, early)
+
+
+def test_er_gains_on_device(msgpu, irs):
+    """The host batch path plans the ER offsets and k_er_gains draws the gains on
+    the device (MSGPU_ER_DEV=1, the default) from the same stream positions,
+    merged taps summed in tap order; against the host-drawn gains (=0) the
+    renders agree to the last float64 ulp of exp: a preset with many merged
+    offsets (2000 taps within 5 ms at 48 kHz), C3, H48 and a 192 kHz ER + IR."""
+    base = dict(gen_mode="Resonant strike", event_process="Poisson", _ir_audio=irs["tiny_room_ir"])
+    params = [msgpu.merged(base, base_sr=48000, out_dur_s=0.4, er_cloud_on=True, er_taps=2000, er_max_ms=5.0,
+                           space_ir_on=False, seed=31),
+              msgpu.config_params("C3", seed=1500, irs=irs, out_dur_s=0.3),
+              msgpu.config_params("H48", seed=1501, irs=irs, out_dur_s=0.5),
+              msgpu.merged(base, base_sr=192000, out_dur_s=0.3, er_cloud_on=True, er_taps=640, er_max_ms=120.0,
+                           space_ir_on=True, space_ir_max_samps=8192, seed=32)]
+    _, host = _render_env(params, {"MSGPU_ER_DEV": "0"})
+    _, dev = _render_env(params, {"MSGPU_ER_DEV": "1"})
+    d = float(np.max(np.abs(host - dev)))
+    print(f"max |host-drawn - device-drawn| = {d:.3e}, identical samples {np.mean(host == dev):.4f}")
+    assert d <= 1e-6
