@@ -626,38 +626,47 @@ k_gen_normal(const msg_preset* __restrict__ presets, const msg_event* __restrict
 // Early-reflection gains of the host batch path (MS:410-417).  The host planned
 // the offsets (draws j of default_rng(seed + 202)) and merged equal ones; tap
 // j's gain is draw ntap + j of the same stream times exp(-42 d_j), and the taps
-// of one merged slot add in tap order.  One wave per preset, lanes over its live
-// slots, every draw reached by jump-ahead; products and sums rounded one by one
-// (no contraction), as the host's plan.h does them.
+// of one merged slot add in tap order.  One workgroup per preset: each thread
+// jumps to its run of taps in both halves of the stream and steps through it,
+// writing the per-tap gains to g_tap; then threads over the live slots add
+// them up.  Products and sums are rounded one by one (no contraction), as the
+// host's plan.h does them.
 // ---------------------------------------------------------------------------
-MSG_DEV double er_uniform(const nprng::Pcg64& g0, uint64_t k, double lo, double hi) {
-    nprng::Pcg64 g = g0;
-    g.state = nprng::apply_jump(nprng::jump_of(k), g0.state, g0.inc);
+constexpr int ER_T = 256;
+
+MSG_DEV double er_uniform(nprng::Pcg64& g, double lo, double hi) {
     return __dadd_rn(lo, __dmul_rn(hi - lo, nprng::next_double(g)));
 }
 
-__global__ void __launch_bounds__(64)
+__global__ void __launch_bounds__(ER_T)
 k_er_gains(const msg_preset* __restrict__ presets, const PresetRt* __restrict__ rt, int n_presets,
            const int32_t* __restrict__ er_key, const int32_t* __restrict__ er_first,
-           const int32_t* __restrict__ er_cnt, double* __restrict__ er_gain) {
+           const int32_t* __restrict__ er_cnt, double* __restrict__ g_tap, double* __restrict__ er_gain) {
     const int p = blockIdx.x;
     if (p >= n_presets) return;
     const msg_preset& pr = presets[p];
-    if (!(pr.flags & MSG_F_ER_CLOUD)) return;
+    if (!(pr.flags & MSG_F_ER_CLOUD)) return;                // uniform: before any barrier
     const PresetRt& r = rt[p];
     const int ntap = pr.er_taps > 1 ? pr.er_taps : 1;
-    const nprng::Pcg64 g0 = nprng::default_rng((uint64_t)(pr.seed + 202));
     const int b = r.er_base;
-    for (int sl = (int)threadIdx.x; sl < r.n_taps; sl += 64) {
-        const int f = er_first[b + sl], c = er_cnt[b + sl];
-        double acc = 0.0;
-        for (int i = 0; i < c; ++i) {
-            const int j = er_key[b + f + i];
-            const double d = er_uniform(g0, (uint64_t)j, 0.3, pr.er_max_ms) / 1000.0;
-            const double u = er_uniform(g0, (uint64_t)(ntap + j), -1.0, 1.0);
-            const double gn = __dmul_rn(u, exp(__dmul_rn(-d, 42.0)));
-            acc = i == 0 ? gn : __dadd_rn(acc, gn);
+    const int per = (ntap + ER_T - 1) / ER_T;
+    const int j0 = (int)threadIdx.x * per, j1 = min(j0 + per, ntap);
+    if (j0 < j1) {
+        const nprng::Pcg64 g0 = nprng::default_rng((uint64_t)(pr.seed + 202));
+        nprng::Pcg64 gd = g0, gu = g0;                        // draws j0 .. and ntap + j0 ..
+        gd.state = nprng::apply_jump(nprng::jump_of((uint64_t)j0), g0.state, g0.inc);
+        gu.state = nprng::apply_jump(nprng::jump_of((uint64_t)(ntap + j0)), g0.state, g0.inc);
+        for (int j = j0; j < j1; ++j) {
+            const double d = er_uniform(gd, 0.3, pr.er_max_ms) / 1000.0;
+            const double u = er_uniform(gu, -1.0, 1.0);
+            g_tap[b + j] = __dmul_rn(u, exp(__dmul_rn(-d, 42.0)));
         }
+    }
+    __syncthreads();                                          // the preset's per-tap gains, workgroup-visible
+    for (int sl = (int)threadIdx.x; sl < r.n_taps; sl += ER_T) {
+        const int f = er_first[b + sl], c = er_cnt[b + sl];
+        double acc = g_tap[b + er_key[b + f]];
+        for (int i = 1; i < c; ++i) acc = __dadd_rn(acc, g_tap[b + er_key[b + f + i]]);
         er_gain[b + sl] = acc;
     }
 }

@@ -260,6 +260,7 @@ struct msg_ctx {
     Slice<double> er_gain;
     Slice<int32_t> er_key, er_first, er_cnt;
     DevBuf<double> er_gain_d;           // k_er_gains' output (host batch path)
+    DevBuf<double> er_tap_d;            // k_er_gains' per-tap gains
     Slice<EventRt> ert;
     Slice<PresetRt> prt;
     Slice<int32_t> gen_list, spec_small, spec_big, tile_begin, fir_begin, h_begin, st_begin, fir_plan_of;
@@ -2009,10 +2010,11 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
     const double* erg = ctx->er_gain.p;
     if (er_dev) {
         HIPCHK(ctx, ctx->er_gain_d.ensure((size_t)std::max<int64_t>(1, ntaps)));
+        HIPCHK(ctx, ctx->er_tap_d.ensure((size_t)std::max<int64_t>(1, ntaps)));
         erg = ctx->er_gain_d.p;
         if (ntaps > 0) {
-            hipLaunchKernelGGL(k_er_gains, dim3((unsigned)P), dim3(64), 0, s, ctx->presets.p, ctx->prt.p, P,
-                               ctx->er_key.p, ctx->er_first.p, ctx->er_cnt.p, ctx->er_gain_d.p);
+            hipLaunchKernelGGL(k_er_gains, dim3((unsigned)P), dim3(ER_T), 0, s, ctx->presets.p, ctx->prt.p, P,
+                               ctx->er_key.p, ctx->er_first.p, ctx->er_cnt.p, ctx->er_tap_d.p, ctx->er_gain_d.p);
             HIPCHK(ctx, hipGetLastError());
         }
     }
