@@ -2006,17 +2006,14 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
     HIPCHK(ctx, h2d(&ctx->imgbank.p, imgbank.data(), imgbank.size()));
     const auto h2 = hclock::now();
     HIPCHK(ctx, ctx->staging.flush(s));
-    // the merged ER gains (host batch path), before any filter kernel reads them
+    // the merged ER gains (host batch path): k_er_gains runs first in
+    // launch_h_spectra, before every filter kernel that reads them (the float64
+    // FIR's k_h64 comes later still), so it does not hold up the generator
     const double* erg = ctx->er_gain.p;
     if (er_dev) {
         HIPCHK(ctx, ctx->er_gain_d.ensure((size_t)std::max<int64_t>(1, ntaps)));
         HIPCHK(ctx, ctx->er_tap_d.ensure((size_t)std::max<int64_t>(1, ntaps)));
         erg = ctx->er_gain_d.p;
-        if (ntaps > 0) {
-            hipLaunchKernelGGL(k_er_gains, dim3((unsigned)P), dim3(ER_T), 0, s, ctx->presets.p, ctx->prt.p, P,
-                               ctx->er_key.p, ctx->er_first.p, ctx->er_cnt.p, ctx->er_tap_d.p, ctx->er_gain_d.p);
-            HIPCHK(ctx, hipGetLastError());
-        }
     }
     if (ctx->profiling) {
         const auto h3 = hclock::now();
@@ -2038,6 +2035,11 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
     // behind a persistent k_fir8p of another stream that holds every CU
     // (C5's fir_h window had been ~100x its isolated time).
     auto launch_h_spectra = [&]() -> int {
+        if (er_dev && ntaps > 0) {
+            hipLaunchKernelGGL(k_er_gains, dim3((unsigned)P), dim3(ER_T), 0, s, ctx->presets.p, ctx->prt.p, P,
+                               ctx->er_key.p, ctx->er_first.p, ctx->er_cnt.p, ctx->er_tap_d.p, ctx->er_gain_d.p);
+            HIPCHK(ctx, hipGetLastError());
+        }
         if (htiles > 0)
             HIPCHK(ctx, launch_h_build((unsigned)htiles, s, ctx->prt.p, ctx->h_tile_begin.p, P, ctx->er_off.p,
                                        erg, ctx->irbank.p, ctx->hscratch.p));

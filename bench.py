@@ -51,7 +51,8 @@ STAGE_KERNEL = {"generate": ("k_gen_normal",), "spectral": ("k_spec3", "k_spectr
                 # the stereo window also holds the float64 FIR route (flag, h, spectra,
                 # blocks, peak again) and the odd-length rotation
                 "stereo": ("k_stereo_max", "k_stereo_out", "k_stereo_remax", "k_fir64", "k_h64", "k_hspec64", "k_so_"),
-                "fir_h": ("k_fir8_hconv", "k_fir8_spec", "k_h_build", "k_fir4_hpart", "k_fir_h", "k_ir_spec")}
+                "fir_h": ("k_er_gains", "k_fir8_hconv", "k_fir8_spec", "k_h_build", "k_fir4_hpart", "k_fir4_hconv",
+                          "k_fir4_irspec", "k_fir_h", "k_ir_spec")}
 STAGE_NAMES = ["plan", "host_prep", "generate", "spectral", "overlap_add", "fir", "stereo", "total",
                "fir_kernel", "fir_h", "host_plan_wall", "host_records_wall", "host_upload_wall",
                "host_plan_sizes", "host_plan_events", "host_preset_records", "host_event_records", "host_lists",
