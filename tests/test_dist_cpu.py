@@ -180,3 +180,31 @@ def test_plan_costs_track_config_size():
 def test_single_rank_reduce_is_identity():
     assert bench.max_over_ranks(1.5, 1, "cpu") == 1.5
     assert np.array_equal(bench.rank_seeds(0, 4), [1000, 1001, 1002, 1003])
+
+
+def test_stage_bytes_follow_the_fused_overlap_add():
+    """bench.stage_bytes: with the overlap-add inside the FIR (fused share f),
+    the grain reads move from the overlap-add to the FIR kernel and the mono
+    write + read between them disappear; f = 0 is the two-kernel accounting,
+    and fir_rfft sums the spectral and FIR bytes over the three stage windows."""
+    class Info:
+        def __init__(self, pool_len, out_n):
+            self.pool_len, self.out_n = pool_len, out_n
+    infos = [Info(1000, 400), Info(3000, 600)]
+    sum_n, out_n = 4000, 1000
+    plain = bench.stage_bytes(infos)
+    assert plain["overlap_add"] == 4 * sum_n + 4 * out_n
+    assert plain["fir_kernel"] == plain["fir"] == 8 * out_n
+    assert plain["spectral"] == 8 * sum_n and plain["stereo"] == 16 * out_n
+    fused = bench.stage_bytes(infos, fused=1.0)
+    assert fused["overlap_add"] == 0
+    assert fused["fir_kernel"] == 4 * sum_n + 4 * out_n
+    half = bench.stage_bytes(infos, fused=0.5)
+    assert half["overlap_add"] == 0.5 * plain["overlap_add"]
+    assert half["fir_kernel"] == 0.5 * plain["fir_kernel"] + 0.5 * fused["fir_kernel"]
+    assert bench.stage_bytes(infos, fused=7.0) == fused          # clamped to [0, 1]
+    st = {"spectral": 2.0, "fir_h": 0.5, "fir_kernel": 1.5}
+    r = bench.fir_rfft(plain, st, "test")
+    assert r["ms"] == 4.0
+    assert r["algorithmic_bytes"] == plain["spectral"] + plain["fir_kernel"]
+    assert abs(r["achieved"] - r["algorithmic_bytes"] / 4e-3 / 1e9) < 0.1
