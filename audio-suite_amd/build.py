@@ -32,7 +32,7 @@ CSRC = os.path.join(HERE, "csrc")
 OBJ = os.path.join(HERE, "build")
 OUT = os.path.join(HERE, "msgpu", "libmsgpu.so")
 TUS = ["msgpu.hip", "k_spectral.hip", "k_spectral_ct.hip", "k_spec3.hip", "k_fir.hip", "k_grain64.hip", "k_grain64_lds.hip",
-       "k_grain64_glb.hip", "k_stereo_odd.hip", "k_fir64.hip", "k_stereo.hip"]
+       "k_grain64_glb.hip", "k_stereo_odd.hip", "k_fir64.hip", "k_stereo.hip", "k_digest.hip"]
 HEADERS = [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".h")] + \
           [os.path.join(os.path.dirname(HERE), "include", "msgpu.h")]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")

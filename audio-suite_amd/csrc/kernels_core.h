@@ -771,8 +771,8 @@ k_ola_slots(const msg_event* __restrict__ events, const PresetRt* __restrict__ r
             const int32_t* __restrict__ slot_preset, const int32_t* __restrict__ n_slots, int tmax,
             const float* __restrict__ grain_pool, float* __restrict__ mono) {
     const int ns = *n_slots;
-    for (int j = blockIdx.x; j < ns * tmax; j += gridDim.x) {
-        const int sl = j / tmax, t = j - sl * tmax;
+    for (int64_t j = blockIdx.x; j < (int64_t)ns * tmax; j += gridDim.x) {   // 64-bit: ns * tmax can pass 2^31
+        const int sl = (int)(j / tmax), t = (int)(j - (int64_t)sl * tmax);
         const PresetRt& r = rt[__builtin_amdgcn_readfirstlane(slot_preset[sl])];
         if (!r.ola_fir || (int64_t)t * OLA_TILE >= r.out_n) continue;   // uniform
         ola_tile(events, r, (int64_t)t * OLA_TILE, grain_pool, mono);

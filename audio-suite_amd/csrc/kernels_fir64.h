@@ -77,8 +77,8 @@ k_h64(const PresetRt* __restrict__ rt, const Fir64Rt* __restrict__ fr, const int
     __shared__ int32_t s_off[H_T];
     __shared__ double s_g[H_T];
     const int ns = fir64_window(n_slots, w0, cap);
-    for (int j = blockIdx.x; j < ns * tmax; j += gridDim.x) {
-        const int sl = j / tmax, t = j - sl * tmax;
+    for (int64_t j = blockIdx.x; j < (int64_t)ns * tmax; j += gridDim.x) {
+        const int sl = (int)(j / tmax), t = (int)(j - (int64_t)sl * tmax);
         const int p = slot_preset[w0 + sl];
         if (t * H_TILE >= fr[p].h_len) continue;               // uniform
         __syncthreads();
@@ -96,8 +96,8 @@ k_hspec64(const Fir64Rt* __restrict__ fr, const Real64Plan* __restrict__ plans, 
     const Real64Plan& rp = plans[plan];
     double* d = reinterpret_cast<double*>(buf);
     const int ns = fir64_window(n_slots, w0, cap);
-    for (int j = blockIdx.x; j < ns * qmax; j += gridDim.x) {
-        const int sl = j / qmax, q = j - sl * qmax;
+    for (int64_t j = blockIdx.x; j < (int64_t)ns * qmax; j += gridDim.x) {
+        const int sl = (int)(j / qmax), q = (int)(j - (int64_t)sl * qmax);
         const int p = slot_preset[w0 + sl];
         const int hl = fr[p].h_len;
         if (q >= fr[p].q) continue;
@@ -125,8 +125,8 @@ k_fir64(const PresetRt* __restrict__ rt, const Fir64Rt* __restrict__ fr, const R
     const int ns = fir64_window(n_slots, w0, cap);
     constexpr int NE = (FIR64_K + FIR64_T - 1) / FIR64_T;
     static_assert(NE <= FIR64_E + 1, "bins per thread");
-    for (int j = blockIdx.x; j < ns * bmax; j += gridDim.x) {
-        const int sl = j / bmax, b = j - sl * bmax;
+    for (int64_t j = blockIdx.x; j < (int64_t)ns * bmax; j += gridDim.x) {
+        const int sl = (int)(j / bmax), b = (int)(j - (int64_t)sl * bmax);
         const int p = slot_preset[w0 + sl];
         const Fir64Rt f = fr[p];
         if (b >= f.blocks) continue;

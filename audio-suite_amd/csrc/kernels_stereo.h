@@ -376,8 +376,8 @@ k_stereo_remax(const PresetRt* __restrict__ rt, const int32_t* __restrict__ st_c
     __shared__ __attribute__((aligned(16))) float w[ST_WIN];
     __shared__ float wm[3 * (ST_T / 64)];
     const int ns = *n_slots;
-    for (int j = blockIdx.x; j < ns * tmax; j += gridDim.x) {
-        const int sl = j / tmax, t = j - sl * tmax;
+    for (int64_t j = blockIdx.x; j < (int64_t)ns * tmax; j += gridDim.x) {   // 64-bit: ns * tmax can pass 2^31
+        const int sl = (int)(j / tmax), t = (int)(j - (int64_t)sl * tmax);
         const int p = st_rfl(slot_preset[sl]);
         if (t >= st_count[p]) continue;                          // uniform
         __syncthreads();
@@ -470,8 +470,8 @@ k_stereo_out_list(const PresetRt* __restrict__ rt, const int32_t* __restrict__ s
     __shared__ __attribute__((aligned(16))) float w[ST_WIN];
     __shared__ __attribute__((aligned(16))) float lw[ST_TILE];
     const int nl = *n_list;
-    for (int j = blockIdx.x; j < nl * tmax; j += gridDim.x) {
-        const int sl = j / tmax, t = j - sl * tmax;
+    for (int64_t j = blockIdx.x; j < (int64_t)nl * tmax; j += gridDim.x) {
+        const int sl = (int)(j / tmax), t = (int)(j - (int64_t)sl * tmax);
         const int p = st_rfl(list[sl]);
         if (t >= st_count[p]) continue;                          // uniform
         __syncthreads();                                         // the previous tile's LDS reads are done

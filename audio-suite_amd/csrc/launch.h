@@ -168,3 +168,11 @@ hipError_t launch_stereo_odd(int64_t n, int row_max, int col_max, int dr, double
 // the app's spectrogram (stft_mag_db, MS:197-212) on the float64 engine
 hipError_t launch_stft64(unsigned frames, int lds_bytes, hipStream_t s, const Real64Plan* plans, int plan,
                          const void* x, int elem_bytes, int64_t n, int channels, int win, int hop, double* S);
+
+// per-render summary and digest (kernels_digest.h): tiles of 2048 frames, then
+// one fold per render into res (msg_digest_rec records); part holds one
+// 48-byte partial per tile.  digest_host: the same fold on the host.
+hipError_t launch_digest(int n, int n_tiles, hipStream_t s, const float* out, const int64_t* frame_off,
+                         const int64_t* frames, const int32_t* tile_base, void* part, void* res);
+int64_t digest_tiles(int64_t frames);
+void digest_host(const float* x, int64_t frames, void* rec);

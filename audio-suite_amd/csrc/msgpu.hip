@@ -214,6 +214,7 @@ struct msg_ctx {
     bool fir4c = true;
     bool fir8 = true;            // N = 65536 one-partition filters on k_fir8 (MSGPU_FIR8=0: off, A/B and tests)
     int fir64 = 1;               // float64 FIR of saturated renders: 0 off, 1 predicted, 2 every FIR preset (MSGPU_FIR64)
+    int fir64_cap = FIR64_CAP;   // float64 FIR slots per window (MSGPU_FIR64_CAP: tests force several windows)
     // k_fir8 blocks (MSGPU_FIR8P): 0 one workgroup per block, 1 persistent workgroups
     // (one per CU, per-XCD block counters; C3 isolated FIR 2.03 -> 1.86 ms, C5 131.6
     // -> 125.9 ms per step, profiles/r04r_ab.json)
@@ -281,8 +282,8 @@ struct msg_ctx {
     Slice<int32_t> st_count, odd_list, odd_cnt;
     DevBuf<double> f64_stats;                   // per preset: sum y^2, sum (1 + (d y)^2)^-2
     DevBuf<int32_t> f64_flag, f64_slot_preset, f64_nslots;
-    // stereo pass (kernels_stereo.h): the fused persistent launch (MSGPU_STEREO_FUSED,
-    // default 1) and its per-preset sync state, per-tile partial sums, counters
+    // stereo pass (kernels_stereo.h): the fused persistent launch (MSGPU_STEREO_FUSED=1;
+    // off by default) and its per-preset sync state, per-tile partial sums, counters
     bool stereo_fused = false;          // measured slower than the two launches
     int st_wgs = 4;                     // k_stereo_fused workgroups per CU (MSGPU_STEREO_WGS)
     uint32_t st_epoch = 0;
@@ -310,6 +311,9 @@ struct msg_ctx {
     DevBuf<double> sf_h;
     DevBuf<float2> sf_hspec, sf_xspec;
     DevBuf<float> sf_hf;                        // float taps of a k_fir8 filter
+    // msg_digest: render extents + tile bases, per-tile partials
+    DevBuf<int64_t> dg_meta;
+    DevBuf<char> dg_part;
     // odd-length stereo rotation (kernels_stereo_odd.h)
     std::map<int64_t, DevBuf<double2>> so_bp;  // chirp kernel spectra by n (float64), LRU-bounded
     std::map<int64_t, uint64_t> so_bp_use;     // batch serial of each entry's last use
@@ -646,6 +650,14 @@ struct DoneGuard {
     ~DoneGuard() { if (armed) stream_done(ctx, s); }
 };
 
+// k_fir8p's per-XCD block counters: zeroed once; every launch leaves them zero
+static hipError_t fir8_counters(msg_ctx* ctx, hipStream_t s) {
+    if (ctx->fir8_ctr.p) return hipSuccess;
+    const hipError_t e = ctx->fir8_ctr.ensure((size_t)(MSG_XCDS + 1) * FIR8P_CTR);
+    if (e != hipSuccess) return e;
+    return hipMemsetAsync(ctx->fir8_ctr.p, 0, sizeof(int32_t) * ctx->fir8_ctr.cap, s);
+}
+
 // Wait for the context's last batch (not the whole device: other contexts'
 // streams keep running).
 static hipError_t wait_last(msg_ctx* ctx) {
@@ -666,6 +678,7 @@ int64_t msg_sizeof(int32_t which) {
         case 0: return (int64_t)sizeof(msg_preset);
         case 1: return (int64_t)sizeof(msg_event);
         case 2: return (int64_t)sizeof(msg_plan_info);
+        case 3: return (int64_t)sizeof(msg_digest_rec);
         default: return -1;
     }
 }
@@ -734,6 +747,7 @@ msg_ctx* msg_create(int device_ordinal) {
     if (const char* e = getenv("MSGPU_FIR4C")) ctx->fir4c = e[0] != '0';
     if (const char* e = getenv("MSGPU_FIR8")) ctx->fir8 = e[0] != '0';
     if (const char* e = getenv("MSGPU_FIR64")) ctx->fir64 = atoi(e);
+    if (const char* e = getenv("MSGPU_FIR64_CAP")) ctx->fir64_cap = std::max(1, std::min(FIR64_CAP, atoi(e)));
     if (const char* e = getenv("MSGPU_FIR8P")) ctx->fir8p = atoi(e);
     if (const char* e = getenv("MSGPU_FIR8P_CUS")) ctx->fir8p_cus = std::max(0, atoi(e));
     if (const char* e = getenv("MSGPU_FIR8P_STAGGER")) ctx->fir8p_stagger = std::max(0, atoi(e));
@@ -798,6 +812,7 @@ void msg_destroy(msg_ctx* ctx) {
     hipFree(ctx->d_spec3_tab);
     ctx->sf_prt.release(); ctx->sf_jobs.release(); ctx->sf_irjobs.release(); ctx->sf_h.release();
     ctx->sf_hspec.release(); ctx->sf_xspec.release(); ctx->sf_hf.release();
+    ctx->dg_meta.release(); ctx->dg_part.release();
     for (auto& set : ctx->ev)
         for (auto& ev : set) hipEventDestroy(ev);
     {
@@ -1035,8 +1050,16 @@ int msg_fir(msg_ctx* ctx, const float* x_dev, float* y_dev, int64_t n, int32_t n
         HIPCHK(ctx, hipMemcpyAsync(ctx->sf_hf.p, hf.data(), sizeof(float) * (size_t)M, hipMemcpyHostToDevice, s));
         HIPCHK(ctx, hipMemcpyAsync(ctx->sf_irjobs.p, job, sizeof(job), hipMemcpyHostToDevice, s));
         HIPCHK(ctx, launch_fir8_spec32(1, s, ctx->sf_irjobs.p, ctx->d_fir4tab, ctx->sf_hf.p, ctx->sf_hspec.p));
-        HIPCHK(ctx, launch_fir8((unsigned)fj.size(), s, ctx->sf_prt.p, ctx->sf_jobs.p, ctx->d_fir4tab, ctx->sf_hspec.p,
-                                x_dev, y_dev));
+        if (ctx->fir8p > 0) {   // persistent, as in the render (one workgroup per CU, per-XCD block counters)
+            const int nj = (int)fj.size();
+            const unsigned grid = (unsigned)std::max(MSG_XCDS, (std::min(nj, ctx->n_cu) / MSG_XCDS) * MSG_XCDS);
+            HIPCHK(ctx, fir8_counters(ctx, s));
+            HIPCHK(ctx, launch_fir8p((unsigned)nj, grid, s, ctx->sf_prt.p, ctx->sf_jobs.p, ctx->d_fir4tab,
+                                     ctx->sf_hspec.p, x_dev, y_dev, ctx->fir8_ctr.p, 0, nullptr, nullptr, nullptr));
+        } else {
+            HIPCHK(ctx, launch_fir8((unsigned)fj.size(), s, ctx->sf_prt.p, ctx->sf_jobs.p, ctx->d_fir4tab,
+                                    ctx->sf_hspec.p, x_dev, y_dev));
+        }
         HIPCHK(ctx, done.finish());
         return MSG_OK;
     }
@@ -1090,6 +1113,46 @@ int msg_fir(msg_ctx* ctx, const float* x_dev, float* y_dev, int64_t n, int32_t n
     // pageable-host H2D copies are staged before hipMemcpyAsync returns (as in
     // msg_render_batch), so the host vectors may go; the FIR runs asynchronously.
     HIPCHK(ctx, done.finish());
+    return MSG_OK;
+}
+
+int msg_digest(msg_ctx* ctx, const float* out_dev, const int64_t* out_offsets, const int64_t* out_n,
+               int32_t n_renders, msg_digest_rec* rec_dev, void* stream) {
+    if (!ctx || !out_offsets || !out_n || !rec_dev || n_renders < 0) return fail(ctx, MSG_E_ARG, "bad arguments");
+    if (n_renders == 0) return MSG_OK;
+    // rows: [0, n) frame offsets, [n, 2n) frames, then n + 1 tile bases (int32) in the same upload
+    std::vector<int64_t> meta((size_t)2 * n_renders + (n_renders + 2) / 2 + 1, 0);
+    int32_t* tb = reinterpret_cast<int32_t*>(meta.data() + 2 * (size_t)n_renders);
+    int64_t tiles = 0;
+    for (int i = 0; i < n_renders; ++i) {
+        if (out_n[i] < 0 || out_n[i] > MSG_MAX_FRAMES || out_offsets[i] < 0)
+            return fail(ctx, MSG_E_ARG, "bad render extent");
+        meta[i] = out_offsets[i];
+        meta[(size_t)n_renders + i] = out_n[i];
+        tb[i] = (int32_t)tiles;
+        tiles += digest_tiles(out_n[i]);
+        if (tiles > INT32_MAX) return fail(ctx, MSG_E_UNSUPPORTED, "too many digest tiles");
+    }
+    tb[n_renders] = (int32_t)tiles;
+    if (tiles > 0 && !out_dev) return fail(ctx, MSG_E_ARG, "null output buffer");
+    HIPCHK(ctx, hipSetDevice(ctx->device));
+    hipStream_t s = (hipStream_t)stream;
+    HIPCHK(ctx, stream_handover(ctx, s));
+    DoneGuard done(ctx, s);
+    HIPCHK(ctx, ctx->dg_meta.ensure(meta.size()));
+    HIPCHK(ctx, ctx->dg_part.ensure((size_t)std::max<int64_t>(1, tiles) * sizeof(msg_digest_rec)));
+    // a pageable source is staged before hipMemcpyAsync returns (as msg_fir's uploads)
+    HIPCHK(ctx, hipMemcpyAsync(ctx->dg_meta.p, meta.data(), sizeof(int64_t) * meta.size(), hipMemcpyHostToDevice, s));
+    const int64_t* dm = ctx->dg_meta.p;
+    HIPCHK(ctx, launch_digest(n_renders, (int)tiles, s, out_dev, dm, dm + n_renders,
+                              reinterpret_cast<const int32_t*>(dm + 2 * (size_t)n_renders), ctx->dg_part.p, rec_dev));
+    HIPCHK(ctx, done.finish());
+    return MSG_OK;
+}
+
+int msg_digest_host(const float* x, int64_t out_n, msg_digest_rec* rec) {
+    if (!rec || out_n < 0 || (out_n > 0 && !x)) return fail(nullptr, MSG_E_ARG, "bad arguments");
+    digest_host(x, out_n, rec);
     return MSG_OK;
 }
 
@@ -1982,7 +2045,7 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
     const int64_t f64_hsstride = (int64_t)f64_qmax * FIR64_K;
     // slots per window: every flagged preset is served, FIR64_WINDOW_BYTES of h and H_q at a time
     const int64_t f64_slot_bytes = f64_hstride * (int64_t)sizeof(float) + f64_hsstride * (int64_t)sizeof(double2);
-    const int f64_cap = (int)std::max<int64_t>(1, std::min<int64_t>(std::min(f64_cand, FIR64_CAP),
+    const int f64_cap = (int)std::max<int64_t>(1, std::min<int64_t>(std::min(f64_cand, ctx->fir64_cap),
                                                                      FIR64_WINDOW_BYTES / std::max<int64_t>(1, f64_slot_bytes)));
     if (f64_on) {
         HIPCHK(ctx, ctx->f64_stats.ensure(2 * (size_t)P));
@@ -2146,10 +2209,7 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
                 const int cus = ctx->fir8p_cus > 0 ? std::min(ctx->fir8p_cus, ctx->n_cu)
                                                    : (h_early ? ctx->n_cu - ctx->n_cu / 8 : ctx->n_cu);
                 const unsigned grid = (unsigned)std::max(MSG_XCDS, (std::min((int)nj, cus) / MSG_XCDS) * MSG_XCDS);
-                if (!ctx->fir8_ctr.p) {   // zeroed once; every launch leaves the counters zero
-                    HIPCHK(ctx, ctx->fir8_ctr.ensure((size_t)(MSG_XCDS + 1) * FIR8P_CTR));
-                    HIPCHK(ctx, hipMemsetAsync(ctx->fir8_ctr.p, 0, sizeof(int32_t) * ctx->fir8_ctr.cap, s));
-                }
+                HIPCHK(ctx, fir8_counters(ctx, s));
                 HIPCHK(ctx, launch_fir8p(nj, grid, s, ctx->prt.p, ctx->fir_jobs.p + fjob_off[i],
                                          ctx->d_fir4tab, ctx->hspec.p, ctx->mono_a.p, ctx->mono_y.p, ctx->fir8_ctr.p,
                                          ctx->fir8p_stagger,
@@ -2259,7 +2319,7 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
     int odd_tmax = 0;
     for (int p : odd_presets) odd_tmax = std::max(odd_tmax, st_count[p]);
     if (f64_on)   // the float64 presets' peak from their new y (and R)
-        HIPCHK(ctx, launch_stereo_remax((unsigned)std::min(f64_cand * f64_stmax, 256), s, ctx->prt.p, ctx->st_count.p,
+        HIPCHK(ctx, launch_stereo_remax((unsigned)std::min<int64_t>((int64_t)f64_cand * f64_stmax, 256), s, ctx->prt.p, ctx->st_count.p,
                                         ctx->f64_slot_preset.p, ctx->f64_nslots.p, f64_stmax, yb, ctx->so_r2.p,
                                         ctx->maxbits.p));
     if (n_odd > 0)   // odd lengths: the peak of the rotated R
@@ -2268,7 +2328,7 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
                                         ctx->maxbits.p));
     if (st_fused) {   // the deferred presets' output
         if (f64_on)
-            HIPCHK(ctx, launch_stereo_out_list((unsigned)std::min(f64_cand * f64_stmax, 1024), s, ctx->prt.p,
+            HIPCHK(ctx, launch_stereo_out_list((unsigned)std::min<int64_t>((int64_t)f64_cand * f64_stmax, 1024), s, ctx->prt.p,
                                                ctx->st_count.p, ctx->f64_slot_preset.p, ctx->f64_nslots.p, f64_stmax,
                                                yb, ctx->so_r2.p, ctx->maxbits.p, out_dev));
         if (n_odd > 0)

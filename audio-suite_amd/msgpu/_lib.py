@@ -76,6 +76,11 @@ class MsgPlanInfo(C.Structure):
                 ("n_slots", C.c_int32), ("max_n", C.c_int32), ("pool_len", C.c_int64)]
 
 
+class MsgDigestRec(C.Structure):
+    _fields_ = [("sum_sq", C.c_double), ("peak", C.c_double), ("sum_l", C.c_double), ("sum_r", C.c_double),
+                ("h0", C.c_uint64), ("h1", C.c_uint64)]
+
+
 # name -> (restype, argtypes)
 _PROTOS = {
     "msg_abi_version": (C.c_int, []),
@@ -108,6 +113,9 @@ _PROTOS = {
                           C.POINTER(C.c_int32), C.c_void_p]),
     "msg_stft_mag_db": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.c_int64, C.c_int32, C.c_int32, C.c_int32, C.c_int32,
                                   C.c_void_p, C.POINTER(C.c_int32), C.c_void_p]),
+    "msg_digest": (C.c_int, [C.c_void_p, C.c_void_p, C.POINTER(C.c_int64), C.POINTER(C.c_int64), C.c_int32,
+                             C.c_void_p, C.c_void_p]),
+    "msg_digest_host": (C.c_int, [C.c_void_p, C.c_int64, C.POINTER(MsgDigestRec)]),
     "msg_rng_raw": (C.c_int, [C.c_uint64, C.POINTER(C.c_uint64), C.c_int64]),
     "msg_rng_normal": (C.c_int, [C.c_uint64, C.POINTER(C.c_double), C.c_int64]),
     "msg_rng_exponential": (C.c_int, [C.c_uint64, C.POINTER(C.c_double), C.c_int64]),
@@ -144,7 +152,7 @@ def lib() -> C.CDLL:
                 f.argtypes = args
             if L.msg_abi_version() != ABI_VERSION:
                 raise RuntimeError("libmsgpu ABI version mismatch")
-            for which, st in enumerate((MsgPreset, MsgEvent, MsgPlanInfo)):
+            for which, st in enumerate((MsgPreset, MsgEvent, MsgPlanInfo, MsgDigestRec)):
                 if L.msg_sizeof(which) != C.sizeof(st):
                     raise RuntimeError(f"libmsgpu struct {st.__name__} size mismatch: "
                                        f"{L.msg_sizeof(which)} != {C.sizeof(st)}")

@@ -82,8 +82,8 @@ def _event_note(p, i):
 
 def render_batch(params_list, device: int = 0, results: str = "audio"):
     """Render many presets in one device batch; returns a list of (out_n, 2) float32
-    arrays ("audio"), per-preset summaries ("stats", multi.audio_stats's fields,
-    reduced on the device) or the device tensors themselves ("device")."""
+    arrays ("audio"), per-preset summaries ("stats", multi.rec_stats's fields,
+    reduced on the device by msg_digest) or the device tensors themselves ("device")."""
     if results not in ("audio", "stats", "device"):
         raise ValueError("results must be 'audio', 'stats' or 'device'")
     eng = default_engine(device)
@@ -93,7 +93,7 @@ def render_batch(params_list, device: int = 0, results: str = "audio"):
         return [out[int(o):int(o) + int(n)] for o, n in zip(packed.offsets, packed.out_n)]
     eng.torch.cuda.synchronize(eng.device)
     if results == "stats":
-        from .multi import _device_stats
-        return [_device_stats(out[int(o):int(o) + int(n)]) for o, n in zip(packed.offsets, packed.out_n)]
+        from .multi import device_stats
+        return device_stats(eng, out, packed.offsets, packed.out_n)
     host = out.cpu().numpy()
     return [host[o:o + n].copy() for o, n in zip(packed.offsets, packed.out_n)]

@@ -16,6 +16,11 @@ from . import _lib as L
 from .pack import PackedBatch
 
 
+# msg_digest_rec as a numpy record
+DIGEST_DTYPE = np.dtype([("sum_sq", "<f8"), ("peak", "<f8"), ("sum_l", "<f8"), ("sum_r", "<f8"),
+                         ("h0", "<u8"), ("h1", "<u8")])
+
+
 class Engine:
     def __init__(self, device: int = 0):
         import torch  # device buffers only
@@ -137,6 +142,34 @@ class Engine:
                                     hh.ctypes.data_as(C.c_void_p), int(hh.size), shape,
                                     C.c_void_p(stream.cuda_stream)), self._ctx)
         return out, tuple(shape)
+
+    def digest(self, out, offsets, out_n, stream=None):
+        """msg_digest of renders lying in a device output tensor ((frames, 2)
+        float32, render i at frame offsets[i], out_n[i] frames): one record per
+        render reduced on the device (float64 sums, peak, the 128-bit digest);
+        only the records (48 B each) are copied back.  Returns a numpy structured
+        array with fields sum_sq, peak, sum_l, sum_r, h0, h1."""
+        torch = self.torch
+        if out.dtype != torch.float32 or not out.is_contiguous() or out.device.type != "cuda":
+            raise ValueError("out must be a contiguous float32 device tensor")
+        off = np.ascontiguousarray(offsets, dtype=np.int64)
+        cnt = np.ascontiguousarray(out_n, dtype=np.int64)
+        if off.shape != cnt.shape or off.ndim != 1:
+            raise ValueError("offsets and out_n must be 1-D of one length")
+        if off.size and int((off + cnt).max()) * 2 > out.numel():
+            raise ValueError("a render extends past the output tensor")
+        n = int(off.size)
+        rec = torch.empty((max(n, 1), 6), dtype=torch.float64, device=out.device)
+        if stream is None:
+            stream = torch.cuda.current_stream(out.device)
+        with self._lock:
+            L.check(L.lib().msg_digest(self._ctx, C.c_void_p(out.data_ptr()),
+                                       off.ctypes.data_as(C.POINTER(C.c_int64)),
+                                       cnt.ctypes.data_as(C.POINTER(C.c_int64)), n, C.c_void_p(rec.data_ptr()),
+                                       C.c_void_p(stream.cuda_stream)), self._ctx)
+        with torch.cuda.stream(stream):
+            host = rec.cpu().numpy()       # ordered after the digest on its stream
+        return host[:n].copy().view(DIGEST_DTYPE).reshape(n)
 
     # ---- last-batch inspection -----------------------------------------
     def last_plan(self):

@@ -11,11 +11,13 @@ Three result modes (``render_batch(..., results=...)``):
   shared-memory block, in the caller's order -- what ``render`` returns, for
   batches whose outputs fit in host memory.
 * ``"stats"``: per preset only a summary -- out_n, rms over both channels, peak
-  |x|, the sum of each channel (float64, reduced on the device) and the SHA-1
-  of the float32 interleaved bytes (each preset copied to the host alone and
-  hashed).  For C4/C5-scale batches (C5's ~550 GB of outputs
-  cannot come back to one host); the reference's own batch path writes each
-  render out one at a time (MS:1585-1589).
+  |x|, the sum of each channel and a 128-bit digest of the float32 interleaved
+  bit patterns, all reduced on the device where the render lies (msg_digest,
+  kernels_digest.h): 48 bytes per preset cross PCIe, no audio.  For C4/C5-scale
+  batches (C5's ~550 GB of outputs cannot come back to one
+  host); the reference's own batch path writes each render out one at a time
+  (MS:1585-1589).  ``sha1=True`` adds the SHA-1 of each render's bytes (each
+  preset then copied to the host alone and hashed).
 * ``"device"``: the outputs stay in the workers' HBM; the call returns one
   :class:`DeviceResult` handle per preset.  ``pool.fetch(handle)`` copies one
   back, ``pool.release(handles)`` frees them.
@@ -69,27 +71,49 @@ def _gpu_touched() -> bool:
     return bool(engine._engines)
 
 
-def audio_stats(a) -> dict:
-    """Summary of one (out_n, 2) float32 render on the host (float64 sums)."""
+def rec_stats(rec, out_n) -> dict:
+    """The summary dict of one msg_digest record (rms over both channels)."""
+    n = int(out_n)
+    return {"out_n": n, "rms": float(np.sqrt(rec["sum_sq"] / (2 * n))) if n else 0.0,
+            "peak": float(rec["peak"]), "sum_l": float(rec["sum_l"]), "sum_r": float(rec["sum_r"]),
+            "digest": f"{int(rec['h0']):016x}{int(rec['h1']):016x}"}
+
+
+def digest_host(a):
+    """msg_digest_host of one (out_n, 2) float32 render in host memory: the record
+    the device computes, bit for bit (numpy structured scalar)."""
+    import ctypes as C
+    from . import _lib as L
+    from .engine import DIGEST_DTYPE
     a = np.ascontiguousarray(a, dtype=np.float32)
-    d = a.astype(np.float64)
-    return {"out_n": int(a.shape[0]), "rms": float(np.sqrt(np.mean(d * d))) if a.size else 0.0,
-            "peak": float(np.max(np.abs(d))) if a.size else 0.0,
-            "sum_l": float(d[:, 0].sum()), "sum_r": float(d[:, 1].sum()),
-            "sha1": hashlib.sha1(a.tobytes()).hexdigest()}
+    if a.ndim != 2 or a.shape[1] != 2:
+        raise ValueError("a must be (out_n, 2)")
+    r = L.MsgDigestRec()
+    L.check(L.lib().msg_digest_host(a.ctypes.data_as(C.c_void_p), int(a.shape[0]), C.byref(r)), None)
+    return np.array([(r.sum_sq, r.peak, r.sum_l, r.sum_r, r.h0, r.h1)], dtype=DIGEST_DTYPE)[0]
 
 
-def _device_stats(t) -> dict:
-    """The same summary of a device (out_n, 2) float32 tensor: the reductions in
-    float64 on the device, only the bytes for the hash cross PCIe."""
-    import torch
-    d = t.to(torch.float64)
-    n = int(t.shape[0])
-    host = t.cpu().numpy()
-    return {"out_n": n, "rms": float(torch.sqrt(torch.mean(d * d))) if n else 0.0,
-            "peak": float(torch.max(torch.abs(d))) if n else 0.0,
-            "sum_l": float(d[:, 0].sum()), "sum_r": float(d[:, 1].sum()),
-            "sha1": hashlib.sha1(np.ascontiguousarray(host).tobytes()).hexdigest()}
+def audio_stats(a, sha1: bool = False) -> dict:
+    """Summary of one (out_n, 2) float32 render on the host: the same record
+    msg_digest forms on the device (msg_digest_host), and the SHA-1 of its bytes
+    when asked."""
+    a = np.ascontiguousarray(a, dtype=np.float32)
+    st = rec_stats(digest_host(a), a.shape[0])
+    if sha1:
+        st["sha1"] = hashlib.sha1(a.tobytes()).hexdigest()
+    return st
+
+
+def device_stats(eng, out, offsets, out_n, stream=None, sha1: bool = False) -> list:
+    """Summaries of the renders in a device output tensor, reduced on the device
+    (Engine.digest); with sha1, each render is also copied to the host alone and
+    hashed."""
+    recs = eng.digest(out, offsets, out_n, stream=stream)
+    res = [rec_stats(r, n) for r, n in zip(recs, out_n)]
+    if sha1:
+        for st, o, n in zip(res, offsets, out_n):
+            st["sha1"] = hashlib.sha1(np.ascontiguousarray(out[int(o):int(o) + int(n)].cpu().numpy()).tobytes()).hexdigest()
+    return res
 
 
 def _stub_audio(i, device, n):
@@ -127,6 +151,11 @@ def _worker(slot, device, nworkers, stub, conn):
                 kept.pop(key, None)
             conn.send(("released", msg[1]))
             continue
+        if msg[0] == "drop":          # a failed device-mode job: everything kept for it
+            for key in [k for k in kept if k[0] == msg[2]]:
+                del kept[key]
+            conn.send(("released", msg[1]))
+            continue
         _, seq, mode, shm_name, idx, params, frame_off, out_n = msg
         t0 = time.perf_counter()
         err, payload = None, None
@@ -160,19 +189,22 @@ def _run_job(eng, stub, device, seq, mode, shm_name, idx, params, frame_off, out
         if e2 is not None:
             raise e2
         return None
+    sha1 = mode == "stats_sha1"
+    if sha1:
+        mode = "stats"
     if stub:
         out = []
         for i, n in zip(idx, out_n):
             a = _stub_audio(i, device, int(n))
             if mode == "stats":
-                out.append(audio_stats(a))
+                out.append(audio_stats(a, sha1=sha1))
             else:
                 key = (seq, int(i))
                 kept[key] = a
                 out.append(key)
         return out
-    sink = _StatsSink() if mode == "stats" else _KeepSink(kept, seq, idx)
-    _render_chunks(eng, params, sink)
+    sink = _StatsSink(eng, sha1) if mode == "stats" else _KeepSink(kept, seq, idx)
+    _render_chunks(eng, params, out_n, sink)
     return sink.result()
 
 
@@ -184,7 +216,7 @@ def _fill_audio(shm, stub, eng, device, idx, params, frame_off, out_n):
                 buf[o:o + n, 0] = float(idx[i])
                 buf[o:o + n, 1] = float(device)
         elif params:
-            _render_chunks(eng, params, _ShmSink(buf, frame_off))
+            _render_chunks(eng, params, out_n, _ShmSink(buf, frame_off))
     finally:
         del buf
 
@@ -205,14 +237,20 @@ class _ShmSink:
 
 
 class _StatsSink:
-    """Stats mode: per-preset summaries; at most one preset's bytes on the host."""
+    """Stats mode: per-preset summaries reduced on the device (one msg_digest per
+    device batch, on the drain stream); with sha1, one preset's bytes at a time
+    on the host."""
 
-    def __init__(self):
+    def __init__(self, eng, sha1=False):
+        self.eng, self.sha1 = eng, sha1
         self.stats = {}
 
     def take(self, chunk, packed, out):
-        for i, o, n in zip(chunk, packed.offsets, packed.out_n):
-            self.stats[i] = _device_stats(out[int(o):int(o) + int(n)])
+        import torch
+        res = device_stats(self.eng, out, packed.offsets, packed.out_n, stream=torch.cuda.current_stream(out.device),
+                           sha1=self.sha1)
+        for i, st in zip(chunk, res):
+            self.stats[i] = st
 
     def result(self):
         return [self.stats[i] for i in sorted(self.stats)]
@@ -235,17 +273,17 @@ class _KeepSink:
         return [self.keys[i] for i in sorted(self.keys)]
 
 
-def _render_chunks(eng, params, sink):
-    """Render ``params`` in device batches on a render stream; while batch k
-    renders, the host packs and plans batch k + 1 and drains batch k - 1 (its
-    output handed to ``sink.take(chunk, packed, out)`` on a second stream)."""
+def _render_chunks(eng, params, lens, sink):
+    """Render ``params`` (out_n ``lens``, from the job) in device batches on a
+    render stream; while batch k renders, the host packs and plans batch k + 1
+    and drains batch k - 1 (its output handed to ``sink.take(chunk, packed,
+    out)`` on a second stream)."""
     from .batch import _chunks
     from .pack import PackedBatch
     torch = eng.torch
     dev = eng.device
     rs = torch.cuda.Stream(device=dev)
     cs = torch.cuda.Stream(device=dev)
-    lens = PackedBatch(params).out_n
     prev = None
 
     def drain(item):
@@ -329,12 +367,13 @@ class DevicePool:
                                "out of step, pool closed")
         return msg
 
-    def render_batch(self, params_list, costs=None, results: str = "audio"):
+    def render_batch(self, params_list, costs=None, results: str = "audio", sha1: bool = False):
         """Render ``params_list`` across the pool's GPUs.  Returns, in the caller's
         order, the (out_n, 2) float32 outputs (``results="audio"``), a summary dict
-        per preset (``"stats"``) or a :class:`DeviceResult` per preset
-        (``"device"``).  ``last_split`` records each worker's preset range,
-        predicted cost, pid and time."""
+        per preset (``"stats"``: reduced on the device, see :func:`rec_stats`;
+        ``sha1=True`` adds each render's SHA-1, which copies it to the host) or a
+        :class:`DeviceResult` per preset (``"device"``).  ``last_split`` records
+        each worker's preset range, predicted cost, pid and time."""
         from multiprocessing import shared_memory
         from .pack import PackedBatch
         from .shard import balance, plan_costs
@@ -361,7 +400,8 @@ class DevicePool:
                 live = []
                 for w, c in enumerate(self._conns):
                     lo, hi = cuts[w], cuts[w + 1]
-                    c.send(("job", seq, results, shm_name, list(range(lo, hi)), params_list[lo:hi],
+                    c.send(("job", seq, "stats_sha1" if (results == "stats" and sha1) else results, shm_name,
+                            list(range(lo, hi)), params_list[lo:hi],
                             (off[lo:hi] if results == "audio" else np.zeros(hi - lo, np.int64)).tolist(),
                             out_n[lo:hi].tolist()))
                     live.append((w, lo, hi))
@@ -378,6 +418,8 @@ class DevicePool:
                 raise
             self.last_split = split
             if errors:
+                if results == "device":     # drop what every worker kept for this job (a leak)
+                    self._drop_job(seq, [w for w, _, _ in live])
                 raise RuntimeError("; ".join(errors))
             if results == "audio":
                 return _copy_out(shm, frames, off, out_n)
@@ -422,6 +464,24 @@ class DevicePool:
             if h.pool_id != self._id:
                 raise ValueError("handle belongs to another pool")
             by_w.setdefault(h.worker, []).append(h.key)
+        self._release_keys(by_w)
+
+    def _drop_job(self, job_seq, workers):
+        """Device mode, failed job: each worker frees every render it kept for it
+        (the successful workers' and a failed worker's partial ones)."""
+        for w in workers:
+            seq = self._next_seq()
+            try:
+                self._conns[w].send(("drop", seq, job_seq))
+                tag, s = self._conns[w].recv()
+            except BaseException:
+                self._fail()
+                raise
+            if tag != "released" or s != seq:
+                self._fail()
+                raise RuntimeError("drop reply out of step, pool closed")
+
+    def _release_keys(self, by_w):
         for w, keys in by_w.items():
             seq = self._next_seq()
             try:

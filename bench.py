@@ -442,6 +442,9 @@ class GpuRunner:
         w.outs = None
         self.torch.cuda.empty_cache()
 
+    def free_cache(self):
+        self.torch.cuda.empty_cache()
+
 
 class DryRunner:
     """Stand-in for GpuRunner in the CPU launcher tests: a step sleeps
@@ -551,6 +554,125 @@ def fir_rfft(sbytes, st_ms, where):
             "stage_ms": {k: st_ms.get(k) for k in FIR_RFFT_STAGES}, "note": where}
 
 
+# ---------------------------------------------------------------------------
+# standalone FIR points (SURVEY section 8 config remarks, 8(d)): the 16 k / 64 k-tap
+# filters BASELINE configs[2] / [3] request, which render() caps at 8192 taps (MS:443)
+FIR_SIGNALS, FIR_N = 1024, 384000     # C3's batch and output length
+
+
+def fir_taps(M, seed=7):
+    """SURVEY section 8(d)'s synthetic IR: default_rng(7).standard_normal(M) exp(-6t/M), peak 0.9."""
+    h = np.random.default_rng(seed).standard_normal(M) * np.exp(-6.0 * np.arange(M) / M)
+    return h * (0.9 / float(np.max(np.abs(h))))
+
+
+def fir_signals(seeds, n):
+    """x_b = default_rng(b).standard_normal(n) as float32, drawn on host threads."""
+    from concurrent.futures import ThreadPoolExecutor
+    x = np.empty((len(seeds), n), np.float32)
+
+    def fill(i):
+        x[i] = np.random.default_rng(seeds[i]).standard_normal(n, dtype=np.float32)
+    with ThreadPoolExecutor(max_workers=CORES_PER_GPU) as ex:
+        list(ex.map(fill, range(len(seeds))))
+    return x
+
+
+def np_fir_window(x, h, lo, hi):
+    """y[lo:hi] of np.convolve(x, h)[:n] (MS:444's arithmetic, float64), from the
+    inputs that reach it only: x[max(0, lo - M + 1):hi]."""
+    M = len(h)
+    a = max(0, lo - M + 1)
+    y = np.convolve(np.asarray(x[a:hi], np.float64), h)
+    return y[lo - a:hi - a]
+
+
+class FirRunner:
+    """One msg_fir call over the batch of signals = one step (same timing protocol)."""
+
+    def __init__(self, eng, x, y, h, stream):
+        self.eng, self.x, self.y, self.h, self.stream = eng, x, y, h, stream
+        self.shape = None
+        self.torch = eng.torch
+
+    def step(self, w=None, **kw):
+        _, self.shape = self.eng.fir(self.x, self.h, out=self.y, stream=self.stream)
+
+    def sync(self):
+        self.torch.cuda.synchronize(self.eng.device)
+
+
+def measure_fir(runner, M, steps, comm, rank, cpu=False):
+    """The standalone FIR point: FIR_SIGNALS signals of FIR_N samples through
+    msg_fir with an M-tap filter.  value = output samples / s over all ranks;
+    roofline = algorithmic bytes S (8 n + 4 M) over the device time per call
+    (HIP events on the call's stream); check = |y - np.convolve(x, h)[:n]| RMS
+    relative to the output RMS <= 1e-5 on the first and last signal, over a head
+    and a tail window (edges of the first and last blocks)."""
+    import torch
+    seeds = [rank * FIR_SIGNALS + b for b in range(FIR_SIGNALS)]
+    xh = fir_signals(seeds, FIR_N)
+    h = fir_taps(M)
+    eng = runner.engs[0]
+    stream = runner.streams[0]
+    x = torch.from_numpy(xh).to(f"cuda:{runner.dev}")
+    y = torch.empty_like(x)
+    fr = FirRunner(eng, x, y, h, stream)
+    for _ in range(3):
+        fr.step()
+    fr.sync()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    comm.barrier()
+    t0 = time.perf_counter()
+    e0.record(stream)
+    for _ in range(steps):
+        fr.step()
+    e1.record(stream)
+    fr.sync()
+    comm.barrier()
+    mine = time.perf_counter() - t0
+    elapsed = comm.max(mine)
+    dev_ms = e0.elapsed_time(e1) / steps
+    N, P, Q = fr.shape
+    engine = {(65536, 1): "k_fir8p", (65536, 2): "k_fir8p (two partitions)"}.get(
+        (N, Q), "k_fdl" if P == N // 2 and Q >= 8 else ("k_fir4" if N == 32768 else "k_fir2"))
+    S, n = FIR_SIGNALS, FIR_N
+    alg = S * (8.0 * n + 4.0 * M)
+    rec = {"value": round(S * n * comm.world * steps / elapsed / 1e6, 3), "unit": "Msamples/s",
+           "ms_per_step": round(elapsed / steps * 1e3, 4), "steps": steps,
+           "workload": f"standalone FIR: {S} signals x {n} samples, {M}-tap synthetic IR (SURVEY 8(d)), "
+                       "y = np.convolve(x, h)[:n] (MS:444 without the MS:443 cap)",
+           "fir_shape": {"N": fr.shape[0], "P": fr.shape[1], "Q": fr.shape[2]},
+           "roofline": {"bound": "hbm", "kernel": f"msg_fir: filter spectra + {engine}", "achieved": round(alg / (dev_ms * 1e-3) / 1e9, 1),
+                        "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(alg / (dev_ms * 1e-3) / 8e12, 4),
+                        "algorithmic_bytes": alg, "kernel_ms": round(dev_ms, 4),
+                        "note": "device time per call (HIP events on its stream), filter spectra included"},
+           "_rank_s": mine}
+    if rank == 0:
+        yh = y.cpu().numpy()
+        res, ok = {}, True
+        for b in (0, S - 1):
+            for lo, hi in ((0, 40000), (n - 20000, n)):
+                r = np_fir_window(xh[b], h, lo, hi)
+                e = float(np.sqrt(np.mean((yh[b, lo:hi] - r) ** 2)) / max(np.sqrt(np.mean(r ** 2)), 1e-30))
+                res[f"{b}:{lo}-{hi}"] = float(f"{e:.3g}")
+                ok &= e <= 1e-5
+        rec["check"] = {"windows": res, "all_ok": bool(ok),
+                        "tolerance": "RMS(y - np.convolve(x, h)[:n]) / RMS <= 1e-5 (float64 reference) on the "
+                                     "first and last signal, head and tail windows"}
+        if cpu:
+            t0 = time.perf_counter()
+            np_fir_window(xh[0], h, 0, 40000)
+            dt = time.perf_counter() - t0
+            rec["cpu_baseline"] = {"value": round(40000 / dt / 1e6, 4), "unit": "Msamples/s", "cores": 1,
+                                   "kind": "reference",
+                                   "sample": "np.convolve (the reference's own call, MS:444) of a 40000-sample "
+                                             "window on one host core"}
+    del x, y
+    runner.free_cache()
+    return rec
+
+
 def pack_ms(w, reps=5):
     """Host time to pack the workload's param dicts (all sub-batches), best of reps."""
     from msgpu.pack import PackedBatch
@@ -629,6 +751,8 @@ def parse():
     ap.add_argument("--points", default="H48,C4,C5",
                     help="secondary configs timed after the headline (comma list, '' = none)")
     ap.add_argument("--point-steps", type=int, default=10)
+    ap.add_argument("--fir-points", default="16384,65536",
+                    help="standalone FIR tap counts timed after the points (comma list, '' = none)")
     ap.add_argument("--dry-run", type=float, default=0.0, metavar="MS",
                     help="CPU launcher test: a step sleeps MS*(rank+1) ms instead of rendering")
     ap.add_argument("--rehearse-one-gpu", action="store_true",
@@ -733,6 +857,9 @@ def main():
             points[pc] = measure(runner, pc, rank_seeds(rank, pb), default_sub(pc, args, pb), psteps, 3, comm,
                                  irs, golden, iso_steps=args.iso_steps,
                                  from_dicts_steps=psteps if (pc == "H48" and args.from_dicts_steps) else 0)
+        for M in [int(t) for t in args.fir_points.split(",") if t]:
+            points[f"FIR{M // 1024}K"] = measure_fir(runner, M, max(args.point_steps, 20), comm, rank,
+                                                     cpu=(rank == 0 and not args.no_cpu))
         lat = dropin_latency(cpu) if (rank == 0 and world == 1 and not args.no_cpu) else None
         ranks = comm.gather({"rank": rank, "pid": os.getpid(), "device": device,
                              "cpus": [cpus[0], cpus[-1], len(cpus)], "host_threads": host_threads(),
@@ -768,9 +895,25 @@ def main():
             }
             if args.rehearse_one_gpu:
                 line["rehearsal"] = "all ranks shared device 0: checks the multi-rank path, not a scaling point"
+            # last, so that a reader keeping only the line's tail sees every point and its check
+            line["points_summary"] = points_summary(head, points)
             print(json.dumps(line), file=out, flush=True)
     finally:
         comm.close()
+
+
+def points_summary(head, points):
+    """{config: [ms_per_step, value, check.all_ok, roofline frac]} for the headline
+    and every point: the FIR + rFFT stage's isolated frac for render configs, the
+    standalone FIR's frac for the FIR points."""
+    def row(r):
+        rf = r.get("roofline") or {}
+        frac = ((rf.get("fir_rfft_stage") or {}).get("isolated") or {}).get("frac", rf.get("frac"))
+        return [r.get("ms_per_step"), round(float(r.get("value", 0.0)), 1), bool((r.get("check") or {}).get("all_ok")),
+                frac]
+    out = {"fields": "ms_per_step, Msamples/s, check.all_ok, frac (FIR+rFFT isolated | FIR)", "head": row(head)}
+    out.update({k: row(v) for k, v in points.items()})
+    return out
 
 
 def dry_main(args, comm, cfg, seeds, local, cpus, out):

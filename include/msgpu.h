@@ -12,6 +12,7 @@
  *   msg_preset       one params dict (MS:1166-1266) flattened to POD
  *   msg_render_batch render(params) for N presets at once      (replaces MS:588)
  *   msg_plan_host    the render's scalar/RNG plan, host-side    (MS:589-646, 742-751)
+ *   msg_digest       per-render checksums on the device         (MS:1585-1589)
  *   msg_rng_*        NumPy PCG64 stream primitives, host-side   (np.random.default_rng)
  */
 #ifndef MSGPU_H
@@ -112,7 +113,7 @@ int         msg_abi_version(void);
 /* Threads of the process-wide host planning pool (the caller included):
  * MSGPU_HOST_THREADS, else the CPU affinity / LOCAL_WORLD_SIZE, at most 16. */
 int         msg_host_threads(void);
-/* sizeof of the ABI structs (0 msg_preset, 1 msg_event, 2 msg_plan_info) for binding checks */
+/* sizeof of the ABI structs (0 msg_preset, 1 msg_event, 2 msg_plan_info, 3 msg_digest_rec) for binding checks */
 int64_t     msg_sizeof(int32_t which);
 msg_ctx*    msg_create(int device_ordinal);
 void        msg_destroy(msg_ctx* ctx);
@@ -214,6 +215,29 @@ int msg_fir(msg_ctx* ctx, const float* x_dev, float* y_dev, int64_t n, int32_t n
  * Windows up to 16384 samples (the float64 LDS engine). */
 int msg_stft_mag_db(msg_ctx* ctx, const void* x_dev, int32_t elem_bytes, int64_t n, int32_t channels, int32_t win,
                     int32_t hop, int32_t max_frames, double* S_dev, int32_t* frames, void* stream);
+
+/* Per-render summary and digest, reduced where the renders lie in HBM (SURVEY
+ * §5: a multi-GPU batch returns checksums; the reference's batch path writes
+ * one render at a time, main_v2.py:1585-1589).  For a render of out_n
+ * interleaved L/R float32 frames, words j = 0 .. 2 out_n - 1 with bit patterns
+ * w_j and k_j = j << 32 | w_j:
+ *   sum_sq, sum_l, sum_r  float64 sums (x^2 over both channels, L, R), folded
+ *                         in the fixed tile / wave order of kernels_digest.h;
+ *   peak                  max |x|;
+ *   h0, h1                sum_j fmix64(k_j ^ S) mod 2^64 for S = 0x9E3779B97F4A7C15
+ *                         and 0xD1B54A32D192ED03 (fmix64: MurmurHash3's finaliser).
+ * The same render gives the same record on any device and on the host. */
+typedef struct msg_digest_rec {
+    double sum_sq, peak, sum_l, sum_r;
+    uint64_t h0, h1;
+} msg_digest_rec;
+/* n_renders renders of out_dev (device), render i at frame out_offsets[i] with
+ * out_n[i] frames (host arrays); rec_dev: n_renders device records.  Enqueued
+ * on stream; one call in flight per context. */
+int msg_digest(msg_ctx* ctx, const float* out_dev, const int64_t* out_offsets, const int64_t* out_n,
+               int32_t n_renders, msg_digest_rec* rec_dev, void* stream);
+/* The same record of one render in host memory (x: out_n interleaved frames). */
+int msg_digest_host(const float* x, int64_t out_n, msg_digest_rec* rec);
 
 /* ---- NumPy stream primitives on the host (tests pin them against NumPy) ---- */
 /* Raw PCG64 outputs of np.random.default_rng(seed).bit_generator.random_raw(n). */

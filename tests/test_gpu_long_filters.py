@@ -301,6 +301,30 @@ def test_fir64_serves_every_flagged_preset(msgpu, irs):
     assert e <= FIR_TOL and not np.array_equal(one[:n], f32[:n])   # the float64 route did run
 
 
+def test_fir64_windows_bit_identical(msgpu, irs):
+    """with the default cap (1024 slots, 1 GiB) the batch above fits
+    one window, so the w0 > 0 path never ran.  MSGPU_FIR64_CAP=48 cuts 140
+    flagged copies into three windows (48 + 48 + 44 slots: slot_preset[w0 + sl],
+    h / H_q buffers reused between windows, fir64_window clamping the last one),
+    and a mixed batch interleaves unflagged presets between the flagged ones;
+    every copy matches the preset rendered alone, bit for bit."""
+    p = msgpu.merged(gen_mode="Resonant strike", event_process="Poisson", _ir_audio=irs["tiny_room_ir"],
+                     base_sr=48000, out_dur_s=0.3, space_ir_on=True, seed=22, er_cloud_on=True,
+                     space_ir_max_samps=8192, stereo_width=0.3)
+    q = msgpu.config_params("C3", seed=1001, irs=irs, out_dur_s=0.05)      # float32 FIR, not flagged
+    packed1, one = _render_env([p], {})
+    packedq, oneq = _render_env([q], {})
+    batch = [p] * 100 + [q, p, q] + [p] * 39
+    packedN, many = _render_env(batch, {"MSGPU_FIR64_CAP": "48"})
+    n, nq = int(packed1.out_n[0]), int(packedq.out_n[0])
+    for i, pp in enumerate(batch):
+        off = int(packedN.offsets[i])
+        if pp is p:
+            assert np.array_equal(many[off:off + n], one[:n]), i
+        else:
+            assert np.array_equal(many[off:off + nq], oneq[:nq]), i
+
+
 def test_stereo_fused_matches_two_launches(msgpu, irs):
     """k_stereo_fused (MSGPU_STEREO_FUSED=1: max and output passes in one
     persistent launch, deferred float64-FIR and odd-length presets) writes the
@@ -365,9 +389,10 @@ def test_ola_fused_matches_ola_kernel(msgpu, irs):
 
 
 def test_filter_spectra_early_same_bits(msgpu, irs):
-    """The filter spectra launched before the generator (MSGPU_H_EARLY=1, the
-    default) or at the FIR stage: the same kernels on the same inputs, so the
-    same bits, for the k_fir8 / k_fir4 one-partition and the partitioned paths."""
+    """The filter spectra launched before the generator (MSGPU_H_EARLY=1; the
+    default, 2, does so only for batches with an output of at least 2^22 frames)
+    or at the FIR stage (=0): the same kernels on the same inputs, so the same
+    bits, for the k_fir8 / k_fir4 one-partition and the partitioned paths."""
     params = [msgpu.config_params("C3", seed=1400, irs=irs, out_dur_s=0.4),
               msgpu.config_params("H48", seed=1401, irs=irs, out_dur_s=0.5),
               msgpu.config_params("C2", seed=1402, irs=irs, out_dur_s=0.25)]

@@ -19,8 +19,13 @@ print("  iso", {k: i["stage_ms"][k] for k in ("generate", "spectral", "overlap_a
 print("  from_dicts", d.get("from_dicts") or d.get("points", {}).get("C3", {}).get("from_dicts"))
 for k, v in d["points"].items():
     iso = v.get("roofline_isolated") or {}
+    if k.startswith("FIR"):
+        print(k, "step", v["ms_per_step"], "value", v["value"], "shape", v["fir_shape"], "roof", v["roofline"]["frac"],
+              v["roofline"]["kernel_ms"], "check", v["check"])
+        continue
     print(k, "step", v["ms_per_step"], "value", v["value"], "check", (v["check"] or {}).get("all_ok"),
           "iso", {a: b for a, b in (iso.get("stage_ms") or {}).items() if a in ("generate", "spectral", "overlap_add", "fir_kernel", "stereo", "total")},
           "fd", v.get("from_dicts"))
 print("cpu", d["cpu_baseline"])
+print("summary", json.dumps(d.get("points_summary")))
 PY
