@@ -545,6 +545,211 @@ k_fir8p(const PresetRt* __restrict__ rt, const int2* __restrict__ jobs, int n_jo
 }
 
 // ---------------------------------------------------------------------------
+// k_fir8q: two partitions on the 65 536-point engine (the standalone FIR of
+// SURVEY §8 at 64 k taps; round 5 ran it on k_fir4 with
+// five partitions of 13 108 taps at N = 32 768).  Uniformly partitioned
+// overlap-save: P = B = N / 2 = 32 768, H_q = FFT_N(h[q P, (q + 1) P)), q < 2,
+// and block j (outputs [j P, (j + 1) P)) is the last half of
+//     IFFT(X_j H_0 + X_{j-1} H_1),   X_j = FFT_N(x[(j - 1) P, (j + 1) P)),
+// one forward and one inverse transform per block, as k_fir8p's one-partition
+// blocks but with B = P instead of N - P + 1 (2 transforms per 32 768 outputs
+// instead of 6 of 32 768 points per 19 661 on k_fir4).  A workgroup takes a run
+// of consecutive blocks of one signal (one atomic per run) and keeps X_{j-1}
+// for the next block in a per-workgroup scratch slot (the even and odd halves'
+// last-pass registers v, 2 x 2 R4 float2 per thread, 256 KB per workgroup):
+// each thread reads back only what it wrote, element by element just before
+// overwriting it with X_j, so no extra registers stay live.  A run that starts
+// past a signal's first block opens with one forward transform of X_{j0-1}.
+// The MAC splits the two partitions' bins with the same per-pair arithmetic
+// as k_fir8 (fir_pair_mac, thread 0's slot permutation) and accumulates
+// X_j H_0 then X_{j-1} H_1 before the inverse pre-step.
+// ---------------------------------------------------------------------------
+namespace fir8 {
+constexpr int Q2_SLOT = 2 * 2 * R4 * T;          // float2 per workgroup: halves x (2 R4) x threads
+
+MSG_DEV float2* q2_slot(float2* scratch, int half, int h, int r) {
+    return scratch + ((half * 2 + h) * R4 + r) * T + otid();
+}
+
+// acc += X[2 kappa] . He over this thread's pairs (k_fir8's even_mac_pre without
+// the pre-step; thread 0's slots stay permuted: even_pre_q2 undoes it)
+MSG_DEV void even_mac_acc(const float2* tab, const float2 (&v)[2][R4], const float2* __restrict__ He,
+                          float2 (&acc)[2][R4]) {
+    const int t = otid();
+    if (t != 0) {
+        const float2 wA = fir4_wM(tab, G::OFF_PLO, G::OFF_PHI, t);
+#pragma unroll
+        for (int r = 0; r < R4; ++r) {
+            const int kA = t + r * NB4;
+            const float2 wk = cmul_k(wA, fir_cr<R4>(r));
+            fir_pair_mac(v[0][r], v[1][R4 - 1 - r], wk, at32(He, kA), at32(He, MH - kA), acc[0][r],
+                         acc[1][R4 - 1 - r]);
+        }
+    } else {
+        float2 a[R4], bb[R4];
+        fir_slots<R4>(v, a, bb, true);
+#pragma unroll
+        for (int r = 0; r < R4; ++r) {
+            const int kA = fir_k0<MH, R4>(r);
+            if (r < R4 - 1) {
+                fir_pair_mac(a[r], bb[R4 - 1 - r], fir_w0<MH, R4>(r), He[kA], He[MH - kA], acc[0][r],
+                             acc[1][R4 - 1 - r]);
+            } else {   // DC/Nyquist packed as (Y[0], Y[M]) and bin M/2
+                const float2 z0 = a[r];
+                acc[0][r].x = fmaf(z0.x + z0.y, He[0].x, acc[0][r].x);
+                acc[0][r].y = fmaf(z0.x - z0.y, He[MH].x, acc[0][r].y);
+                acc[1][0] = cfma(acc[1][0], cconj(bb[0]), He[MH / 2]);
+            }
+        }
+    }
+}
+MSG_DEV void even_pre_q2(const float2* tab, float2 (&acc)[2][R4]) {
+    const int t = otid();
+    if (t != 0) {
+        const float2 wA = fir4_wM(tab, G::OFF_PLO, G::OFF_PHI, t);
+#pragma unroll
+        for (int r = 0; r < R4; ++r) fir_pair_pre(acc[0][r], acc[1][R4 - 1 - r], cmul_k(wA, fir_cr<R4>(r)));
+    } else {
+#pragma unroll
+        for (int r = 0; r < R4 - 1; ++r) fir_pair_pre(acc[0][r], acc[1][R4 - 1 - r], fir_w0<MH, R4>(r));
+        const float y0 = acc[0][R4 - 1].x, yN = acc[0][R4 - 1].y;
+        acc[0][R4 - 1] = make_float2(0.5f * (y0 + yN), -0.5f * (y0 - yN));   // bin M/2: conj Z' = Y
+        fir_unslots<R4>(acc, true);
+    }
+}
+// acc += X[2 kappa + 1] . Ho (pairs kappa, MH-1-kappa), then (pre) the inverse pre-step
+MSG_DEV void odd_mac_acc(const float2* tab, const float2 (&v)[2][R4], const float2* __restrict__ Ho,
+                         float2 (&acc)[2][R4]) {
+    const int t = otid();
+    const float2 wA = cmul_k(fir4_wM(tab, G::OFF_PLO, G::OFF_PHI, t), wN1());   // W_N^(2t+1)
+#pragma unroll
+    for (int r = 0; r < R4; ++r) {
+        const int kA = t + r * NB4;
+        const float2 wk = cmul_k(wA, fir_cr<R4>(r));
+        float2 xk, xm;
+        fir_split(v[0][r], v[1][R4 - 1 - r], wk, xk, xm);
+        acc[0][r] = cfma(acc[0][r], xk, at32(Ho, kA));
+        acc[1][R4 - 1 - r] = cfma(acc[1][R4 - 1 - r], xm, at32(Ho, MH - 1 - kA));
+    }
+}
+MSG_DEV void odd_pre_q2(const float2* tab, float2 (&acc)[2][R4]) {
+    const int t = otid();
+    const float2 wA = cmul_k(fir4_wM(tab, G::OFF_PLO, G::OFF_PHI, t), wN1());
+#pragma unroll
+    for (int r = 0; r < R4; ++r) fir_pair_pre(acc[0][r], acc[1][R4 - 1 - r], cmul_k(wA, fir_cr<R4>(r)));
+}
+
+// one half of a block: acc = X_j H0 (+ X_{j-1} H1 from the slot), X_j into the slot
+template <bool ODD>
+MSG_DEV void q2_half_mac(const float2* tab, float2 (&v)[2][R4], const float2* __restrict__ H0,
+                         const float2* __restrict__ H1, float2* scratch, bool prev, float2 (&acc)[2][R4]) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int r = 0; r < R4; ++r) acc[h][r] = make_float2(0.f, 0.f);
+    if (ODD) odd_mac_acc(tab, v, H0, acc);
+    else even_mac_acc(tab, v, H0, acc);
+    // swap v with the slot, one element at a time (read X_{j-1}, write X_j)
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int r = 0; r < R4; ++r) {
+            float2* sl = q2_slot(scratch, ODD ? 1 : 0, h, r);
+            const float2 cur = v[h][r];
+            v[h][r] = prev ? *sl : make_float2(0.f, 0.f);
+            *sl = cur;
+        }
+    if (prev) {
+        if (ODD) odd_mac_acc(tab, v, H1, acc);
+        else even_mac_acc(tab, v, H1, acc);
+    }
+    if (ODD) odd_pre_q2(tab, acc);
+    else even_pre_q2(tab, acc);
+}
+}  // namespace fir8
+
+// jobs: runs (signal, first block); every run has run_len blocks but the
+// signal's last, which stops at its end (rt[signal].fir_Q holds the signal's
+// block count).  ctr: the launch's run counter at ctr[0] and the done count at
+// ctr[MSG_XCDS * FIR8P_CTR] (k_fir8p's counter block; zero before, left zero).
+__global__ void __launch_bounds__(fir8::T)
+k_fir8q(const PresetRt* __restrict__ rt, const int2* __restrict__ runs, int n_runs, int run_len,
+        const float2* __restrict__ tables, const float2* __restrict__ hspec, const float* __restrict__ x_in,
+        float* __restrict__ y_out, float2* __restrict__ scratch_all, int32_t* __restrict__ ctr) {
+    using namespace fir8;
+    extern __shared__ __attribute__((aligned(16))) float2 lds[];
+    __shared__ int s_take;
+    float2* tab = lds;
+    float2* buf = lds + G::TAB;
+    float2* scratch = scratch_all + (int64_t)blockIdx.x * Q2_SLOT;
+    const int t = otid();
+    { TabCopy<G::TAB_USED, T> tc; tc.fetch(tables); tc.put(tab); }
+    constexpr int P = MH * 2;                      // partition length = block length = N / 2
+    const float2* He0 = hspec;
+    const float2* Ho0 = He0 + (MH + 1);
+    const float2* He1 = hspec + (2 * MH + 1);
+    const float2* Ho1 = He1 + (MH + 1);
+    for (;;) {
+        __syncthreads();                          // tables visible; the last run's s_take read
+        if (t == 0) s_take = atomicAdd(ctr, 1);
+        __syncthreads();
+        const int run = s_take;
+        if (run >= n_runs) break;
+        const int2 job = runs[run];
+        const PresetRt& pr = rt[job.x];
+        const int64_t n = pr.out_n;
+        const int nb = pr.fir_Q;
+        const int j0 = job.y, j1 = j0 + run_len < nb ? j0 + run_len : nb;
+        const float* x = x_in + pr.y_off;
+        float2 a[R1], b[R1];
+        float2 v[2][R4];
+        if (j0 > 0) {                             // X_{j0-1} into the slot
+            load_halves(x, n, (int64_t)(j0 - 2) * P, a, b);
+            dif_split(tab, a, b);
+            fwd_half<false>(buf, tab, a, v);
+#pragma unroll
+            for (int h = 0; h < 2; ++h)
+#pragma unroll
+                for (int r = 0; r < R4; ++r) *q2_slot(scratch, 0, h, r) = v[h][r];
+            fwd_half<true>(buf, tab, b, v);
+#pragma unroll
+            for (int h = 0; h < 2; ++h)
+#pragma unroll
+                for (int r = 0; r < R4; ++r) *q2_slot(scratch, 1, h, r) = v[h][r];
+        }
+        for (int j = j0; j < j1; ++j) {
+            const int64_t t0 = (int64_t)j * P;
+            load_halves(x, n, t0 - P, a, b);
+            dif_split(tab, a, b);
+            float2 acc[2][R4], A[R1];
+            fwd_half<false>(buf, tab, a, v);
+            q2_half_mac<false>(tab, v, He0, He1, scratch, j > 0, acc);
+            inv_half<false>(buf, tab, acc, A);
+            fwd_half<true>(buf, tab, b, v);
+            q2_half_mac<true>(tab, v, Ho0, Ho1, scratch, j > 0, acc);
+            float2 (&B)[R1] = a;                  // a is dead: its registers take B
+            inv_half<true>(buf, tab, acc, B);
+            const float2 wt = fir4_wM(tab, G::OFF_PLO, G::OFF_PHI, t);
+            const SegOut so = seg_out(y_out, pr.y_off, t0, n, P, P + 1);
+            const int d0 = 2 * t - P;
+            const float s = 1.0f / (float)M;
+#pragma unroll
+            for (int r = 0; r < R1; ++r) {
+                const float2 wb = r == 0 ? cmul(B[r], wt) : cmul(B[r], cmul_k(wt, w32<R1>(r)));
+                const float2 f[2] = {ff(vv(A[r]) + vv(wb)), ff(vv(A[r]) - vv(wb))};
+#pragma unroll
+                for (int hh = 0; hh < 2; ++hh)
+                    so.put((uint32_t)(d0 + 2 * (r * NB1 + hh * MH)), make_float2(f[hh].x * s, -f[hh].y * s));
+            }
+        }
+    }
+    if (t == 0 && atomicAdd(ctr + MSG_XCDS * FIR8P_CTR, 1) == (int)gridDim.x - 1) {
+        ctr[0] = 0;
+        ctr[MSG_XCDS * FIR8P_CTR] = 0;
+    }
+}
+
+// ---------------------------------------------------------------------------
 // Filter spectra in the even/odd layout, one workgroup per (filter, half): the
 // even half needs a = z0 + z1 and the odd half b = (z0 - z1) W only, so each
 // half is its own workgroup (twice the workgroups of a per-filter kernel, each

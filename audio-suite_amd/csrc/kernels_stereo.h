@@ -36,8 +36,6 @@ static_assert(ST_TILE >= 4 * ST_T && ST_TILE % (4 * ST_T) == 0,
               "MSG_ST_TILE must be a multiple of 4 * ST_T (every frame of a tile has a run)");
 static_assert((2 * ST_TILE + 48) * 4 <= 160 * 1024, "MSG_ST_TILE: stereo tile window exceeds the 160 KiB LDS of a CU");
 constexpr int ST_WIN = ST_TILE + 48;
-constexpr int ST_WPER = (ST_WIN + ST_T - 1) / ST_T;
-constexpr int ST_LPER = ST_TILE / ST_T;
 
 struct StereoTile {
     int t0, cnt;             // first frame, frames in this tile
@@ -60,43 +58,67 @@ MSG_DEV int st_tid() {
     return t;
 }
 
-// Stage len floats y[(b0 + u) mod n] into w[0 .. len): coalesced loads into
-// registers (stereo_load), then LDS stores (stereo_store), split so that a
-// kernel can have every global load of its tile in flight before the first
-// store waits on them.
-template <int PER>
-MSG_DEV void stereo_load(const float* __restrict__ y, int n, int b0, int len, float (&v)[PER]) {
+MSG_DEV int st_rfl(int v) { return __builtin_amdgcn_readfirstlane(v); }
+
+// Stage len floats y[(b0 + u) mod n] into w[0 .. len) with 16-byte loads
+// (round 5 staged them with dword loads, 256 B per wave
+// instruction): the aligned float4s covering y[b0, b0 + len)
+// are loaded (all of them in flight before the first LDS store), then stored
+// to LDS shifted back by the misalignment sh (uniform: the window's address
+// mod 16).  Reads past either end stay inside the aligned 16-byte blocks
+// holding the window's first and last samples (no other page).  A window that
+// wraps past n (at most one per preset and pass) takes dword loads in the same
+// register layout with sh = 0.
+constexpr int ST_PER4 = (ST_WIN + 3 + 3) / 4 / ST_T + 1;   // float4s per thread, any shift
+struct Win4 {
+    float4 q[ST_PER4];
+    int sh;
+};
+MSG_DEV void stereo_load4(const float* __restrict__ y, int n, int b0, int len, Win4& W) {
     const int tid = st_tid();
-    if (b0 + len <= n) {                       // no wrap (nearly every tile): one base, 32-bit offsets
-        const float* yb = y + b0;
+    if (b0 + len <= n) {
+        const float* a = y + b0;
+        W.sh = (int)((reinterpret_cast<uintptr_t>(a) >> 2) & 3);
+        const float4* a4 = reinterpret_cast<const float4*>(a - W.sh);
+        const int c4 = (len + W.sh + 3) >> 2;
 #pragma unroll
-        for (int i = 0; i < PER; ++i) {
-            const int u = tid + i * ST_T;
-            v[i] = u < len ? at32(yb, (uint32_t)u) : 0.f;
+        for (int i = 0; i < ST_PER4; ++i) {
+            const int j = tid + i * ST_T;
+            W.q[i] = j < c4 ? at32(a4, (uint32_t)j) : make_float4(0.f, 0.f, 0.f, 0.f);
         }
-    } else if (n >= len) {                     // one wrap at most
+        return;
+    }
+    W.sh = 0;
 #pragma unroll
-        for (int i = 0; i < PER; ++i) {
-            const int u = tid + i * ST_T;
+    for (int i = 0; i < ST_PER4; ++i) {
+        float v[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int u = 4 * (tid + i * ST_T) + k;
             int j = b0 + u;
-            if (j >= n) j -= n;
-            v[i] = u < len ? y[j] : 0.f;          // j up to n: 64-bit addressing (n may pass 2^30)
+            if (n >= len) { if (j >= n) j -= n; }
+            else j = (int)(((int64_t)b0 + u) % n);
+            v[k] = u < len ? y[j] : 0.f;                  // j up to n: 64-bit addressing (n may pass 2^30)
         }
-    } else {
-#pragma unroll
-        for (int i = 0; i < PER; ++i) {
-            const int u = tid + i * ST_T;
-            v[i] = u < len ? y[(b0 + u) % n] : 0.f;
-        }
+        W.q[i] = make_float4(v[0], v[1], v[2], v[3]);
     }
 }
-template <int PER>
-MSG_DEV void stereo_store(int len, const float (&v)[PER], float* w) {
+MSG_DEV void stereo_store4(int len, const Win4& W, float* w) {
     const int tid = st_tid();
+    const int sh = st_rfl(W.sh);
 #pragma unroll
-    for (int i = 0; i < PER; ++i) {
-        const int u = tid + i * ST_T;
-        if (u < len) w[u] = v[i];
+    for (int i = 0; i < ST_PER4; ++i) {
+        const int u0 = 4 * (tid + i * ST_T) - sh;
+        if (sh == 0 && u0 + 4 <= len) {
+            *reinterpret_cast<float4*>(w + u0) = W.q[i];
+            continue;
+        }
+        const float v[4] = {W.q[i].x, W.q[i].y, W.q[i].z, W.q[i].w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int u = u0 + k;
+            if (u >= 0 && u < len) w[u] = v[k];
+        }
     }
 }
 
@@ -178,7 +200,6 @@ MSG_DEV int job_order_st() { return xcd_block(blockIdx.x, gridDim.x); }
 
 constexpr int ST_EXIT = INT32_MIN;
 
-MSG_DEV int st_rfl(int v) { return __builtin_amdgcn_readfirstlane(v); }
 
 // Cross-workgroup hand-off without agent-scope fences.  Every value another
 // workgroup reads in this launch (tile peaks, partial sums, counters, the ready
@@ -214,9 +235,9 @@ MSG_DEV float stereo_max_vals(const PresetRt& r, int tile, const float* __restri
     const bool fir = r.stereo_fir == 1;
     float4 yv[ST_RUNS];
     if (fir) {
-        float wv[ST_WPER];
-        stereo_load<ST_WPER>(y, n, mod_n((int64_t)st.t0 + r.dr - 24, n), ST_WIN, wv);
-        stereo_store<ST_WPER>(ST_WIN, wv, w);
+        Win4 wv;
+        stereo_load4(y, n, mod_n((int64_t)st.t0 + r.dr - 24, n), ST_WIN, wv);
+        stereo_store4(ST_WIN, wv, w);
     } else {
 #pragma unroll
         for (int i = 0; i < ST_RUNS; ++i) {
@@ -386,21 +407,35 @@ k_stereo_remax(const PresetRt* __restrict__ rt, const int32_t* __restrict__ st_c
 }
 
 // The clipped, normalised (L, R) of one tile of preset p, peak M = the float
-// bits peak_bits (w: the R window, lw: the L window, LDS).  (L straight into
-// registers -- 16.6 KB of LDS per workgroup instead of 33 -- measured 1.64 vs
-// 1.60 ms isolated on C3: the pass is not limited by its workgroups per CU.)
+// bits peak_bits (sm: LDS of ST_SM floats -- the L window, then the R window;
+// after the arithmetic, the tile's (L, R) pairs).  (L straight into registers
+// -- 16.6 KB of LDS per workgroup instead of 33 -- measured 1.64 vs 1.60 ms
+// isolated on C3: the pass is not limited by its workgroups per CU.)
+// Round 6: the windows come in with 16-byte loads (stereo_load4), and the
+// output leaves through LDS so that every store instruction writes 1 KB of
+// consecutive frames (two frames per lane); a thread's own runs of four frames
+// would store 32 B per lane at a 32-byte stride, leaving every line
+// half-written by each instruction (the streaming probe: 4.8 TB/s for that
+// shape against 5.2 - 5.3 for contiguous stores, profiles/r06c_stream_rates.txt).
+constexpr int ST_SM = ST_TILE + ST_WIN;
+static_assert(ST_SM >= 2 * ST_TILE, "the (L, R) staging reuses both windows");
+#ifndef MSG_ST_NT
+#define MSG_ST_NT 0                 // nontemporal output stores (tuning builds)
+#endif
 MSG_DEV void stereo_out_tile(const PresetRt& r, int tile, const float* __restrict__ ybuf, const float* __restrict__ rbuf,
-                             unsigned peak_bits, float* __restrict__ out, float* w, float* lw) {
+                             unsigned peak_bits, float* __restrict__ out, float* sm) {
+    float* lw = sm;
+    float* w = sm + ST_TILE;
     const float* y = ybuf + r.y_off;
     const int n = (int)r.out_n;
     const StereoTile st = stereo_tile(r, (int64_t)tile * ST_TILE);
     const int tid = st_tid();
     {
-        float lv[ST_LPER], wv[ST_WPER];
-        stereo_load<ST_LPER>(y, n, r.stereo_fir ? st.lbase : st.t0, st.cnt, lv);
-        if (r.stereo_fir == 1) stereo_load<ST_WPER>(y, n, mod_n((int64_t)st.t0 + r.dr - 24, n), ST_WIN, wv);
-        stereo_store<ST_LPER>(st.cnt, lv, lw);
-        if (r.stereo_fir == 1) stereo_store<ST_WPER>(ST_WIN, wv, w);
+        Win4 lv, wv;
+        stereo_load4(y, n, r.stereo_fir ? st.lbase : st.t0, st.cnt, lv);
+        if (r.stereo_fir == 1) stereo_load4(y, n, mod_n((int64_t)st.t0 + r.dr - 24, n), ST_WIN, wv);
+        stereo_store4(st.cnt, lv, lw);
+        if (r.stereo_fir == 1) stereo_store4(ST_WIN, wv, w);
     }
     const float d = r.drive;
     const float inv_td = d > 0.f ? 1.0f / tanh_fast(d) : 1.f;
@@ -408,9 +443,8 @@ MSG_DEV void stereo_out_tile(const PresetRt& r, int tile, const float* __restric
     const float mc = sat(M, d, inv_td);
     const float scale = mc > 0.f ? r.peak / mc : 1.f;
     const float k_out = inv_td * scale;                     // one multiply per channel after the tanh
-    float2* o = reinterpret_cast<float2*>(out) + r.out_off + st.t0;
-    const bool o16 = ((r.out_off + st.t0) & 1) == 0;      // float4 stores of two frames
     __syncthreads();
+    float4 res[ST_RUNS][2];                                 // (L, R) of frames u .. u + 3 per run
 #pragma unroll
     for (int i = 0; i < ST_RUNS; ++i) {
         const int u = 4 * (tid + i * ST_T);
@@ -437,14 +471,45 @@ MSG_DEV void stereo_out_tile(const PresetRt& r, int tile, const float* __restric
 #pragma unroll
             for (int k = 0; k < 4; ++k) v[k] = make_float2(L[k] * scale, R[k] * scale);
         }
-        if (o16 && u + 4 <= st.cnt) {
-            float4* o4 = reinterpret_cast<float4*>(reinterpret_cast<char*>(o) + (uint32_t)u * 8u);   // 32-bit offset
-            o4[0] = make_float4(v[0].x, v[0].y, v[1].x, v[1].y);
-            o4[1] = make_float4(v[2].x, v[2].y, v[3].x, v[3].y);
+        res[i][0] = make_float4(v[0].x, v[0].y, v[1].x, v[1].y);
+        res[i][1] = make_float4(v[2].x, v[2].y, v[3].x, v[3].y);
+    }
+    __syncthreads();                                        // every window read done: sm takes the pairs
+#pragma unroll
+    for (int i = 0; i < ST_RUNS; ++i) {
+        const int u = 4 * (tid + i * ST_T);
+        if (u >= st.cnt) continue;
+        float4* o = reinterpret_cast<float4*>(sm + 2 * u);
+        o[0] = res[i][0];
+        o[1] = res[i][1];
+    }
+    __syncthreads();
+    // frame pairs aligned to the output: pair j holds local frames 2 j - a, 2 j - a + 1
+    const int a = (int)((r.out_off + st.t0) & 1);
+    float* ob = out + 2 * (r.out_off + st.t0 - a);          // 16-byte aligned
+    const int pairs = (st.cnt + a + 1) >> 1;
+#pragma unroll
+    for (int i = 0; i < (ST_TILE / 2 + 1 + ST_T - 1) / ST_T; ++i) {
+        const int j = tid + i * ST_T;
+        if (j >= pairs) break;
+        const int f0 = 2 * j - a;
+        if (f0 >= 0 && f0 + 1 < st.cnt) {
+            const float2 p0 = *reinterpret_cast<const float2*>(sm + 2 * f0);
+            const float2 p1 = *reinterpret_cast<const float2*>(sm + 2 * f0 + 2);
+            float* dst = ob + 4 * (uint32_t)j;
+#if MSG_ST_NT
+            typedef float v4f __attribute__((ext_vector_type(4)));
+            __builtin_nontemporal_store(v4f{p0.x, p0.y, p1.x, p1.y}, reinterpret_cast<v4f*>(dst));
+#else
+            *reinterpret_cast<float4*>(dst) = make_float4(p0.x, p0.y, p1.x, p1.y);
+#endif
         } else {
 #pragma unroll
-            for (int k = 0; k < 4; ++k)
-                if (u + k < st.cnt) at32(o, (uint32_t)(u + k)) = v[k];
+            for (int k = 0; k < 2; ++k) {
+                const int f = f0 + k;
+                if (f >= 0 && f < st.cnt)
+                    *reinterpret_cast<float2*>(ob + 4 * (uint32_t)j + 2 * k) = *reinterpret_cast<const float2*>(sm + 2 * f);
+            }
         }
     }
 }
@@ -453,11 +518,10 @@ __global__ void __launch_bounds__(ST_T)
 k_stereo_out(const PresetRt* __restrict__ rt, const int32_t* __restrict__ st_begin, int n_presets,
              const float* __restrict__ ybuf, const float* __restrict__ rbuf, const unsigned* __restrict__ maxbits,
              float* __restrict__ out) {
-    __shared__ __attribute__((aligned(16))) float w[ST_WIN];
-    __shared__ __attribute__((aligned(16))) float lw[ST_TILE];
+    __shared__ __attribute__((aligned(16))) float sm[ST_SM];
     const int b = job_order_st();
     const int p = find_preset(st_begin, n_presets, b);
-    stereo_out_tile(rt[p], b - st_begin[p], ybuf, rbuf, maxbits[p], out, w, lw);
+    stereo_out_tile(rt[p], b - st_begin[p], ybuf, rbuf, maxbits[p], out, sm);
 }
 
 // The output tiles of the listed presets (the deferred ones of k_stereo_fused:
@@ -467,15 +531,14 @@ k_stereo_out_list(const PresetRt* __restrict__ rt, const int32_t* __restrict__ s
                   const int32_t* __restrict__ list, const int32_t* __restrict__ n_list, int tmax,
                   const float* __restrict__ ybuf, const float* __restrict__ rbuf, const unsigned* __restrict__ maxbits,
                   float* __restrict__ out) {
-    __shared__ __attribute__((aligned(16))) float w[ST_WIN];
-    __shared__ __attribute__((aligned(16))) float lw[ST_TILE];
+    __shared__ __attribute__((aligned(16))) float sm[ST_SM];
     const int nl = *n_list;
     for (int64_t j = blockIdx.x; j < (int64_t)nl * tmax; j += gridDim.x) {
         const int sl = (int)(j / tmax), t = (int)(j - (int64_t)sl * tmax);
         const int p = st_rfl(list[sl]);
         if (t >= st_count[p]) continue;                          // uniform
         __syncthreads();                                         // the previous tile's LDS reads are done
-        stereo_out_tile(rt[p], t, ybuf, rbuf, maxbits[p], out, w, lw);
+        stereo_out_tile(rt[p], t, ybuf, rbuf, maxbits[p], out, sm);
     }
 }
 
@@ -513,8 +576,8 @@ __global__ void __launch_bounds__(ST_T) __attribute__((amdgpu_waves_per_eu(4)))
 k_stereo_fused(const PresetRt* __restrict__ rt, const int32_t* __restrict__ st_begin, int n_presets, int n_tiles,
                const float* __restrict__ ybuf, unsigned* __restrict__ maxbits, StereoSync sy,
                int32_t* __restrict__ ctr, float* __restrict__ out) {
-    __shared__ __attribute__((aligned(16))) float w[ST_WIN];
-    __shared__ __attribute__((aligned(16))) float lw[ST_TILE];
+    __shared__ __attribute__((aligned(16))) float sm[ST_SM];
+    float* w = sm + ST_TILE;                                    // the max pass's window
     __shared__ float wm[3 * (ST_T / 64)];
     __shared__ double s_red[2 * (ST_T / 64)];
     __shared__ int32_t s_begin[ST_LDS_PRESETS];
@@ -591,7 +654,7 @@ k_stereo_fused(const PresetRt* __restrict__ rt, const int32_t* __restrict__ st_b
                 if (!st_rfl(s_skip)) {
                     const unsigned peak = (unsigned)st_rfl((int)s_peak);
                     for (int u = t; u < te; ++u) {
-                        stereo_out_tile(r, u - tb, ybuf, nullptr, peak, out, w, lw);
+                        stereo_out_tile(r, u - tb, ybuf, nullptr, peak, out, sm);
                         __syncthreads();                            // LDS windows free for the next tile
                     }
                 }

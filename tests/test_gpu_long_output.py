@@ -3,9 +3,12 @@ NotImplementedError there).  The reference computes out_n = round(out_dur *
 base_sr) with no limit (MS:591); a hand-written params dict at 384 kHz passes
 2^29 frames after 23.3 minutes.  One preset of 2^29 + 2^18 frames (no ER / IR,
 Poisson events at 2 / s, so grains land on both sides of frame 2^29) is
-rendered on the device and its summary checked against the NumPy restatement's
-render of the same dict, computed in the container (tools/gen_golden_r5.py,
-tests/golden/long_2e29.json: the render itself is 8.6 GB)."""
+rendered on the device and its summary checked against the reference's own
+render of the same dict, computed in the container by importing
+microsound_0.2.1/main_v2.py (tools/gen_golden_r5.py, tests/golden/long_2e29.json:
+the render itself is 8.6 GB).  The NumPy restatement's
+summary of the same render is equal to it field for field (the fixture's
+``oracle_equal``)."""
 import json
 import os
 

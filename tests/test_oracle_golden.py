@@ -227,3 +227,16 @@ def test_progress_messages_pinned(irs, full_renders):
         O.render(_progress_params(case, irs, full_renders["image_gray"]),
                  progress=lambda v, m: msgs.append([int(v), str(m)]))
         assert msgs == case["messages"], name
+
+
+def test_long_fixture_is_the_references():
+    """the > 2^29-frame fixture is the reference's own render
+    (tools/gen_golden_r5.py imports main_v2.render), and the NumPy restatement's
+    summary of the same dict was equal to it in every field."""
+    import json
+    import os
+    with open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "long_2e29.json")) as f:
+        g = json.load(f)
+    assert g["source"].startswith("reference: microsound_0.2.1/main_v2.py")
+    assert g["out_n"] == (1 << 29) + (1 << 18)
+    assert g["oracle_equal"] and all(g["oracle_equal"].values())

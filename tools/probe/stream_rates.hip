@@ -128,6 +128,79 @@ __global__ void __launch_bounds__(T) k_copy2(const float4* __restrict__ y, int64
     }
 }
 
+// copy with contiguous stores: each lane loads two frames (8 B, 512 B per wave
+// instruction) and stores their (L, R) pairs as one float4 (1 KB per wave
+// instruction) -- k_copy's two float4 stores per lane each cover every other
+// 16 B of 2 KB, so every store instruction leaves half-written lines
+template <int T, int U, int NT, int C>
+__global__ void __launch_bounds__(T) k_copyb(const float2* __restrict__ y, int64_t n2, float4* __restrict__ out) {
+    Walk<T, U, C> w(n2);
+    for (int64_t i = w.base; i < w.end; i += U * w.step) {
+        float2 v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t j = i + u * w.step;
+            v[u] = j < w.end ? y[j] : make_float2(0.f, 0.f);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t j = i + u * w.step;
+            if (j < w.end) st<NT>(out + j, make_float4(v[u].x, v[u].x, v[u].y, v[u].y));
+        }
+    }
+}
+
+// k_copy's ownership (four frames per lane) with the two stores made
+// contiguous per instruction by a cross-lane exchange (ds_bpermute): store s
+// of lane l writes pair-chunk 64 s + l, frames 2 (64 s + l) .. + 1, which lane
+// (64 s + l) / 2 of the wave holds
+template <int T, int U, int NT, int C>
+__global__ void __launch_bounds__(T) k_copys(const float4* __restrict__ y, int64_t n4, float4* __restrict__ out) {
+    Walk<T, U, C> w(n4);
+    const int lane = (int)(threadIdx.x & 63);
+    for (int64_t i = w.base; i < w.end; i += U * w.step) {
+        float4 v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t j = i + u * w.step;
+            v[u] = j < w.end ? ld<NT>(y + j) : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t j0 = i + u * w.step - lane;          // the wave's first float4 of y
+#pragma unroll
+            for (int s = 0; s < 2; ++s) {
+                const int src = (64 * s + lane) >> 1;
+                const bool hi = lane & 1;                        // frames 2, 3 of the source lane's four
+                const float a1 = __shfl(v[u].x, src, 64), b1 = __shfl(v[u].y, src, 64);
+                const float a2 = __shfl(v[u].z, src, 64), b2 = __shfl(v[u].w, src, 64);
+                const float p = hi ? a2 : a1, q = hi ? b2 : b1;
+                const int64_t chunk = 2 * j0 + 64 * s + lane;
+                if (j0 + src < w.end) st<NT>(out + chunk, make_float4(p, p, q, q));
+            }
+        }
+    }
+}
+
+// 1:1 copy (the guide's float4 copy: 16 B read, 16 B written per lane)
+template <int T, int U, int NT, int C>
+__global__ void __launch_bounds__(T) k_copy1(const float4* __restrict__ y, int64_t n4, float4* __restrict__ out) {
+    Walk<T, U, C> w(n4);
+    for (int64_t i = w.base; i < w.end; i += U * w.step) {
+        float4 v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t j = i + u * w.step;
+            v[u] = j < w.end ? ld<NT>(y + j) : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t j = i + u * w.step;
+            if (j < w.end) st<NT>(out + j, v[u]);
+        }
+    }
+}
+
 #define CHK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e_)); return 1; } } while (0)
 
 struct Bufs { float4* y; float4* out; float* sink; int64_t frames, n4; int cus; hipEvent_t a, b; };
@@ -165,6 +238,23 @@ template <int T, int U, int NT, int C> static int variant(Bufs& B, int wpc) {
     return 0;
 }
 
+// the contiguous-store copies and the 1:1 copy
+template <int T, int U, int NT, int C> static int variant2(Bufs& B, int wpc) {
+    const unsigned grid = (unsigned)(B.cus * wpc);
+    char tag[64];
+    const double fr = (double)B.frames;
+    snprintf(tag, sizeof tag, "T=%d U=%d NT=%d W=%d C=%d", T, U, NT, wpc, C);
+    char nm[96];
+    snprintf(nm, sizeof nm, "copyb  %s", tag);
+    if (timeit(B, nm, 12.0 * fr, [&] { hipLaunchKernelGGL((k_copyb<T, U, NT, C>), dim3(grid), dim3(T), 0, nullptr,
+                                                         reinterpret_cast<const float2*>(B.y), 2 * B.n4, B.out); })) return 1;
+    snprintf(nm, sizeof nm, "copys  %s", tag);
+    if (timeit(B, nm, 12.0 * fr, [&] { hipLaunchKernelGGL((k_copys<T, U, NT, C>), dim3(grid), dim3(T), 0, nullptr, B.y, B.n4, B.out); })) return 1;
+    snprintf(nm, sizeof nm, "copy1  %s", tag);
+    if (timeit(B, nm, 8.0 * fr, [&] { hipLaunchKernelGGL((k_copy1<T, U, NT, C>), dim3(grid), dim3(T), 0, nullptr, B.y, B.n4, B.out); })) return 1;
+    return 0;
+}
+
 int main() {
     Bufs B;
     B.frames = 393216000;
@@ -177,6 +267,12 @@ int main() {
     CHK(hipEventCreate(&B.a));
     CHK(hipEventCreate(&B.b));
     int rc = 0;
+    rc |= variant2<256, 1, 0, 0>(B, 8);
+    rc |= variant2<256, 4, 0, 0>(B, 8);
+    rc |= variant2<256, 4, 1, 0>(B, 8);
+    rc |= variant2<256, 4, 0, 1>(B, 8);
+    rc |= variant2<1024, 4, 0, 0>(B, 2);
+    rc |= variant2<1024, 4, 1, 0>(B, 1);
     rc |= variant<256, 1, 0, 0>(B, 8);     // the round-5 probe
     rc |= variant<256, 4, 0, 0>(B, 8);
     rc |= variant<256, 4, 1, 0>(B, 8);
