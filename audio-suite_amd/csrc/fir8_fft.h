@@ -556,34 +556,58 @@ k_fir8p(const PresetRt* __restrict__ rt, const int2* __restrict__ jobs, int n_jo
 // instead of 6 of 32 768 points per 19 661 on k_fir4).  A workgroup takes a run
 // of consecutive blocks of one signal (one atomic per run) and keeps X_{j-1}
 // for the next block in a per-workgroup scratch slot (the even and odd halves'
-// last-pass registers v, 2 x 2 R4 float2 per thread, 256 KB per workgroup):
-// each thread reads back only what it wrote, element by element just before
-// overwriting it with X_j, so no extra registers stay live.  A run that starts
-// past a signal's first block opens with one forward transform of X_{j0-1}.
-// The MAC splits the two partitions' bins with the same per-pair arithmetic
-// as k_fir8 (fir_pair_mac, thread 0's slot permutation) and accumulates
-// X_j H_0 then X_{j-1} H_1 before the inverse pre-step.
+// last-pass registers v, 2 x 2 R4 float2 per thread, 256 KB per workgroup) --
+// as the carry C_{j+1} = X_j H_1 (the product formed while X_j's bins are
+// split for X_j H_0, so X_{j-1} is never split again): block j adds C_j to
+// X_j H_0 before the inverse pre-step.  Each thread reads back only what it
+// wrote, pair by pair just before overwriting it, so no extra registers stay
+// live.  A run that starts past a signal's first block opens with one forward
+// transform of X_{j0-1} for its carry; a run's last block emits none.
 // ---------------------------------------------------------------------------
 namespace fir8 {
 constexpr int Q2_SLOT = 2 * 2 * R4 * T;          // float2 per workgroup: halves x (2 R4) x threads
 
-MSG_DEV float2* q2_slot(float2* scratch, int half, int h, int r) {
-    return scratch + ((half * 2 + h) * R4 + r) * T + otid();
+// the slot of one half: 2 R4 carries per thread, element e of thread t at e T + t
+MSG_DEV float2* q2_slot(float2* scratch, int half) { return scratch + half * 2 * R4 * T; }
+
+// One pair (k, M - k) of a half: the split X of this block's bins, acc = X H0
+// (+ the carry C_j = X_{j-1} H1 that the previous block left in the slot), and
+// the new carry X H1 into the slot (load before store: each thread reads back
+// only what it wrote).  The empty asm with a memory clobber keeps the pairs'
+// slot accesses in order, so the carries do not pile up in registers.
+MSG_DEV void q2_pair(float2 xk, float2 xm, float2 h0k, float2 h0m, float2 h1k, float2 h1m, float2& ak, float2& am,
+                     float2& sk, float2& sm, bool prev, bool emit) {
+    asm volatile("" ::: "memory");
+    ak = cmul(xk, h0k);
+    am = cmul(xm, h0m);
+    if (prev) {
+        ak = ff(vv(ak) + vv(sk));
+        am = ff(vv(am) + vv(sm));
+    }
+    if (emit) {
+        sk = cmul(xk, h1k);
+        sm = cmul(xm, h1m);
+    }
 }
 
-// acc += X[2 kappa] . He over this thread's pairs (k_fir8's even_mac_pre without
-// the pre-step; thread 0's slots stay permuted: even_pre_q2 undoes it)
-MSG_DEV void even_mac_acc(const float2* tab, const float2 (&v)[2][R4], const float2* __restrict__ He,
-                          float2 (&acc)[2][R4]) {
+// Even half of a block on the carry form (k_fir8's even_mac_pre with H0, plus
+// the carry in / out); leaves acc as conj Z' pairs for inv_half.
+MSG_DEV void even_q2(const float2* tab, const float2 (&v)[2][R4], const float2* __restrict__ H0,
+                     const float2* __restrict__ H1, float2* sl, bool prev, bool emit, float2 (&acc)[2][R4]) {
     const int t = otid();
+    const uint32_t tu = (uint32_t)t;
     if (t != 0) {
         const float2 wA = fir4_wM(tab, G::OFF_PLO, G::OFF_PHI, t);
 #pragma unroll
         for (int r = 0; r < R4; ++r) {
             const int kA = t + r * NB4;
             const float2 wk = cmul_k(wA, fir_cr<R4>(r));
-            fir_pair_mac(v[0][r], v[1][R4 - 1 - r], wk, at32(He, kA), at32(He, MH - kA), acc[0][r],
-                         acc[1][R4 - 1 - r]);
+            float2 xk, xm;
+            fir_split(v[0][r], v[1][R4 - 1 - r], wk, xk, xm);
+            q2_pair(xk, xm, at32(H0, kA), at32(H0, MH - kA), at32(H1, kA), at32(H1, MH - kA), acc[0][r],
+                    acc[1][R4 - 1 - r], at32(sl, tu + (uint32_t)(r * T)), at32(sl, tu + (uint32_t)((R4 + r) * T)),
+                    prev, emit);
+            fir_pair_pre(acc[0][r], acc[1][R4 - 1 - r], wk);
         }
     } else {
         float2 a[R4], bb[R4];
@@ -592,35 +616,42 @@ MSG_DEV void even_mac_acc(const float2* tab, const float2 (&v)[2][R4], const flo
         for (int r = 0; r < R4; ++r) {
             const int kA = fir_k0<MH, R4>(r);
             if (r < R4 - 1) {
-                fir_pair_mac(a[r], bb[R4 - 1 - r], fir_w0<MH, R4>(r), He[kA], He[MH - kA], acc[0][r],
-                             acc[1][R4 - 1 - r]);
+                float2 xk, xm;
+                fir_split(a[r], bb[R4 - 1 - r], fir_w0<MH, R4>(r), xk, xm);
+                q2_pair(xk, xm, H0[kA], H0[MH - kA], H1[kA], H1[MH - kA], acc[0][r], acc[1][R4 - 1 - r],
+                        sl[r * T], sl[(R4 + r) * T], prev, emit);
             } else {   // DC/Nyquist packed as (Y[0], Y[M]) and bin M/2
                 const float2 z0 = a[r];
-                acc[0][r].x = fmaf(z0.x + z0.y, He[0].x, acc[0][r].x);
-                acc[0][r].y = fmaf(z0.x - z0.y, He[MH].x, acc[0][r].y);
-                acc[1][0] = cfma(acc[1][0], cconj(bb[0]), He[MH / 2]);
+                const float2 xd = make_float2(z0.x + z0.y, z0.x - z0.y), xh = cconj(bb[0]);
+                asm volatile("" ::: "memory");
+                acc[0][r] = make_float2(xd.x * H0[0].x, xd.y * H0[MH].x);
+                acc[1][0] = cmul(xh, H0[MH / 2]);
+                float2& s0 = sl[r * T];
+                float2& s1 = sl[(2 * R4 - 1) * T];
+                if (prev) {
+                    acc[0][r] = ff(vv(acc[0][r]) + vv(s0));
+                    acc[1][0] = ff(vv(acc[1][0]) + vv(s1));
+                }
+                if (emit) {
+                    s0 = make_float2(xd.x * H1[0].x, xd.y * H1[MH].x);
+                    s1 = cmul(xh, H1[MH / 2]);
+                }
             }
         }
-    }
-}
-MSG_DEV void even_pre_q2(const float2* tab, float2 (&acc)[2][R4]) {
-    const int t = otid();
-    if (t != 0) {
-        const float2 wA = fir4_wM(tab, G::OFF_PLO, G::OFF_PHI, t);
-#pragma unroll
-        for (int r = 0; r < R4; ++r) fir_pair_pre(acc[0][r], acc[1][R4 - 1 - r], cmul_k(wA, fir_cr<R4>(r)));
-    } else {
 #pragma unroll
         for (int r = 0; r < R4 - 1; ++r) fir_pair_pre(acc[0][r], acc[1][R4 - 1 - r], fir_w0<MH, R4>(r));
         const float y0 = acc[0][R4 - 1].x, yN = acc[0][R4 - 1].y;
         acc[0][R4 - 1] = make_float2(0.5f * (y0 + yN), -0.5f * (y0 - yN));   // bin M/2: conj Z' = Y
         fir_unslots<R4>(acc, true);
     }
+    asm volatile("" ::: "memory");
 }
-// acc += X[2 kappa + 1] . Ho (pairs kappa, MH-1-kappa), then (pre) the inverse pre-step
-MSG_DEV void odd_mac_acc(const float2* tab, const float2 (&v)[2][R4], const float2* __restrict__ Ho,
-                         float2 (&acc)[2][R4]) {
+
+// Odd half (pairs kappa, MH-1-kappa), the same carry form
+MSG_DEV void odd_q2(const float2* tab, const float2 (&v)[2][R4], const float2* __restrict__ H0,
+                    const float2* __restrict__ H1, float2* sl, bool prev, bool emit, float2 (&acc)[2][R4]) {
     const int t = otid();
+    const uint32_t tu = (uint32_t)t;
     const float2 wA = cmul_k(fir4_wM(tab, G::OFF_PLO, G::OFF_PHI, t), wN1());   // W_N^(2t+1)
 #pragma unroll
     for (int r = 0; r < R4; ++r) {
@@ -628,43 +659,12 @@ MSG_DEV void odd_mac_acc(const float2* tab, const float2 (&v)[2][R4], const floa
         const float2 wk = cmul_k(wA, fir_cr<R4>(r));
         float2 xk, xm;
         fir_split(v[0][r], v[1][R4 - 1 - r], wk, xk, xm);
-        acc[0][r] = cfma(acc[0][r], xk, at32(Ho, kA));
-        acc[1][R4 - 1 - r] = cfma(acc[1][R4 - 1 - r], xm, at32(Ho, MH - 1 - kA));
+        q2_pair(xk, xm, at32(H0, kA), at32(H0, MH - 1 - kA), at32(H1, kA), at32(H1, MH - 1 - kA), acc[0][r],
+                acc[1][R4 - 1 - r], at32(sl, tu + (uint32_t)(r * T)), at32(sl, tu + (uint32_t)((R4 + r) * T)), prev,
+                emit);
+        fir_pair_pre(acc[0][r], acc[1][R4 - 1 - r], wk);
     }
-}
-MSG_DEV void odd_pre_q2(const float2* tab, float2 (&acc)[2][R4]) {
-    const int t = otid();
-    const float2 wA = cmul_k(fir4_wM(tab, G::OFF_PLO, G::OFF_PHI, t), wN1());
-#pragma unroll
-    for (int r = 0; r < R4; ++r) fir_pair_pre(acc[0][r], acc[1][R4 - 1 - r], cmul_k(wA, fir_cr<R4>(r)));
-}
-
-// one half of a block: acc = X_j H0 (+ X_{j-1} H1 from the slot), X_j into the slot
-template <bool ODD>
-MSG_DEV void q2_half_mac(const float2* tab, float2 (&v)[2][R4], const float2* __restrict__ H0,
-                         const float2* __restrict__ H1, float2* scratch, bool prev, float2 (&acc)[2][R4]) {
-#pragma unroll
-    for (int h = 0; h < 2; ++h)
-#pragma unroll
-        for (int r = 0; r < R4; ++r) acc[h][r] = make_float2(0.f, 0.f);
-    if (ODD) odd_mac_acc(tab, v, H0, acc);
-    else even_mac_acc(tab, v, H0, acc);
-    // swap v with the slot, one element at a time (read X_{j-1}, write X_j)
-#pragma unroll
-    for (int h = 0; h < 2; ++h)
-#pragma unroll
-        for (int r = 0; r < R4; ++r) {
-            float2* sl = q2_slot(scratch, ODD ? 1 : 0, h, r);
-            const float2 cur = v[h][r];
-            v[h][r] = prev ? *sl : make_float2(0.f, 0.f);
-            *sl = cur;
-        }
-    if (prev) {
-        if (ODD) odd_mac_acc(tab, v, H1, acc);
-        else even_mac_acc(tab, v, H1, acc);
-    }
-    if (ODD) odd_pre_q2(tab, acc);
-    else even_pre_q2(tab, acc);
+    asm volatile("" ::: "memory");
 }
 }  // namespace fir8
 
@@ -675,7 +675,7 @@ MSG_DEV void q2_half_mac(const float2* tab, float2 (&v)[2][R4], const float2* __
 __global__ void __launch_bounds__(fir8::T)
 k_fir8q(const PresetRt* __restrict__ rt, const int2* __restrict__ runs, int n_runs, int run_len,
         const float2* __restrict__ tables, const float2* __restrict__ hspec, const float* __restrict__ x_in,
-        float* __restrict__ y_out, float2* __restrict__ scratch_all, int32_t* __restrict__ ctr) {
+        float* __restrict__ y_out, float2* __restrict__ scratch_all, int32_t* __restrict__ ctr, int mode) {
     using namespace fir8;
     extern __shared__ __attribute__((aligned(16))) float2 lds[];
     __shared__ int s_take;
@@ -703,19 +703,14 @@ k_fir8q(const PresetRt* __restrict__ rt, const int2* __restrict__ runs, int n_ru
         const float* x = x_in + pr.y_off;
         float2 a[R1], b[R1];
         float2 v[2][R4];
-        if (j0 > 0) {                             // X_{j0-1} into the slot
+        if (j0 > 0) {                             // the carry X_{j0-1} H1 into the slot
+            float2 acc[2][R4];
             load_halves(x, n, (int64_t)(j0 - 2) * P, a, b);
             dif_split(tab, a, b);
             fwd_half<false>(buf, tab, a, v);
-#pragma unroll
-            for (int h = 0; h < 2; ++h)
-#pragma unroll
-                for (int r = 0; r < R4; ++r) *q2_slot(scratch, 0, h, r) = v[h][r];
+            even_q2(tab, v, He0, He1, q2_slot(scratch, 0), false, true, acc);
             fwd_half<true>(buf, tab, b, v);
-#pragma unroll
-            for (int h = 0; h < 2; ++h)
-#pragma unroll
-                for (int r = 0; r < R4; ++r) *q2_slot(scratch, 1, h, r) = v[h][r];
+            odd_q2(tab, v, Ho0, Ho1, q2_slot(scratch, 1), false, true, acc);
         }
         for (int j = j0; j < j1; ++j) {
             const int64_t t0 = (int64_t)j * P;
@@ -723,15 +718,16 @@ k_fir8q(const PresetRt* __restrict__ rt, const int2* __restrict__ runs, int n_ru
             dif_split(tab, a, b);
             float2 acc[2][R4], A[R1];
             fwd_half<false>(buf, tab, a, v);
-            q2_half_mac<false>(tab, v, He0, He1, scratch, j > 0, acc);
+            even_q2(tab, v, He0, He1, q2_slot(scratch, 0), j > 0 && !(mode & 1), j + 1 < j1 && !(mode & 2), acc);
             inv_half<false>(buf, tab, acc, A);
             fwd_half<true>(buf, tab, b, v);
-            q2_half_mac<true>(tab, v, Ho0, Ho1, scratch, j > 0, acc);
+            odd_q2(tab, v, Ho0, Ho1, q2_slot(scratch, 1), j > 0 && !(mode & 1), j + 1 < j1 && !(mode & 2), acc);
             float2 (&B)[R1] = a;                  // a is dead: its registers take B
             inv_half<true>(buf, tab, acc, B);
-            const float2 wt = fir4_wM(tab, G::OFF_PLO, G::OFF_PHI, t);
+            const int tt = otid();                // per block: loop-invariant twiddles would be hoisted
+            const float2 wt = fir4_wM(tab, G::OFF_PLO, G::OFF_PHI, tt);
             const SegOut so = seg_out(y_out, pr.y_off, t0, n, P, P + 1);
-            const int d0 = 2 * t - P;
+            const int d0 = 2 * tt - P;
             const float s = 1.0f / (float)M;
 #pragma unroll
             for (int r = 0; r < R1; ++r) {

@@ -31,6 +31,8 @@ void fir_init_attrs() {
                               Fir4Geo<16384>::LDS_BYTES);
     (void)hipFuncSetAttribute((const void*)k_fir8p<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               Fir4Geo<16384>::LDS_BYTES);
+    (void)hipFuncSetAttribute((const void*)k_fir8q, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              Fir4Geo<16384>::LDS_BYTES);
     (void)hipFuncSetAttribute((const void*)k_fir8p<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               Fir4Geo<16384>::LDS_BYTES);
     (void)hipFuncSetAttribute((const void*)k_fir8_hconv<0>, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -163,6 +165,16 @@ hipError_t launch_fir8p(unsigned n_jobs, unsigned grid, hipStream_t s, const Pre
                            (int)n_jobs, tables, hspec, x_in, y_out, ctr, stagger, events, grain_pool, ev_lo);
     return hipGetLastError();
 }
+
+// two-partition k_fir8q (fir8_fft.h): runs of run_len blocks, scratch: grid x fir8q_scratch_per_wg() float2
+hipError_t launch_fir8q(unsigned n_runs, int run_len, unsigned grid, hipStream_t s, const PresetRt* rt, const int2* runs,
+                        const float2* tables, const float2* hspec, const float* x_in, float* y_out, float2* scratch,
+                        int32_t* ctr, int mode) {
+    hipLaunchKernelGGL(k_fir8q, dim3(grid), dim3(fir8::T), Fir4Geo<16384>::LDS_BYTES, s, rt, runs, (int)n_runs, run_len,
+                       tables, hspec, x_in, y_out, scratch, ctr, mode);
+    return hipGetLastError();
+}
+int64_t fir8q_scratch_per_wg() { return fir8::Q2_SLOT; }
 
 hipError_t launch_fir8_hconv(unsigned n_presets, hipStream_t s, const PresetRt* rt, const int32_t* list,
                              const float2* tables, const int32_t* er_off, const double* er_gain, float2* hspec) {

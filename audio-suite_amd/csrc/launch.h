@@ -99,6 +99,13 @@ hipError_t launch_fir8p(unsigned n_jobs, unsigned grid, hipStream_t s, const Pre
                         int stagger, const msg_event* events, const float* grain_pool,
                         const int32_t* ev_lo);   // events: null if no ola_fir preset; ev_lo: per job, the
                                                  // first event reaching its segment
+// two partitions of N / 2 taps on the N = 65536 engine (fir8_fft.h k_fir8q): B = P = 32768,
+// runs (signal, first block) of run_len blocks; the signal's PresetRt::fir_Q holds its block count
+constexpr int FIR8Q_P = FIR8_N / 2;
+hipError_t launch_fir8q(unsigned n_runs, int run_len, unsigned grid, hipStream_t s, const PresetRt* rt, const int2* runs,
+                        const float2* tables, const float2* hspec, const float* x_in, float* y_out, float2* scratch,
+                        int32_t* ctr, int mode = 0);   // mode: timing experiments only (MSGPU_FIR8Q_MODE)
+int64_t fir8q_scratch_per_wg();
 hipError_t launch_fir8_hconv(unsigned n_presets, hipStream_t s, const PresetRt* rt, const int32_t* list,
                              const float2* tables, const int32_t* er_off, const double* er_gain, float2* hspec);
 hipError_t launch_fir8_spec64(unsigned n_jobs, hipStream_t s, const int64_t* jobs, const float2* tables,

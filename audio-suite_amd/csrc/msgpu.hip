@@ -219,6 +219,7 @@ struct msg_ctx {
     // (one per CU, per-XCD block counters; C3 isolated FIR 2.03 -> 1.86 ms, C5 131.6
     // -> 125.9 ms per step, profiles/r04r_ab.json)
     int fir8p = 1;
+    bool fir8q = true;           // msg_fir: 32 k < M <= 64 k taps as two partitions on k_fir8q (MSGPU_FIR8Q=0: off)
     int n_cu = 256;              // compute units (persistent grids)
     int fir8p_cus = 0;           // persistent FIR workgroups (MSGPU_FIR8P_CUS, A/B; 0: one per CU)
     int fir8p_stagger = 0;       // k_fir8p: every other workgroup starts this many 10-ns ticks later (MSGPU_FIR8P_STAGGER)
@@ -749,6 +750,7 @@ msg_ctx* msg_create(int device_ordinal) {
     if (const char* e = getenv("MSGPU_FIR64")) ctx->fir64 = atoi(e);
     if (const char* e = getenv("MSGPU_FIR64_CAP")) ctx->fir64_cap = std::max(1, std::min(FIR64_CAP, atoi(e)));
     if (const char* e = getenv("MSGPU_FIR8P")) ctx->fir8p = atoi(e);
+    if (const char* e = getenv("MSGPU_FIR8Q")) ctx->fir8q = e[0] != '0';
     if (const char* e = getenv("MSGPU_FIR8P_CUS")) ctx->fir8p_cus = std::max(0, atoi(e));
     if (const char* e = getenv("MSGPU_FIR8P_STAGGER")) ctx->fir8p_stagger = std::max(0, atoi(e));
     if (const char* e = getenv("MSGPU_OLA_FIR")) ctx->ola_fir = e[0] != '0';
@@ -1014,6 +1016,52 @@ int msg_fir(msg_ctx* ctx, const float* x_dev, float* y_dev, int64_t n, int32_t n
     // 8 B/output of spectrum writes and 8 Q B/output of reads.  Measured on
     // MI355X: slower at 64 k taps (classic Q = 5: 7.1 ms vs 7.7 ms per 1024
     // signals), so it takes over only from Q = 8 (>= ~115 k taps).
+    // Two partitions of 32 768 taps on the 65 536-point engine (k_fir8q, 32 768
+    // < M <= 65 536 beyond the one-partition limit): one forward and one inverse
+    // per 32 768 outputs (MSGPU_FIR8Q=0: the choice above, k_fir4 at 64 k taps).
+    // Above 35 748 taps the two partitions' 32 768-frame blocks beat one
+    // partition's 65 537 - M (a k_fir8q block costs ~1.1 k_fir8p blocks).
+    if (ctx->fir8 && ctx->fir8q && ctx->fir8p > 0 && M <= 2 * (int64_t)FIR8Q_P &&
+        (double)(FIR8_N + 1 - M) * 1.1 < (double)FIR8Q_P) {
+        const int64_t nb = (n + FIR8Q_P - 1) / FIR8Q_P;
+        if (nb * n_signals > INT32_MAX) return fail(ctx, MSG_E_UNSUPPORTED, "too many output blocks");
+        if (fir_shape) { fir_shape[0] = FIR8_N; fir_shape[1] = FIR8Q_P; fir_shape[2] = 2; }
+        // runs of consecutive blocks: about four per CU over the call, whole signals when they suffice
+        const int64_t want = 4 * (int64_t)ctx->n_cu;
+        const int run_len = (int)std::max<int64_t>(1, std::min<int64_t>(nb, (nb * n_signals + want - 1) / want));
+        std::vector<PresetRt> prt((size_t)n_signals);
+        std::vector<int2> runs;
+        for (int i = 0; i < n_signals; ++i) {
+            PresetRt& r = prt[i];
+            memset(&r, 0, sizeof(r));
+            r.out_n = n;
+            r.y_off = (int64_t)i * n;
+            r.fir_on = 1; r.fir_N = FIR8_N; r.fir_P = FIR8Q_P; r.fir_Q = (int32_t)nb; r.fir_B = FIR8Q_P;
+            for (int64_t j = 0; j < nb; j += run_len) runs.push_back(make_int2(i, (int)j));
+        }
+        std::vector<float> hf((size_t)M);
+        for (int64_t i = 0; i < M; ++i) hf[i] = (float)h[i];
+        const int64_t K8 = FIR8_N / 2 + 1;
+        const int64_t job[8] = {0, FIR8Q_P, 0, 0, FIR8Q_P, M - FIR8Q_P, K8, 0};   // H_0, H_1 from the float taps
+        const unsigned grid = (unsigned)std::min<int64_t>((int64_t)runs.size(), ctx->n_cu);
+        HIPCHK(ctx, ctx->sf_prt.ensure(prt.size()));
+        HIPCHK(ctx, ctx->sf_jobs.ensure(runs.size()));
+        HIPCHK(ctx, ctx->sf_hf.ensure((size_t)M));
+        HIPCHK(ctx, ctx->sf_irjobs.ensure(8));
+        HIPCHK(ctx, ctx->sf_hspec.ensure((size_t)(2 * K8)));
+        HIPCHK(ctx, ctx->sf_xspec.ensure((size_t)grid * (size_t)fir8q_scratch_per_wg()));
+        HIPCHK(ctx, fir8_counters(ctx, s));
+        HIPCHK(ctx, hipMemcpyAsync(ctx->sf_prt.p, prt.data(), sizeof(PresetRt) * prt.size(), hipMemcpyHostToDevice, s));
+        HIPCHK(ctx, hipMemcpyAsync(ctx->sf_jobs.p, runs.data(), sizeof(int2) * runs.size(), hipMemcpyHostToDevice, s));
+        HIPCHK(ctx, hipMemcpyAsync(ctx->sf_hf.p, hf.data(), sizeof(float) * (size_t)M, hipMemcpyHostToDevice, s));
+        HIPCHK(ctx, hipMemcpyAsync(ctx->sf_irjobs.p, job, sizeof(job), hipMemcpyHostToDevice, s));
+        HIPCHK(ctx, launch_fir8_spec32(2, s, ctx->sf_irjobs.p, ctx->d_fir4tab, ctx->sf_hf.p, ctx->sf_hspec.p));
+        HIPCHK(ctx, launch_fir8q((unsigned)runs.size(), run_len, grid, s, ctx->sf_prt.p, ctx->sf_jobs.p, ctx->d_fir4tab,
+                                 ctx->sf_hspec.p, x_dev, y_dev, ctx->sf_xspec.p, ctx->fir8_ctr.p,
+                                 getenv("MSGPU_FIR8Q_MODE") ? atoi(getenv("MSGPU_FIR8Q_MODE")) : 0));
+        HIPCHK(ctx, done.finish());
+        return MSG_OK;
+    }
     const bool fdl = Q >= 8;
     if (fdl) {
         N = FIR_NMAX;

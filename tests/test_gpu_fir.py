@@ -73,7 +73,7 @@ def test_fir_errors():
         eng.fir(x, np.ones(64 * 32768))
 
 
-@pytest.mark.parametrize("M", [16383, 16384, 25473, 40000])
+@pytest.mark.parametrize("M", [16383, 16384, 25473, 35000])
 def test_fir8_block_edges_and_alignment(M):
     """k_fir8's block epilogue and edge-block loads: odd and even tap counts (the
     output pairs are written as 8-byte stores only for odd P and an 8-byte-aligned
@@ -95,3 +95,37 @@ def test_fir8_block_edges_and_alignment(M):
         print(f"M={M} row {b}: rel rms {e:.3e}")
         assert e <= REL, (M, b)
         assert np.all(np.isfinite(y[b]))
+
+
+@pytest.mark.parametrize("M,n,S", [(65536, 384000, 4), (40000, 100001, 3), (36000, 1_000_000, 3), (65536, 20000, 2)])
+def test_fir8q_two_partitions(M, n, S):
+    """k_fir8q: 35 749 <= M <= 64 k taps as two 32 768-tap
+    partitions on the 65 536-point engine, B = P = 32 768 (below, one partition
+    on k_fir8 has the longer block).  Whole-signal runs
+    (C3-like batch), runs of single blocks that open with X_{j0-1} (few signals,
+    many blocks: every run past block 0 takes the pre-block path), an odd length
+    with odd row offsets, and a signal shorter than one block; MSGPU_FIR8Q=0
+    (k_fir4, five partitions) agrees too."""
+    import os
+    import torch
+    from msgpu.engine import Engine
+    from oracle import msound_oracle as O
+    h = O.synthetic_fir_taps(M)
+    x = np.stack([np.random.default_rng(11 + b).standard_normal(n).astype(np.float32) for b in range(S)])
+    outs = {}
+    for flag in ("1", "0"):
+        os.environ["MSGPU_FIR8Q"] = flag
+        try:
+            eng = Engine(0)
+        finally:
+            os.environ.pop("MSGPU_FIR8Q", None)
+        y, shape = eng.fir(torch.from_numpy(x).cuda(), h)
+        torch.cuda.synchronize()
+        outs[flag] = (y.cpu().numpy(), shape)
+    assert outs["1"][1] == (65536, 32768, 2) and outs["0"][1] != (65536, 32768, 2)
+    for b in range(S):
+        r = _ref(x[b], h)
+        for flag, (y, shape) in outs.items():
+            e = _rel_rms(y[b], r)
+            print(f"M={M} n={n} row {b} FIR8Q={flag} {shape}: rel rms {e:.3e}")
+            assert e <= REL and np.all(np.isfinite(y[b])), (flag, b)

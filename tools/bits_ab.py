@@ -37,7 +37,7 @@ def batch():
            msgpu.merged(out_dur_s=0.3, seed=8, sat_drive=0.0),                                # no tanh
            msgpu.merged(base, base_sr=48000, out_dur_s=0.3, space_ir_on=True, seed=22, er_cloud_on=True,
                         space_ir_max_samps=8192, stereo_width=0.3),                            # float64 FIR
-           msgpu.merged(out_dur_s=0.0013, seed=9),                                             # under one tile
+           msgpu.merged(out_dur_s=0.0013, seed=9, env_a=0.0, env_r=0.5),                     # under one tile
            msgpu.merged(out_dur_s=1.5, seed=10, stereo_width=1.0, base_sr=44100)]
     for i in range(5):                                                                         # odd offsets
         ps.append(msgpu.merged(out_dur_s=0.1 + 0.0000227 * i, seed=40 + i, base_sr=44100))
