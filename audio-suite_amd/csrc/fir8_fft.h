@@ -571,23 +571,45 @@ constexpr int Q2_SLOT = 2 * 2 * R4 * T;          // float2 per workgroup: halves
 MSG_DEV float2* q2_slot(float2* scratch, int half) { return scratch + half * 2 * R4 * T; }
 
 // One pair (k, M - k) of a half: the split X of this block's bins, acc = X H0
-// (+ the carry C_j = X_{j-1} H1 that the previous block left in the slot), and
-// the new carry X H1 into the slot (load before store: each thread reads back
-// only what it wrote).  The empty asm with a memory clobber keeps the pairs'
-// slot accesses in order, so the carries do not pile up in registers.
+// (+ the carry C_j = X_{j-1} H1 that the previous block left in the slot, read
+// into ck / cm at the start of the half: all of the half's carry loads are in
+// flight before the first product), and the new carry X H1 into the slot (each
+// thread overwrites only what it read).
 MSG_DEV void q2_pair(float2 xk, float2 xm, float2 h0k, float2 h0m, float2 h1k, float2 h1m, float2& ak, float2& am,
-                     float2& sk, float2& sm, bool prev, bool emit) {
-    asm volatile("" ::: "memory");
+                     float2 ck, float2 cm, float2& sk, float2& sm, bool prev, bool emit) {
     ak = cmul(xk, h0k);
     am = cmul(xm, h0m);
     if (prev) {
-        ak = ff(vv(ak) + vv(sk));
-        am = ff(vv(am) + vv(sm));
+        ak = ff(vv(ak) + vv(ck));
+        am = ff(vv(am) + vv(cm));
     }
     if (emit) {
         sk = cmul(xk, h1k);
         sm = cmul(xm, h1m);
     }
+}
+// this thread's carries of pair r of one half (elements r and R4 + r at e T + t),
+// loaded MSG_Q2_AHEAD pairs ahead of their use; the empty asm statements (memory
+// clobbers) keep the compiler from hoisting every load to the top of the half
+// (sixteen carries beside v, b and the accumulators: scratch spills).  Measured
+// at 64 k taps per 1024 x 384 000 (profiles/r06h_fir8q_prefetch_ab.txt): 0 pairs
+// ahead 2.89 / 2.90 ms, 2 ahead 2.96 / 2.94, 4 ahead 3.14 / 3.10 (each pair
+// ahead costs 16 B of scratch spills per lane)
+#ifndef MSG_Q2_AHEAD
+#define MSG_Q2_AHEAD 0
+#endif
+constexpr int Q2_AHEAD = MSG_Q2_AHEAD;
+MSG_DEV void q2_carry_load(const float2* sl, bool prev, int r, float2 (&c)[2][R4]) {
+    if (r >= R4) return;
+    const uint32_t tu = (uint32_t)otid();
+    asm volatile("" ::: "memory");
+    c[0][r] = prev ? at32(sl, tu + (uint32_t)(r * T)) : make_float2(0.f, 0.f);
+    c[1][r] = prev ? at32(sl, tu + (uint32_t)((R4 + r) * T)) : make_float2(0.f, 0.f);
+    asm volatile("" ::: "memory");
+}
+MSG_DEV void q2_carry_first(const float2* sl, bool prev, float2 (&c)[2][R4]) {
+#pragma unroll
+    for (int r = 0; r < Q2_AHEAD; ++r) q2_carry_load(sl, prev, r, c);
 }
 
 // Even half of a block on the carry form (k_fir8's even_mac_pre with H0, plus
@@ -596,6 +618,8 @@ MSG_DEV void even_q2(const float2* tab, const float2 (&v)[2][R4], const float2* 
                      const float2* __restrict__ H1, float2* sl, bool prev, bool emit, float2 (&acc)[2][R4]) {
     const int t = otid();
     const uint32_t tu = (uint32_t)t;
+    float2 c[2][R4];
+    q2_carry_first(sl, prev, c);
     if (t != 0) {
         const float2 wA = fir4_wM(tab, G::OFF_PLO, G::OFF_PHI, t);
 #pragma unroll
@@ -603,10 +627,11 @@ MSG_DEV void even_q2(const float2* tab, const float2 (&v)[2][R4], const float2* 
             const int kA = t + r * NB4;
             const float2 wk = cmul_k(wA, fir_cr<R4>(r));
             float2 xk, xm;
+            q2_carry_load(sl, prev, r + Q2_AHEAD, c);
             fir_split(v[0][r], v[1][R4 - 1 - r], wk, xk, xm);
             q2_pair(xk, xm, at32(H0, kA), at32(H0, MH - kA), at32(H1, kA), at32(H1, MH - kA), acc[0][r],
-                    acc[1][R4 - 1 - r], at32(sl, tu + (uint32_t)(r * T)), at32(sl, tu + (uint32_t)((R4 + r) * T)),
-                    prev, emit);
+                    acc[1][R4 - 1 - r], c[0][r], c[1][r], at32(sl, tu + (uint32_t)(r * T)),
+                    at32(sl, tu + (uint32_t)((R4 + r) * T)), prev, emit);
             fir_pair_pre(acc[0][r], acc[1][R4 - 1 - r], wk);
         }
     } else {
@@ -615,22 +640,22 @@ MSG_DEV void even_q2(const float2* tab, const float2 (&v)[2][R4], const float2* 
 #pragma unroll
         for (int r = 0; r < R4; ++r) {
             const int kA = fir_k0<MH, R4>(r);
+            q2_carry_load(sl, prev, r + Q2_AHEAD, c);
             if (r < R4 - 1) {
                 float2 xk, xm;
                 fir_split(a[r], bb[R4 - 1 - r], fir_w0<MH, R4>(r), xk, xm);
                 q2_pair(xk, xm, H0[kA], H0[MH - kA], H1[kA], H1[MH - kA], acc[0][r], acc[1][R4 - 1 - r],
-                        sl[r * T], sl[(R4 + r) * T], prev, emit);
+                        c[0][r], c[1][r], sl[r * T], sl[(R4 + r) * T], prev, emit);
             } else {   // DC/Nyquist packed as (Y[0], Y[M]) and bin M/2
                 const float2 z0 = a[r];
                 const float2 xd = make_float2(z0.x + z0.y, z0.x - z0.y), xh = cconj(bb[0]);
-                asm volatile("" ::: "memory");
                 acc[0][r] = make_float2(xd.x * H0[0].x, xd.y * H0[MH].x);
                 acc[1][0] = cmul(xh, H0[MH / 2]);
                 float2& s0 = sl[r * T];
                 float2& s1 = sl[(2 * R4 - 1) * T];
                 if (prev) {
-                    acc[0][r] = ff(vv(acc[0][r]) + vv(s0));
-                    acc[1][0] = ff(vv(acc[1][0]) + vv(s1));
+                    acc[0][r] = ff(vv(acc[0][r]) + vv(c[0][r]));
+                    acc[1][0] = ff(vv(acc[1][0]) + vv(c[1][R4 - 1]));
                 }
                 if (emit) {
                     s0 = make_float2(xd.x * H1[0].x, xd.y * H1[MH].x);
@@ -652,16 +677,19 @@ MSG_DEV void odd_q2(const float2* tab, const float2 (&v)[2][R4], const float2* _
                     const float2* __restrict__ H1, float2* sl, bool prev, bool emit, float2 (&acc)[2][R4]) {
     const int t = otid();
     const uint32_t tu = (uint32_t)t;
+    float2 c[2][R4];
+    q2_carry_first(sl, prev, c);
     const float2 wA = cmul_k(fir4_wM(tab, G::OFF_PLO, G::OFF_PHI, t), wN1());   // W_N^(2t+1)
 #pragma unroll
     for (int r = 0; r < R4; ++r) {
         const int kA = t + r * NB4;
         const float2 wk = cmul_k(wA, fir_cr<R4>(r));
         float2 xk, xm;
+        q2_carry_load(sl, prev, r + Q2_AHEAD, c);
         fir_split(v[0][r], v[1][R4 - 1 - r], wk, xk, xm);
         q2_pair(xk, xm, at32(H0, kA), at32(H0, MH - 1 - kA), at32(H1, kA), at32(H1, MH - 1 - kA), acc[0][r],
-                acc[1][R4 - 1 - r], at32(sl, tu + (uint32_t)(r * T)), at32(sl, tu + (uint32_t)((R4 + r) * T)), prev,
-                emit);
+                acc[1][R4 - 1 - r], c[0][r], c[1][r], at32(sl, tu + (uint32_t)(r * T)),
+                at32(sl, tu + (uint32_t)((R4 + r) * T)), prev, emit);
         fir_pair_pre(acc[0][r], acc[1][R4 - 1 - r], wk);
     }
     asm volatile("" ::: "memory");

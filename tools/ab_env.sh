@@ -8,7 +8,7 @@ for spec in "$@"; do
   IFS='|' read -r label envs lib <<< "$spec"
   if [ "$lib" != base ] && [ -n "$lib" ]; then libenv="MSGPU_LIB=$PWD/audio-suite_amd/msgpu/libmsgpu_$lib.so"; else libenv=""; fi
   echo "=== $label ($envs $libenv)"
-  env $envs $libenv timeout -k 10 200 python bench.py --no-cpu --points= --steps 40 --from-dicts-steps 0 \
+  env $envs $libenv timeout -k 10 200 python bench.py --no-cpu --points= --fir-points= --steps 40 --from-dicts-steps 0 \
       > gpurun_out/${tag}_$label.json 2> gpurun_out/${tag}_$label.log
   rc=$?
   if [ $rc -ne 0 ]; then echo "rc=$rc"; tail -5 gpurun_out/${tag}_$label.log; exit $rc; fi

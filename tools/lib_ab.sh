@@ -6,7 +6,7 @@ set -e
 mkdir -p gpurun_out
 for v in "$@"; do
   if [ "$v" != base ]; then export MSGPU_LIB=$PWD/audio-suite_amd/msgpu/libmsgpu_$v.so; else unset MSGPU_LIB; fi
-  timeout -k 10 200 python bench.py --no-cpu --points= > gpurun_out/ab_$v.json 2>/dev/null
+  timeout -k 10 200 python bench.py --no-cpu --points= --fir-points= > gpurun_out/ab_$v.json 2>/dev/null
   python3 -c "
 import json;d=json.load(open('gpurun_out/ab_$v.json'));i=d['roofline_isolated']['stage_ms'];t=d['stage_ms']
 print('$v', 'step', d['ms_per_step'], 'ok', d['checked']['all_ok'])
