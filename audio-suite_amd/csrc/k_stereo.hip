@@ -9,6 +9,13 @@ hipError_t launch_stereo_max(unsigned n_tiles, hipStream_t s, const PresetRt* rt
     return hipGetLastError();
 }
 
+hipError_t launch_stereo_pred(unsigned n_presets, hipStream_t s, const PresetRt* rt, const int32_t* st_begin,
+                              int n_tiles, const unsigned* maxbits, const StereoSync& sy) {
+    hipLaunchKernelGGL(k_stereo_pred, dim3(n_presets), dim3(ST_T), 0, s, rt, st_begin, (int)n_presets, n_tiles, maxbits,
+                       sy);
+    return hipGetLastError();
+}
+
 hipError_t launch_stereo_fused(unsigned grid, unsigned n_tiles, hipStream_t s, const PresetRt* rt,
                                const int32_t* st_begin, int n_presets, const float* y, unsigned* maxbits,
                                const StereoSync& sy, int32_t* ctr, float* out) {

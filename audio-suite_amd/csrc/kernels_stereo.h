@@ -373,19 +373,61 @@ MSG_DEV int st_tiles_of(const int32_t* __restrict__ st_begin, int n_presets, int
     return (p + 1 < n_presets ? st_begin[p + 1] : n_tiles) - st_begin[p];
 }
 
+// The max pass of the two-launch path: each tile's peak into maxbits[p] (a
+// non-returning atomic) and, for the float64 FIR's predictor, its two partial
+// sums into part[2 b] -- no count of finished tiles: round 5 ended every tile
+// with stereo_run_done's drain and returning atomic (the last tile of a preset
+// summed the partials), a memory round trip per 4096 frames the workgroup
+// waited out; k_stereo_pred now does that per preset after the launch.
 __global__ void __launch_bounds__(ST_T)
 k_stereo_max(const PresetRt* __restrict__ rt, const int32_t* __restrict__ st_begin, int n_presets, int n_tiles,
              const float* __restrict__ ybuf, unsigned* __restrict__ maxbits, StereoSync sy) {
     __shared__ __attribute__((aligned(16))) float w[ST_WIN];
     __shared__ float wm[3 * (ST_T / 64)];
-    __shared__ double s_red[2 * (ST_T / 64)];
-    __shared__ int s_last;
     const int b = job_order_st();
     const int p = find_preset(st_begin, n_presets, b);
     const PresetRt& r = rt[p];
     const float m = stereo_max_vals(r, b - st_begin[p], ybuf, nullptr,
                                     (sy.part && r.fir_on) ? sy.part + 2 * b : nullptr, false, w, wm);
-    stereo_run_done(r, p, st_begin[p], st_tiles_of(st_begin, n_presets, n_tiles, p), 1, m, maxbits, sy, &s_last, s_red);
+    if (threadIdx.x == 0) atomicMax(maxbits + p, __float_as_uint(m));
+    (void)n_tiles;
+}
+
+// Per preset, after k_stereo_max (sy.part set: the float64 FIR is on): the
+// tiles' partial sums added in tile order -- thread i takes tiles i, i + ST_T,
+// ..., then the waves' butterflies and the waves in order, the arithmetic of
+// stereo_run_done's last tile, so the sums and the route are the same bits --
+// then the predictor and flag64 (0 for a preset without a filter).
+__global__ void __launch_bounds__(ST_T)
+k_stereo_pred(const PresetRt* __restrict__ rt, const int32_t* __restrict__ st_begin, int n_presets, int n_tiles,
+              const unsigned* __restrict__ maxbits, StereoSync sy) {
+    __shared__ double s_red[2 * (ST_T / 64)];
+    const int p = blockIdx.x;
+    const PresetRt& r = rt[p];
+    if (!r.fir_on) {
+        if (threadIdx.x == 0) sy.flag64[p] = 0;
+        return;
+    }
+    const int tile0 = st_begin[p], cnt = st_tiles_of(st_begin, n_presets, n_tiles, p);
+    double a = 0.0, b = 0.0;
+    for (int i = threadIdx.x; i < cnt; i += ST_T) {
+        a += __hip_atomic_load(sy.part + 2 * (tile0 + i), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        b += __hip_atomic_load(sy.part + 2 * (tile0 + i) + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    for (int off = 32; off > 0; off >>= 1) { a += __shfl_xor(a, off); b += __shfl_xor(b, off); }
+    if ((threadIdx.x & 63) == 0) {
+        s_red[threadIdx.x >> 6] = a;
+        s_red[ST_T / 64 + (threadIdx.x >> 6)] = b;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        a = s_red[0];
+        b = s_red[ST_T / 64];
+        for (int k = 1; k < ST_T / 64; ++k) { a += s_red[k]; b += s_red[ST_T / 64 + k]; }
+        sy.stats[2 * p] = a;
+        sy.stats[2 * p + 1] = b;
+        sy.flag64[p] = (sy.f64mode >= 2 || fir64_pred(r, a, b, maxbits[p]) > FIR64_PRED) ? 1 : 0;
+    }
 }
 
 // The float64 FIR's presets again (kernels_fir64.h) and the odd-length presets

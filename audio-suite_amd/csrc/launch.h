@@ -153,6 +153,9 @@ hipError_t launch_fft64_one(int lds_bytes, hipStream_t s, const Real64Plan* plan
 // stereo, tanh clip and peak normalisation (kernels_stereo.h)
 hipError_t launch_stereo_max(unsigned n_tiles, hipStream_t s, const PresetRt* rt, const int32_t* st_begin, int n_presets,
                              const float* y, unsigned* maxbits, const StereoSync& sy);
+// after k_stereo_max, with the float64 FIR on: per preset the predictor's sums (tile order) and flag64
+hipError_t launch_stereo_pred(unsigned n_presets, hipStream_t s, const PresetRt* rt, const int32_t* st_begin,
+                              int n_tiles, const unsigned* maxbits, const StereoSync& sy);
 hipError_t launch_stereo_fused(unsigned grid, unsigned n_tiles, hipStream_t s, const PresetRt* rt,
                                const int32_t* st_begin, int n_presets, const float* y, unsigned* maxbits,
                                const StereoSync& sy, int32_t* ctr, float* out);

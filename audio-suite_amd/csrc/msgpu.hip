@@ -2309,6 +2309,8 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
                                         sy, ctx->st_ctr.p, out_dev));
     } else {
         HIPCHK(ctx, launch_stereo_max((unsigned)stiles, s, ctx->prt.p, ctx->st_begin.p, P, yb, ctx->maxbits.p, sy));
+        if (f64_on)   // the float64 FIR's predictor per preset, from the tiles' partial sums
+            HIPCHK(ctx, launch_stereo_pred((unsigned)P, s, ctx->prt.p, ctx->st_begin.p, stiles, ctx->maxbits.p, sy));
     }
     if (f64_on) {   // flagged presets: the FIR again in float64, y overwritten (kernels_fir64.h)
         Fir64Launch a;

@@ -10,6 +10,6 @@ export TMPDIR=/tmp
 cd /tmp
 timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE \
     --output-format csv -d "$O/${tag}_sq" -o run -- \
-    python3 "$R/bench.py" --steps 2 --warmup 1 --no-cpu --iso-steps 0 --points= --streams 1 "$@" > "$O/${tag}_sq.log" 2>&1
+    python3 "$R/bench.py" --steps 2 --warmup 1 --no-cpu --iso-steps 0 --points= --fir-points= --streams 1 "$@" > "$O/${tag}_sq.log" 2>&1
 cd "$R"
 python3 tools/pmc_summary.py "$O/${tag}_sq" > "$O/${tag}_sq_summary.txt" 2>&1 || true

@@ -13,7 +13,7 @@ bash tools/pmc_sq.sh "$tag" || exit $?
 for c in C4 C5; do
   steps=10; [ $c = C5 ] && steps=3
   (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/${tag}_$c" -o run -- \
-      python3 "$R/bench.py" --config $c --no-cpu --iso-steps 0 --points= --steps $steps \
+      python3 "$R/bench.py" --config $c --no-cpu --iso-steps 0 --points= --fir-points= --steps $steps \
       > "$R/gpurun_out/${tag}_${c}_bench.json" 2> "$R/gpurun_out/${tag}_$c.log") || exit $?
   python3 - "$tag" $c <<'PY'
 import csv, glob, json, sys
@@ -28,7 +28,7 @@ done
 cd /tmp
 for k in FETCH_SIZE WRITE_SIZE; do
   timeout -k 10 300 rocprofv3 --pmc $k --output-format csv -d "$R/gpurun_out/${tag}_C5_pmc_$k" -o run -- \
-      python3 "$R/bench.py" --config C5 --steps 1 --warmup 1 --no-cpu --iso-steps 0 --points= \
+      python3 "$R/bench.py" --config C5 --steps 1 --warmup 1 --no-cpu --iso-steps 0 --points= --fir-points= \
       > "$R/gpurun_out/${tag}_C5_pmc_$k.log" 2>&1 || exit $?
 done
 cd "$R"

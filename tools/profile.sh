@@ -18,11 +18,11 @@ mkdir -p "$O"
 export TMPDIR=/tmp
 cd /tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/${tag}_prof" -o run -- \
-    python3 "$R/bench.py" --no-cpu --iso-steps 0 --points= "$@" > "$O/${tag}_prof_bench.json" 2> "$O/${tag}_prof.log"
+    python3 "$R/bench.py" --no-cpu --iso-steps 0 --points= --fir-points= "$@" > "$O/${tag}_prof_bench.json" 2> "$O/${tag}_prof.log"
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$O/${tag}_pmc_fetch" -o run -- \
-    python3 "$R/bench.py" --steps 2 --warmup 1 --no-cpu --iso-steps 0 --points= "$@" > "$O/${tag}_pmc_fetch.log" 2>&1
+    python3 "$R/bench.py" --steps 2 --warmup 1 --no-cpu --iso-steps 0 --points= --fir-points= "$@" > "$O/${tag}_pmc_fetch.log" 2>&1
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$O/${tag}_pmc_write" -o run -- \
-    python3 "$R/bench.py" --steps 2 --warmup 1 --no-cpu --iso-steps 0 --points= "$@" > "$O/${tag}_pmc_write.log" 2>&1
+    python3 "$R/bench.py" --steps 2 --warmup 1 --no-cpu --iso-steps 0 --points= --fir-points= "$@" > "$O/${tag}_pmc_write.log" 2>&1
 cd "$R"
 python3 tools/pmc_traffic.py "$O/${tag}_pmc_fetch" "$O/${tag}_pmc_write" --config "${CONFIG:-C3}" \
     --batch "${BATCH:-341}" --out "$O/${tag}_traffic.json"
