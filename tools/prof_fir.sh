@@ -17,23 +17,15 @@ for k in FETCH_SIZE WRITE_SIZE; do
       python3 "$R/tools/fir_bench.py" --taps 16384,65536 --steps 2 --warmup 1 > "$O/${tag}_fir_pmc_$k.log" 2>&1
 done
 cd "$R"
+python3 tools/pmc_traffic.py "$O/${tag}_fir_pmc_FETCH_SIZE" "$O/${tag}_fir_pmc_WRITE_SIZE" --config FIR \
+    --batch 1024 --out "$O/${tag}_traffic_FIR.json"
 python3 - "$O" "$tag" <<'PY'
 import csv, glob, json, sys
 O, tag = sys.argv[1:3]
 f = glob.glob(f"{O}/{tag}_fir_prof/**/*kernel_stats.csv", recursive=True)[0]
-print("kernel stats:", f)
 for r in sorted(csv.DictReader(open(f)), key=lambda r: -float(r["TotalDurationNs"]))[:8]:
     print("  ", r["Name"][:70], r["Calls"], round(float(r["AverageNs"]) / 1e6, 4), "ms avg")
-for k in ("FETCH_SIZE", "WRITE_SIZE"):
-    fs = glob.glob(f"{O}/{tag}_fir_pmc_{k}/**/*counter_collection.csv", recursive=True)
-    tot = {}
-    for ff in fs:
-        for r in csv.DictReader(open(ff)):
-            n = r.get("Kernel_Name", "")
-            if "k_fir8" not in n:
-                continue
-            key = n.split("(")[0]
-            tot.setdefault(key, []).append(float(r["Counter_Value"]))
-    for key, v in tot.items():
-        print(k, key, "launches", len(v), "avg KB", round(sum(v) / len(v), 1))
+t = json.load(open(f"{O}/{tag}_traffic_FIR.json"))
+for k, v in t["kernels"].items():
+    print("  traffic", k[:60], v.get("hbm_bytes_per_launch"))
 PY
