@@ -1,6 +1,7 @@
 // host_san.cpp — host-only build of libmsgpu's host entry points for the
 // sanitizers (SURVEY §5 "race detection / sanitizers"): the render plan
-// (plan.h, msg_plan_host) and the NumPy stream primitives (nprng.h, msg_rng_*)
+// (plan.h, msg_plan_host), the NumPy stream primitives (nprng.h, msg_rng_*) and
+// the render digest's host reference (digest.h, msg_digest_host)
 // compiled by g++ with -fsanitize=address,undefined into
 // msgpu/libmsgpu_hostsan.so.  The device entry points are stubs that fail with
 // MSG_E_DEVICE, so the ctypes binding (_lib.py) loads this library unchanged
@@ -16,6 +17,7 @@
 #include "nprng.h"
 #include "plan.h"
 #include "host_pool.h"
+#include "digest.h"
 #include "../../include/msgpu.h"
 
 namespace {
@@ -37,6 +39,7 @@ int64_t msg_sizeof(int32_t which) {
         case 0: return (int64_t)sizeof(msg_preset);
         case 1: return (int64_t)sizeof(msg_event);
         case 2: return (int64_t)sizeof(msg_plan_info);
+        case 3: return (int64_t)sizeof(msg_digest_rec);
         default: return -1;
     }
 }
@@ -63,6 +66,18 @@ int msg_fir(msg_ctx*, const float*, float*, int64_t, int32_t, const double*, int
 int msg_stft_mag_db(msg_ctx*, const void*, int32_t, int64_t, int32_t, int32_t, int32_t, int32_t, double*, int32_t*,
                     void*) {
     return no_device();
+}
+int msg_digest(msg_ctx*, const float*, const int64_t*, const int64_t*, int32_t, msg_digest_rec*, void*) {
+    return no_device();
+}
+// the digest's host reference (digest.h), the same code the product library runs
+int msg_digest_host(const float* x, int64_t out_n, msg_digest_rec* rec) {
+    if (!rec || out_n < 0 || (out_n > 0 && !x)) return fail(nullptr, MSG_E_ARG, "bad arguments");
+    static_assert(sizeof(DigestPart) == sizeof(msg_digest_rec), "DigestPart is msg_digest_rec");
+    DigestPart r;
+    dg_host(x, out_n, &r);
+    std::memcpy(rec, &r, sizeof(r));
+    return MSG_OK;
 }
 #include "host_abi.inc"
 }  // extern "C"

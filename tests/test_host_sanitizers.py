@@ -2,12 +2,14 @@
 
 The render plan (csrc/plan.h) and the NumPy stream primitives (csrc/nprng.h)
 run on the host in every batch (msg_render_batch plans on a host thread pool)
-and on the device.  csrc/host_san.cpp compiles their host entry points
-(csrc/host_abi.inc, the same source the product library includes) with
-``g++ -fsanitize=address,undefined -fno-sanitize-recover=undefined`` into a
-host-only library, and this test runs tests/test_plan_host.py and
-tests/test_rng_host.py against it in a child interpreter with the sanitizer
-runtimes preloaded.  Any ASan report or UBSan runtime error fails the run.
+and on the device; the render digest's host reference (csrc/digest.h) is the
+check of msg_digest.  csrc/host_san.cpp compiles their host entry points
+(csrc/host_abi.inc and digest.h, the same sources the product library
+includes) with ``g++ -fsanitize=address,undefined -fno-sanitize-recover=undefined``
+into a host-only library, and this test runs tests/test_plan_host.py,
+tests/test_rng_host.py and the host tests of tests/test_digest.py against it in
+a child interpreter with the sanitizer runtimes preloaded.  Any ASan report or
+UBSan runtime error fails the run.
 """
 import os
 import shutil
@@ -38,7 +40,9 @@ def test_plan_and_rng_under_asan_ubsan(tmp_path):
                ASAN_OPTIONS="detect_leaks=0:abort_on_error=1", UBSAN_OPTIONS="print_stacktrace=1:halt_on_error=1",
                PYTHONDONTWRITEBYTECODE="1")
     r = subprocess.run([sys.executable, "-m", "pytest", "-q", "-x", "-p", "no:cacheprovider",
-                        os.path.join(REPO, "tests", "test_plan_host.py"), os.path.join(REPO, "tests", "test_rng_host.py")],
+                        os.path.join(REPO, "tests", "test_plan_host.py"), os.path.join(REPO, "tests", "test_rng_host.py"),
+                        os.path.join(REPO, "tests", "test_digest.py") + "::test_host_digest_matches_definition",
+                        os.path.join(REPO, "tests", "test_digest.py") + "::test_digest_sees_bits_and_positions"],
                        capture_output=True, text=True, env=env, cwd=REPO, timeout=900)
     out = r.stdout + r.stderr
     assert r.returncode == 0, out[-4000:]
