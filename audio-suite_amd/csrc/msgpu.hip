@@ -1597,9 +1597,10 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
             choose_fir(f.M, info[p].out_n, f.N, f.P, f.Q, ctx->fir8, fir4s_ok ? &f.stream : nullptr, fir4s_k,
                        h_taps(p, true));
         const double w = std::min(std::max(presets[p].stereo_width, 0.0), 1.0);
-        for (int m = -12; m <= 12; ++m) {
-            const double j = bessel_j(std::abs(m), w * 0.9);
-            f.bess[m + 12] = (float)((m < 0 && (m & 1)) ? -j : j);
+        for (int m = 0; m <= 12; ++m) {                // J_{-m} = (-1)^m J_m: one series per |m|
+            const double j = bessel_j(m, w * 0.9);
+            f.bess[m + 12] = (float)j;
+            f.bess[12 - m] = (float)((m & 1) ? -j : j);
         }
     });
     // The overlap-add inside k_fir8p, decided for the batch as a whole: all of its
