@@ -2,11 +2,14 @@
 // kernel (spec3.h) for the 30 MHz hot length.
 #include "spec3.h"
 #include "launch.h"
+#include <algorithm>
 #include <cstdlib>
 #include <cmath>
 
 void spec3_init_attrs() {
     (void)hipFuncSetAttribute((const void*)k_spec3<Spec3P18750>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              Spec3P18750::LDS_BYTES);
+    (void)hipFuncSetAttribute((const void*)k_spec3p<Spec3P18750>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               Spec3P18750::LDS_BYTES);
 }
 
@@ -42,8 +45,14 @@ bool spec3_eligible(int n, int ops, int gen_sr, double cutoff_gen, double roll, 
 
 hipError_t launch_spec3(unsigned grid, hipStream_t s, const msg_event* events, const EventRt* ert, const PresetRt* rt,
                         const float2* tables, const int32_t* ev_list, int n_list, const float* micro_pool,
-                        float* grain_pool) {
+                        float* grain_pool, int persist, int32_t* ctr) {
     using P = Spec3P18750;
+    if (persist > 0 && ctr) {
+        grid = (unsigned)std::max(1, std::min(persist, n_list));
+        hipLaunchKernelGGL((k_spec3p<P>), dim3(grid), dim3(P::T), P::LDS_BYTES, s, events, ert, rt, tables, ev_list,
+                           n_list, micro_pool, grain_pool, ctr);
+        return hipGetLastError();
+    }
     grid = (unsigned)((n_list + MSG_S3_EVENTS - 1) / MSG_S3_EVENTS);   // MSG_S3_EVENTS per workgroup (spec3.h)
     hipLaunchKernelGGL((k_spec3<P>), dim3(grid), dim3(P::T), P::LDS_BYTES, s, events, ert, rt, tables, ev_list,
                        n_list, micro_pool, grain_pool);

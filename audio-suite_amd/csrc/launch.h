@@ -34,9 +34,11 @@ void spec3_init_attrs();
 bool spec3_tables(std::vector<float>& out);
 bool spec3_eligible(int n, int ops, int gen_sr, double cutoff_gen, double roll, double stretch, int64_t float_off,
                     int32_t* kb, int32_t* kz, int32_t* ky, double* inv_f, int32_t* exact32);
+// persist > 0: k_spec3p on that many workgroups (one per CU) with the per-XCD
+// event counters ctr ((MSG_XCDS + 1) x S3P_CTR int32, zero; left zero)
 hipError_t launch_spec3(unsigned grid, hipStream_t s, const msg_event* events, const EventRt* ert, const PresetRt* rt,
                         const float2* tables, const int32_t* ev_list, int n_list, const float* micro_pool,
-                        float* grain_pool);
+                        float* grain_pool, int persist = 0, int32_t* ctr = nullptr);
 
 void fir_init_attrs();
 // the float64 space FIR of heavily saturated renders (kernels_fir64.h): flag, h, H_q, blocks

@@ -223,6 +223,10 @@ struct msg_ctx {
     int n_cu = 256;              // compute units (persistent grids)
     int fir8p_cus = 0;           // persistent FIR workgroups (MSGPU_FIR8P_CUS, A/B; 0: one per CU)
     int fir8p_stagger = 0;       // k_fir8p: every other workgroup starts this many 10-ns ticks later (MSGPU_FIR8P_STAGGER)
+    // k_spec3 events (MSGPU_SPEC3P): 0 two per workgroup (the chain), 1 persistent
+    // workgroups, one per CU, events from per-XCD counters (k_spec3p); > 1: that
+    // many persistent workgroups (A/B)
+    int spec3p = 0;
     // overlap-add inside k_fir8p's loads (PresetRt::ola_fir) for batches whose k_fir8p
     // presets' grains total at most ola_fir_density x their frames (MSGPU_OLA_FIR=0: never)
     bool ola_fir = true;
@@ -292,6 +296,7 @@ struct msg_ctx {
     DevBuf<uint32_t> st_ready;
     DevBuf<double> st_part;
     DevBuf<int32_t> fir8_ctr;           // k_fir8p's per-XCD block counters
+    DevBuf<int32_t> spec3_ctr;          // k_spec3p's per-XCD event counters
     DevBuf<float> f64_h;
     DevBuf<double2> f64_hs;
     // float64 grain chain (kernels_grain64.h)
@@ -659,6 +664,14 @@ static hipError_t fir8_counters(msg_ctx* ctx, hipStream_t s) {
     return hipMemsetAsync(ctx->fir8_ctr.p, 0, sizeof(int32_t) * ctx->fir8_ctr.cap, s);
 }
 
+// k_spec3p's per-XCD event counters: zeroed once; every launch leaves them zero
+static hipError_t spec3_counters(msg_ctx* ctx, hipStream_t s) {
+    if (ctx->spec3_ctr.p) return hipSuccess;
+    const hipError_t e = ctx->spec3_ctr.ensure((size_t)(MSG_XCDS + 1) * S3P_CTR);
+    if (e != hipSuccess) return e;
+    return hipMemsetAsync(ctx->spec3_ctr.p, 0, sizeof(int32_t) * ctx->spec3_ctr.cap, s);
+}
+
 // Wait for the context's last batch (not the whole device: other contexts'
 // streams keep running).
 static hipError_t wait_last(msg_ctx* ctx) {
@@ -753,6 +766,7 @@ msg_ctx* msg_create(int device_ordinal) {
     if (const char* e = getenv("MSGPU_FIR8Q")) ctx->fir8q = e[0] != '0';
     if (const char* e = getenv("MSGPU_FIR8P_CUS")) ctx->fir8p_cus = std::max(0, atoi(e));
     if (const char* e = getenv("MSGPU_FIR8P_STAGGER")) ctx->fir8p_stagger = std::max(0, atoi(e));
+    if (const char* e = getenv("MSGPU_SPEC3P")) ctx->spec3p = atoi(e);
     if (const char* e = getenv("MSGPU_OLA_FIR")) ctx->ola_fir = e[0] != '0';
     if (const char* e = getenv("MSGPU_H_EARLY")) ctx->h_early = atoi(e);
     if (const char* e = getenv("MSGPU_ER_DEV")) ctx->er_dev = e[0] != '0';
@@ -834,6 +848,7 @@ void msg_destroy(msg_ctx* ctx) {
     ctx->mono_a.release(); ctx->mono_y.release(); ctx->hspec.release();
     ctx->hscratch.release(); ctx->maxbits.release();
     ctx->f64_stats.release(); ctx->f64_flag.release(); ctx->st_done.release(); ctx->st_ctr.release();
+    ctx->fir8_ctr.release(); ctx->spec3_ctr.release();
     ctx->st_ready.release(); ctx->st_part.release(); ctx->f64_slot_preset.release(); ctx->f64_nslots.release();
     ctx->f64_h.release(); ctx->f64_hs.release();
     for (void* p : ctx->plans64.allocs) hipFree(p);
@@ -2198,9 +2213,13 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
     HIPCHK(ctx, hipGetLastError());
     // ---- spectral chain ----
     stage_mark(ctx, 3, s);
-    if (!spec3.empty())
+    if (!spec3.empty()) {
+        if (ctx->spec3p > 0) HIPCHK(ctx, spec3_counters(ctx, s));
         HIPCHK(ctx, launch_spec3((unsigned)spec3.size(), s, ctx->events.p, ctx->ert.p, ctx->prt.p, ctx->d_spec3_tab,
-                                 ctx->spec3_list.p, (int)spec3.size(), ctx->micro.p, ctx->grain.p));
+                                 ctx->spec3_list.p, (int)spec3.size(), ctx->micro.p, ctx->grain.p,
+                                 ctx->spec3p > 1 ? ctx->spec3p : (ctx->spec3p > 0 ? ctx->n_cu : 0),
+                                 ctx->spec3_ctr.p));
+    }
     for (int i = 0; i < SPEC_CT_PLANS; ++i)
         if (ct_off[i + 1] > ct_off[i])
             HIPCHK(ctx, launch_spectral_ct(i, (unsigned)(ct_off[i + 1] - ct_off[i]), s, ctx->events.p, ctx->ert.p,

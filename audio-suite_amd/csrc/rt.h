@@ -166,6 +166,7 @@ constexpr int ST_TILE = MSG_ST_TILE;
 // takes one contiguous range of jobs: the shared lines then stay in one L2.
 constexpr int MSG_XCDS = 8;
 constexpr int FIR8P_CTR = 32;   // int32 stride of k_fir8p's per-XCD block counters (128 B apart)
+constexpr int S3P_CTR = 32;     // int32 stride of k_spec3p's per-XCD event counters (128 B apart)
 __device__ __forceinline__ int xcd_block(int b, int grid) {
     const int x = b % MSG_XCDS, i = b / MSG_XCDS;
     const int per = grid / MSG_XCDS, rem = grid % MSG_XCDS;

@@ -350,7 +350,10 @@ MSG_DEV void s3_rest(float2* buf, const float2* tab, const EventRt* __restrict__
                     const int r = (i - j) / P::NB1;
                     const float2 wr = make_float2((float)__builtin_cos(3.14159265358979323846 * r * P::NB1 / M),
                                                   (float)-__builtin_sin(3.14159265358979323846 * r * P::NB1 / M));
-                    const float2 wh = r == 0 ? wjh : cmul(wjh, wr);         // w_i / 2
+                    // wr in an SGPR pair (cmul_k: the same two packed instructions): as a
+                    // VGPR operand the 24 constant pairs are hoisted out of k_spec3p's
+                    // event loop and spilled
+                    const float2 wh = r == 0 ? wjh : cmul_k(wjh, wr);       // w_i / 2
                     const float2 o1 = cmulc(a, wh);                          // a conj(w_i) / 2
                     // mirror term with w_{M-i} = -conj(w_i): -(b . w_i) / 2
                     const float2 p2 = cmul(b, wh);
@@ -510,6 +513,74 @@ k_spec3(const msg_event* __restrict__ events, const EventRt* __restrict__ ert, c
     s3_load<P>(events, rt, ev_list, li, micro_pool, v);
     tc.put(tab);
     s3_chain<P, MSG_S3_EVENTS>(buf, tab, events, ert, rt, ev_list, n_list, micro_pool, grain_pool, li, v);
+}
+
+// Persistent form (MSGPU_SPEC3P=1; VERDICT r05 item 2a, the k_fir8p recipe):
+// one workgroup per CU for the whole launch stages the tables once and loops
+// over events taken from per-XCD counters (XCD x takes events x, x + 8, ...,
+// then helps the other XCDs); every event's grain is loaded into registers
+// while the previous event runs (the two-event chain above leaves each
+// workgroup's first load exposed).  Events are independent, so which
+// workgroup runs which one does not change a bit of the output.
+// ctr: (MSG_XCDS + 1) x S3P_CTR int32, zero before the launch; the last
+// workgroup to finish zeroes it again.
+template <class P>
+__global__ void __launch_bounds__(P::T)
+k_spec3p(const msg_event* __restrict__ events, const EventRt* __restrict__ ert, const PresetRt* __restrict__ rt,
+         const float2* __restrict__ tables, const int32_t* __restrict__ ev_list, int n_list,
+         const float* __restrict__ micro_pool, float* __restrict__ grain_pool, int32_t* __restrict__ ctr) {
+    constexpr int T = P::T;
+    extern __shared__ __attribute__((aligned(16))) float2 lds[];
+    __shared__ int s_take[2];
+    float2* tab = lds;
+    float2* buf = lds + P::TAB;
+    const int x0 = (int)(blockIdx.x % MSG_XCDS);
+    int k = 0;                                      // thread 0: counters exhausted so far
+    auto take = [&]() -> int {                      // thread 0 only; -1 when every counter is done
+        while (k < MSG_XCDS) {
+            const int x = (x0 + k) % MSG_XCDS;
+            const int li = atomicAdd(ctr + x * S3P_CTR, 1) * MSG_XCDS + x;
+            if (li < n_list) return li;
+            ++k;
+        }
+        return -1;
+    };
+    TabCopy<P::TAB_USED, T> tc;
+    tc.fetch(tables);
+    if (threadIdx.x == 0) s_take[0] = take();
+    __syncthreads();
+    int cur = s_take[0];
+    float2 v[P::R1];
+    if (cur >= 0) s3_load<P>(events, rt, ev_list, cur, micro_pool, v);
+    tc.put(tab);
+    if (threadIdx.x == 0 && cur >= 0) s_take[1] = take();   // read after the first pass 1's barrier
+    int par = 1;
+    while (cur >= 0) {                              // uniform
+        s3_first<P>(buf, v);
+        __syncthreads();
+        const int nxt = s_take[par];
+        float2 pre[P::R1];
+        if (nxt >= 0) {
+            s3_load<P>(events, rt, ev_list, nxt, micro_pool, pre);   // in flight through event cur
+            // the event after next: s_take[par ^ 1] was last read before this
+            // iteration's barriers, and is read again after the next pass 1's
+            if (threadIdx.x == 0) s_take[par ^ 1] = take();
+        }
+        const msg_event& e = events[ev_list[cur]];
+        const int64_t off = rt[e.preset].pool_base + e.pool_off;
+        s3_rest<P>(buf, tab, ert, ev_list[cur], off, grain_pool);
+        if (nxt < 0) break;
+        __syncthreads();                            // exchange B read before the next pass 1 writes
+        cur = nxt;
+#pragma unroll
+        for (int r = 0; r < P::R1; ++r) v[r] = pre[r];
+        par ^= 1;
+    }
+    // every take of this workgroup has returned (thread 0 made them in order)
+    if (threadIdx.x == 0 && atomicAdd(ctr + MSG_XCDS * S3P_CTR, 1) == (int)gridDim.x - 1) {
+        for (int x = 0; x < MSG_XCDS; ++x) ctr[x * S3P_CTR] = 0;
+        ctr[MSG_XCDS * S3P_CTR] = 0;
+    }
 }
 
 // Host: twiddle tables (float64-built, rounded once).

@@ -278,6 +278,24 @@ def test_fir8_persistent_bit_identical(msgpu, irs, full_renders):
     assert rms(outs["1"][:int(packed.out_n[0])], full_renders["C3_audio"]) <= RMS_TOL
 
 
+def test_spec3_persistent_bit_identical(msgpu, irs, full_renders):
+    """k_spec3's persistent form (MSGPU_SPEC3P=1: one workgroup per CU taking
+    events from per-XCD counters, each next grain loaded during the current
+    event) runs every event with the two-event chain's arithmetic (=0): the
+    outputs are bit-identical on C3 (narrow band), C4 (wide band), a batch of
+    fewer events than CUs and one whose event count is not a multiple of the
+    XCD count; C3 still matches the reference render."""
+    params = [msgpu.config_params("C3", seed=1000 + s, irs=irs) for s in range(3)]
+    params += [msgpu.config_params("C4", seed=1000, irs=irs), msgpu.merged(out_dur_s=0.2, seed=5)]
+    outs = {m: _render_env(params, {"MSGPU_SPEC3P": m})[1] for m in ("0", "1")}
+    assert np.array_equal(outs["0"], outs["1"])
+    few = [msgpu.config_params("C3", seed=3000, irs=irs, out_dur_s=0.2)]      # a handful of events
+    fo = {m: _render_env(few, {"MSGPU_SPEC3P": m})[1] for m in ("0", "1")}
+    assert np.array_equal(fo["0"], fo["1"])
+    packed, _ = _render_env(params[:1], {})
+    assert rms(outs["1"][:int(packed.out_n[0])], full_renders["C3_audio"]) <= RMS_TOL
+
+
 def test_fir64_serves_every_flagged_preset(msgpu, irs):
     """the float64 FIR had 128 slots per batch and left flagged
     presets beyond them on float32, so a preset's output depended on the batch

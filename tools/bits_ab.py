@@ -7,9 +7,11 @@ batch in its own process (MSGPU_LIB selects the build; the ctypes binding loads
 one library per process); the outputs are compared here.
 
     python tools/bits_ab.py audio-suite_amd/msgpu/libmsgpu_base.so [other.so]
+    python tools/bits_ab.py 'lib.so,MSGPU_X=0' 'lib.so,MSGPU_X=1'
 
-The second library defaults to the product build.  Prints one JSON line and
-exits non-zero when any preset differs.
+The second library defaults to the product build.  A side may add KEY=VALUE
+settings after commas (the same library under two settings).  Prints one JSON
+line and exits non-zero when any preset differs.
 """
 import json
 import os
@@ -62,22 +64,26 @@ def child(out):
 def main():
     if len(sys.argv) > 1 and sys.argv[1] == "--child":
         return child(sys.argv[2])
-    libs = [os.path.abspath(sys.argv[1]),
-            os.path.abspath(sys.argv[2]) if len(sys.argv) > 2 else os.path.join(REPO, "audio-suite_amd", "msgpu",
-                                                                                 "libmsgpu.so")]
+    sides = [sys.argv[1], sys.argv[2] if len(sys.argv) > 2 else os.path.join(REPO, "audio-suite_amd", "msgpu",
+                                                                           "libmsgpu.so")]
+    libs, envs = [], []
+    for side in sides:
+        lib, *kv = side.split(",")
+        libs.append(os.path.abspath(lib))
+        envs.append(dict(x.split("=", 1) for x in kv))
     tmp = tempfile.mkdtemp()
     res = []
     for k, lib in enumerate(libs):
         f = os.path.join(tmp, f"{k}.npz")
         subprocess.check_call([sys.executable, os.path.abspath(__file__), "--child", f],
-                              env=dict(os.environ, MSGPU_LIB=lib))
+                              env=dict(os.environ, MSGPU_LIB=lib, **envs[k]))
         res.append(np.load(f))
     a, b = res[0]["out"], res[1]["out"]
     diff = []
     for i, (o, n) in enumerate(zip(res[0]["offsets"], res[0]["out_n"])):
         if not np.array_equal(a[o:o + n], b[o:o + n]):
             diff.append(i)
-    print(json.dumps({"libs": libs, "presets": len(res[0]["out_n"]), "frames": int(res[0]["out_n"].sum()),
+    print(json.dumps({"libs": libs, "envs": envs, "presets": len(res[0]["out_n"]), "frames": int(res[0]["out_n"].sum()),
                       "differing_presets": diff, "identical": not diff}), flush=True)
     sys.exit(0 if not diff else 1)
 
