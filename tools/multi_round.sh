@@ -9,9 +9,9 @@ mkdir -p gpurun_out
 timeout -k 10 300 python -u tools/multi_rehearsal.py 2 > gpurun_out/${tag}_pool.json 2> gpurun_out/${tag}_pool.log || exit $?
 cat gpurun_out/${tag}_pool.json
 timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
-  --master-port 29533 bench.py --gpus 2 --steps 20 --warmup 3 --no-cpu --points= --iso-steps 0 \
+  --master-port 29533 bench.py --gpus 2 --steps 20 --warmup 3 --no-cpu --points= --fir-points= --iso-steps 0 \
   --from-dicts-steps 0 --rehearse-one-gpu > gpurun_out/${tag}_tdr.json 2> gpurun_out/${tag}_tdr.log || exit $?
-timeout -k 10 400 python bench.py --gpus 2 --steps 20 --warmup 3 --no-cpu --points= --iso-steps 0 \
+timeout -k 10 400 python bench.py --gpus 2 --steps 20 --warmup 3 --no-cpu --points= --fir-points= --iso-steps 0 \
   --from-dicts-steps 0 --rehearse-one-gpu > gpurun_out/${tag}_self.json 2> gpurun_out/${tag}_self.log || exit $?
 python3 - gpurun_out/${tag}_tdr.json gpurun_out/${tag}_self.json <<'PY'
 import json, sys
