@@ -82,7 +82,12 @@ CONFIG_SUB = {"C5": 171}   # six sub-batches, two per stream (C5 ungated: 126.8 
 # host-bound short-step points: at ~2 ms per step, 10 steps (20 ms) swung by +-40 % between
 # back-to-back runs on a shared-host box (profiles/r03an_h48_sweep.txt); time at least 50
 POINT_STEPS_MIN = {"H48": 50, "C4": 30}
-GATE_OFF = {"C5"}   # configs whose points run ungated (measured slower with --gate 2,4)
+# configs that run ungated under the default gate (measured slower with 2,4): C5, and
+# H48, whose step is a per-stream chain of small kernels the gate serialises across
+# the streams (1.06-1.24 vs 1.26-1.60 ms per step in five alternating pairs,
+# profiles/r06g2_gate_points.txt; C4 within noise either way, so it keeps the gate)
+GATE_OFF = {"C5", "H48"}
+DEFAULT_GATE = "2,4"
 WORKLOAD = {
     "C1": "C1: 48 kHz out, no band limit, unfold x1, stretch x1, Single event, 1 s, ER 320 taps, stereo",
     "C2": "C2: 192 kHz out, unfold x10 (1.92 MHz design SR), stretch x1, Poisson 18/s, 1 s, 4096-tap IR, "
@@ -738,7 +743,7 @@ def parse():
     ap.add_argument("--streams", type=int, default=3,
                     help="in-flight sub-batches (contexts/streams) per GPU (C3 with the 2,4 gate: 3 streams "
                          "9.35-9.38 ms vs 2 streams 9.45 ms per step, profiles/r02zh_streams.txt)")
-    ap.add_argument("--gate", default="2,4",
+    ap.add_argument("--gate", default=DEFAULT_GATE,
                     help="WAIT,RECORD stages of msg_gate between the streams' contexts, or none.  Default 2,4: a "
                          "sub-batch's generator waits until the previous sub-batch's overlap-add begins, so it "
                          "runs beside that sub-batch's FIR and stereo passes rather than its spectral kernel "
@@ -844,8 +849,9 @@ def main():
         with open(os.path.join(REPO, "tests", "golden", "golden_extra.json")) as f:
             golden.update(json.load(f)["summaries"])          # H48_1000..1003 (tools/gen_golden_r3.py)
         gate = None if args.gate in ("", "none") else tuple(int(v) for v in args.gate.split(","))
+        head_gate = None if (cfg in GATE_OFF and args.gate == DEFAULT_GATE) else gate
         device = 0 if args.rehearse_one_gpu else local
-        runner = GpuRunner(device, max(1, args.streams), gate, threaded=args.enqueue == "threads")
+        runner = GpuRunner(device, max(1, args.streams), head_gate, threaded=args.enqueue == "threads")
         head = measure(runner, cfg, seeds, default_sub(cfg, args, batch), args.steps, args.warmup, comm, irs,
                        golden, iso_steps=args.iso_steps, from_dicts_steps=args.from_dicts_steps)
         points = {}
@@ -857,6 +863,8 @@ def main():
             points[pc] = measure(runner, pc, rank_seeds(rank, pb), default_sub(pc, args, pb), psteps, 3, comm,
                                  irs, golden, iso_steps=args.iso_steps,
                                  from_dicts_steps=psteps if (pc == "H48" and args.from_dicts_steps) else 0)
+            if points[pc] is not None:
+                points[pc]["stream_gate"] = "none" if (pc in GATE_OFF or gate is None) else ",".join(map(str, gate))
         for M in [int(t) for t in args.fir_points.split(",") if t]:
             points[f"FIR{M // 1024}K"] = measure_fir(runner, M, max(args.point_steps, 20), comm, rank,
                                                      cpu=(rank == 0 and not args.no_cpu))
@@ -882,7 +890,7 @@ def main():
                            "parallelism": f"preset-sharded x{world}" + (
                                " (rehearsal: every rank on device 0)" if args.rehearse_one_gpu else ""),
                            "streams_per_gpu": len(runner.engs),
-                           "stream_gate": args.gate, "enqueue": args.enqueue},
+                           "stream_gate": ",".join(map(str, head_gate)) if head_gate else "none", "enqueue": args.enqueue},
                 "roofline": head["roofline"], "roofline_isolated": head.get("roofline_isolated"),
                 "stage_ms": head["stage_ms"], "stage_algorithmic_GBs": head["stage_algorithmic_GBs"],
                 "design_msamples_per_s": head["design_msamples_per_s"],
