@@ -536,14 +536,23 @@ MSG_DEV void stereo_out_tile(const PresetRt& r, int tile, const float* __restric
         if (j >= pairs) break;
         const int f0 = 2 * j - a;
         if (f0 >= 0 && f0 + 1 < st.cnt) {
-            const float2 p0 = *reinterpret_cast<const float2*>(sm + 2 * f0);
-            const float2 p1 = *reinterpret_cast<const float2*>(sm + 2 * f0 + 2);
+            // a == 0 (even output offsets: every C3 / C4 / C5 preset): the pair is one
+            // aligned 16-byte read (two 8-byte reads at a 16-byte lane stride hit each
+            // bank twice per 32-lane group)
+            float4 pp;
+            if (a == 0) {
+                pp = *reinterpret_cast<const float4*>(sm + 2 * f0);
+            } else {
+                const float2 p0 = *reinterpret_cast<const float2*>(sm + 2 * f0);
+                const float2 p1 = *reinterpret_cast<const float2*>(sm + 2 * f0 + 2);
+                pp = make_float4(p0.x, p0.y, p1.x, p1.y);
+            }
             float* dst = ob + 4 * (uint32_t)j;
 #if MSG_ST_NT
             typedef float v4f __attribute__((ext_vector_type(4)));
-            __builtin_nontemporal_store(v4f{p0.x, p0.y, p1.x, p1.y}, reinterpret_cast<v4f*>(dst));
+            __builtin_nontemporal_store(v4f{pp.x, pp.y, pp.z, pp.w}, reinterpret_cast<v4f*>(dst));
 #else
-            *reinterpret_cast<float4*>(dst) = make_float4(p0.x, p0.y, p1.x, p1.y);
+            *reinterpret_cast<float4*>(dst) = pp;
 #endif
         } else {
 #pragma unroll
