@@ -193,6 +193,13 @@ struct msg_ctx {
     bool pending_fir[2] = {false, false};
     bool pending_h_early[2] = {false, false};
     int ev_cur = 0;
+    // msg_set_profiling(ctx, k): batches 0, k, 2k, ... of the context record the
+    // stage events and host clocks (k = 1: every batch).  Each profiled batch
+    // adds 12 timed events to its stream and a host read of the set two batches
+    // back (bench.py samples every 4th batch)
+    int prof_every = 1;
+    int64_t prof_n = 0;
+    bool prof_batch = false;      // this batch records (profiling && its turn)
     double stage_sum[10] = {0};   // accumulated stage times since msg_set_profiling(ctx, 1)
     int64_t stage_cnt = 0;
     // host wall clock per batch: plan, records, pinned upload, then the splits
@@ -625,7 +632,7 @@ static void stage_mark(msg_ctx* ctx, int i, hipStream_t s) {
             }
         }
     }
-    if (ctx->profiling) hipEventRecord(ctx->ev[ctx->ev_cur][i], s);
+    if (ctx->prof_batch) hipEventRecord(ctx->ev[ctx->ev_cur][i], s);
 }
 
 // A batch on a different stream than the context's last one waits for that
@@ -893,6 +900,8 @@ int msg_set_profiling(msg_ctx* ctx, int32_t on) {
     if (!ctx) return MSG_E_ARG;
     collect_stage_times(ctx);
     ctx->profiling = on != 0;
+    ctx->prof_every = on > 1 ? on : 1;
+    ctx->prof_n = 0;
     if (ctx->profiling) {
         for (double& v : ctx->stage_sum) v = 0.0;
         for (double& v : ctx->host_sum) v = 0.0;
@@ -1307,6 +1316,7 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
         const int ic = presets[p].ir_conv;
         if (ic >= n_irs || (ic >= 0 && !irs)) return fail(ctx, MSG_E_ARG, "bad IR index");
     }
+    ctx->prof_batch = ctx->profiling && (ctx->prof_n++ % ctx->prof_every) == 0;
     stage_mark(ctx, 0, s);
     using hclock = std::chrono::steady_clock;
     const auto h0 = hclock::now();
@@ -2142,7 +2152,7 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
         HIPCHK(ctx, ctx->er_tap_d.ensure((size_t)std::max<int64_t>(1, ntaps)));
         erg = ctx->er_gain_d.p;
     }
-    if (ctx->profiling) {
+    if (ctx->prof_batch) {
         const auto h3 = hclock::now();
         ctx->host_sum[0] += std::chrono::duration<double, std::milli>(h1 - h0).count();
         ctx->host_sum[1] += std::chrono::duration<double, std::milli>(h2 - h1).count();
@@ -2417,7 +2427,7 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
     ctx->h_ev64 = ev64;
     ctx->h_last64 = last64;
     ctx->last_n = P;
-    if (ctx->profiling) {
+    if (ctx->prof_batch) {
         ctx->pending[ctx->ev_cur] = true;
         ctx->pending_fir[ctx->ev_cur] = hblocks > 0;
         ctx->pending_h_early[ctx->ev_cur] = h_early;

@@ -51,8 +51,10 @@ class Engine:
             pass
 
     # ------------------------------------------------------------------
-    def set_profiling(self, on: bool):
-        L.check(L.lib().msg_set_profiling(self._ctx, 1 if on else 0), self._ctx)
+    def set_profiling(self, on):
+        """False / 0 off, True / 1 every batch, k > 1 every k-th batch of this context."""
+        k = 0 if not on else max(1, int(on))
+        L.check(L.lib().msg_set_profiling(self._ctx, k), self._ctx)
 
     def gate(self, peer, wait_stage: int = 2, record_stage: int = 6):
         """Order this context's batches against ``peer``'s (msg_gate): stage

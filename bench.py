@@ -82,6 +82,13 @@ CONFIG_SUB = {"C5": 171}   # six sub-batches, two per stream (C5 ungated: 126.8 
 # host-bound short-step points: at ~2 ms per step, 10 steps (20 ms) swung by +-40 % between
 # back-to-back runs on a shared-host box (profiles/r03an_h48_sweep.txt); time at least 50
 POINT_STEPS_MIN = {"H48": 50, "C4": 30}
+# stage events (msg_set_profiling) on every PROFILE_EVERY-th batch of a context
+# inside the timed region, so that most batches run without the 12 timed events
+# and the host read of the set: on H48's short step, in one session a run with
+# every batch profiled took 1.02 - 1.18 ms against 0.81 - 0.87 for three
+# unprofiled runs after it, but alternating A/Bs on other boxes stayed inside
+# their +-30 % noise (profiles/r06pe_profile_sampling.txt)
+PROFILE_EVERY = int(os.environ.get("MSGPU_BENCH_PROFILE_EVERY", "4"))   # the env: A/B only (0: no events)
 # configs that run ungated under the default gate (measured slower with 2,4): C5, and
 # H48, whose step is a per-stream chain of small kernels the gate serialises across
 # the streams (1.06-1.24 vs 1.26-1.60 ms per step in five alternating pairs,
@@ -493,7 +500,7 @@ def measure(runner, cfg, seeds, sub, steps, warmup, comm, irs, golden, iso_steps
     for _ in range(max(1, warmup)):
         runner.step(w)
     runner.sync()
-    runner.profiling(True)
+    runner.profiling(PROFILE_EVERY)
     mine, elapsed = timed(runner, w, steps, 0, comm)
     runner.profiling(False)
     stages = {n: round(float(v), 4) for n, v in zip(STAGE_NAMES, runner.stage_ms())}
@@ -504,7 +511,7 @@ def measure(runner, cfg, seeds, sub, steps, warmup, comm, irs, golden, iso_steps
     sb_launch = {k: v / nsub for k, v in sb.items()}
     longest = max(KERNEL_STAGES, key=lambda k: stages[k])
     dom = DOMINANT_STAGE.get(cfg, longest)
-    achieved = sb_launch[dom] / (stages[dom] * 1e-3) / 1e9
+    achieved = sb_launch[dom] / (stages[dom] * 1e-3) / 1e9 if stages[dom] > 0 else 0.0
     launch_batch = len(seeds) // nsub
     sum_n = sum(int(i.pool_len) for i in infos)
     n_ev = sum(int(i.n_events) for i in infos)
@@ -894,6 +901,7 @@ def main():
                 "roofline": head["roofline"], "roofline_isolated": head.get("roofline_isolated"),
                 "stage_ms": head["stage_ms"], "stage_algorithmic_GBs": head["stage_algorithmic_GBs"],
                 "design_msamples_per_s": head["design_msamples_per_s"],
+                "stage_sampling": f"stage events on batches 0, {PROFILE_EVERY}, {2 * PROFILE_EVERY}, ... of each context",
                 "checked": head["check"],
                 "from_dicts": head.get("from_dicts"),
                 "cpu_baseline": cpu,

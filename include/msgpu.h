@@ -174,7 +174,9 @@ int msg_last_grain64(msg_ctx* ctx, int32_t preset, int32_t k, double* grain, int
  * [13] plan sizes, [14] plan events + ER tap merge, [15] preset records,
  * [16] event records, [17] lists, buffers and staging adds; with n >= 19,
  * [18] the presets per batch whose overlap-add ran inside the FIR kernel.
- * Events are read lazily, so profiling does not block the host.             */
+ * Events are read lazily, so profiling does not block the host.
+ * on = 0 off, 1 every batch, k > 1 batches 0, k, 2k, ... of the context
+ * (the others run without the events).                                       */
 int msg_set_profiling(msg_ctx* ctx, int32_t on);
 int msg_stage_times(msg_ctx* ctx, float* ms, int32_t n);
 
