@@ -2,7 +2,7 @@
 # GPU box: the round-6 A/B and diagnostic sessions, one function each (their
 # records are under profiles/r06*; DESIGN section 9 cites them).
 #   usage (on the box): bash tools/round6_ab.sh NAME [args]
-# NAME: h48_host_diag h48_numa_diag h48_sched gate_points_ab gate_c3_ab h48_streams_ab prof_every_ab prof_every_ab2 h48_warmup_ab sub_sweep s3p_check fir8_cus_stamps
+# NAME: c3_streams c3_streams32 h48_host_diag h48_numa_diag h48_sched gate_points_ab gate_c3_ab h48_streams_ab prof_every_ab prof_every_ab2 h48_warmup_ab sub_sweep s3p_check fir8_cus_stamps
 set -o pipefail
 mkdir -p gpurun_out
 
@@ -222,6 +222,34 @@ fir8_cus_stamps() {
 for c in 256 128 64 16 8; do
   echo "=== $c workgroups"
   MSGPU_FIR8P_CUS=$c MSGPU_LIB=$PWD/audio-suite_amd/msgpu/libmsgpu_firstamps.so timeout -k 10 200 python tools/fir8_stamps.py C3 256 || exit $?
+done
+}
+
+# C3 with 2 / 3 / 4 streams (sub-batches of 512 / 342 / 256), default gate, alternating
+c3_streams() {
+for i in 1 2; do
+  for cfg in "3 342" "2 512" "4 256"; do
+    set -- $cfg
+    timeout -k 10 200 python bench.py --no-cpu --points= --fir-points= --steps 30 --from-dicts-steps 0 --iso-steps 0 \
+      --streams $1 --sub $2 > gpurun_out/r06c3s_$1_$i.json 2> gpurun_out/r06c3s_$1_$i.log || exit $?
+    python3 -c "
+import json; d=json.load(open('gpurun_out/r06c3s_$1_$i.json'))
+print('C3 streams $1 sub $2', $i, d['ms_per_step'], d['checked']['all_ok'])"
+  done
+done
+}
+
+# C3 with 3 vs 2 streams, default gate, four alternating pairs
+c3_streams32() {
+for i in 1 2 3 4; do
+  for cfg in "3 342" "2 512"; do
+    set -- $cfg
+    timeout -k 10 200 python bench.py --no-cpu --points= --fir-points= --steps 40 --from-dicts-steps 0 --iso-steps 0 \
+      --streams $1 --sub $2 > gpurun_out/r06c32_$1_$i.json 2> gpurun_out/r06c32_$1_$i.log || exit $?
+    python3 -c "
+import json; d=json.load(open('gpurun_out/r06c32_$1_$i.json'))
+print('C3 streams $1 sub $2', $i, d['ms_per_step'], d['checked']['all_ok'])"
+  done
 done
 }
 
