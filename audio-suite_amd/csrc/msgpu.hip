@@ -1726,7 +1726,7 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
                     if (it == ir8_spec_of.end()) {
                         it = ir8_spec_of.emplace(pr.ir_conv, ir8_sum).first;
                         ir8_jobs.insert(ir8_jobs.end(), {r.ir_off, (int64_t)r.ir_len, ir8_sum, 0});
-                        ir8_sum += N / 2 + 1;
+                        ir8_sum += (N / 2 + 1 + 15) & ~15;
                     }
                     irs = it->second;
                 }
@@ -1748,7 +1748,7 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
                     if (it == ir4_spec_of.end()) {
                         it = ir4_spec_of.emplace(pr.ir_conv, ir4_sum).first;
                         ir4_jobs.insert(ir4_jobs.end(), {r.ir_off, (int64_t)r.ir_len, ir4_sum, 0});
-                        ir4_sum += N / 2 + 1;
+                        ir4_sum += (N / 2 + 1 + 15) & ~15;
                     }
                     irs = it->second;
                 }
@@ -1785,8 +1785,11 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
             fblocks += nblk;
             hblocks += Q;
             if (!r.h_fir4) hblocks_gen += Q;
+            // each preset's spectra start on a 128-byte boundary (N / 2 + 1 float2 per
+            // partition is odd: unpadded, every other preset's He straddled one more
+            // cache line per wave-wide load)
             if (!((N == FIR8_N || r.h_fir4 == 3) && r.ir_len > 0 && !(pr.flags & MSG_F_ER_CLOUD)))
-                hsum += (int64_t)Q * (N / 2 + 1);
+                hsum += ((int64_t)Q * (N / 2 + 1) + 15) & ~int64_t(15);
         } else {
             h_tile_begin[p] = htiles;
         }
