@@ -57,6 +57,9 @@ __device__ unsigned long long g_fir_stamps[16];
 namespace fir8 {
 using G = Fir4Geo<16384>;
 constexpr int MH = 16384, M = 2 * MH, N = 2 * M;
+// Ho follows He (MH + 1 bins) at a 128-byte-aligned offset: at MH + 1 every
+// wave-wide Ho load straddled one more cache line; a spectrum takes HSTRIDE float2
+constexpr int HO = MH + 16, HSTRIDE = HO + MH;
 constexpr int T = G::T, R1 = G::R1, R2 = G::R2, R3 = G::R3, R4 = G::R4;
 constexpr int NB1 = G::NB1, NB4 = G::NB4;
 static_assert(NB1 == T && NB4 == 2 * T, "fir8 geometry");
@@ -380,7 +383,7 @@ k_fir8(const PresetRt* __restrict__ rt, const int2* __restrict__ jobs, const flo
     dif_split(tab, a, b);
     FIR_STAMP(0);
     const float2* He = hspec + pr.h_off;
-    const float2* Ho = He + (MH + 1);
+    const float2* Ho = He + HO;
     float2 v[2][R4], acc[2][R4], A[R1];
     fwd_half<false>(buf, tab, a, v);
     FIR_STAMP(1);
@@ -504,7 +507,7 @@ k_fir8p(const PresetRt* __restrict__ rt, const int2* __restrict__ jobs, int n_jo
         if (!ola) dif_split(tab, a, b);
         FIR_STAMP(0);
         const float2* He = hspec + pr.h_off;
-        const float2* Ho = He + (MH + 1);
+        const float2* Ho = He + HO;
         float2 v[2][R4], acc[2][R4], A[R1];
         fwd_half<false>(buf, tab, a, v);
         FIR_STAMP(1);
@@ -714,9 +717,9 @@ k_fir8q(const PresetRt* __restrict__ rt, const int2* __restrict__ runs, int n_ru
     { TabCopy<G::TAB_USED, T> tc; tc.fetch(tables); tc.put(tab); }
     constexpr int P = MH * 2;                      // partition length = block length = N / 2
     const float2* He0 = hspec;
-    const float2* Ho0 = He0 + (MH + 1);
-    const float2* He1 = hspec + (2 * MH + 1);
-    const float2* Ho1 = He1 + (MH + 1);
+    const float2* Ho0 = He0 + HO;
+    const float2* He1 = hspec + HSTRIDE;
+    const float2* Ho1 = He1 + HO;
     for (;;) {
         __syncthreads();                          // tables visible; the last run's s_take read
         if (t == 0) s_take = atomicAdd(ctr, 1);
@@ -877,7 +880,7 @@ k_fir8_spec(const int64_t* __restrict__ jobs, const float2* __restrict__ tables,
     } else {
         load_half<true>(tab, src + j[0], j[1], in);
         fwd_half<true>(buf, tab, in, v);
-        store_half<true>(tab, v, nullptr, He + (MH + 1));
+        store_half<true>(tab, v, nullptr, He + HO);
     }
 }
 
@@ -923,6 +926,6 @@ k_fir8_hconv(const PresetRt* __restrict__ rt, const int32_t* __restrict__ list, 
         store_half<false>(tab, v, S, He);
     } else {
         fwd_half<true>(buf, tab, in, v);
-        store_half<true>(tab, v, S ? S + (MH + 1) : nullptr, He + (MH + 1));
+        store_half<true>(tab, v, S ? S + HO : nullptr, He + HO);
     }
 }

@@ -4,6 +4,7 @@
 #include "fir4_fft.h"
 #include "fir8_fft.h"
 #include "launch.h"
+static_assert(fir8::HSTRIDE == FIR8_HSTRIDE, "fir8 spectrum stride: fir8_fft.h and launch.h");
 
 template <int M> static void fir2_attr() {
     (void)hipFuncSetAttribute((const void*)k_fir2<M>, hipFuncAttributeMaxDynamicSharedMemorySize,

@@ -94,6 +94,9 @@ hipError_t launch_fir4_irspec(unsigned n_jobs, hipStream_t s, const int64_t* job
 // ER preset (rfft(delta + taps) . S_IR), k_fir8_spec per job [src off, len, spec off, 0]
 // of float64 (IR bank) or float32 samples.
 constexpr int FIR8_N = 65536;
+// float2 per filter spectrum on the N = 65536 engine: He (N / 4 + 1 bins) then Ho
+// (N / 4) from a 128-byte-aligned offset (fir8::HO), a multiple of 16 float2
+constexpr int FIR8_HSTRIDE = FIR8_N / 4 + 16 + FIR8_N / 4;
 hipError_t launch_fir8(unsigned grid, hipStream_t s, const PresetRt* rt, const int2* jobs, const float2* tables,
                        const float2* hspec, const float* x_in, float* y_out);
 hipError_t launch_fir8p(unsigned n_jobs, unsigned grid, hipStream_t s, const PresetRt* rt, const int2* jobs,

@@ -1065,7 +1065,7 @@ int msg_fir(msg_ctx* ctx, const float* x_dev, float* y_dev, int64_t n, int32_t n
         }
         std::vector<float> hf((size_t)M);
         for (int64_t i = 0; i < M; ++i) hf[i] = (float)h[i];
-        const int64_t K8 = FIR8_N / 2 + 1;
+        const int64_t K8 = FIR8_HSTRIDE;          // float2 per spectrum (fir8_fft.h layout)
         const int64_t job[8] = {0, FIR8Q_P, 0, 0, FIR8Q_P, M - FIR8Q_P, K8, 0};   // H_0, H_1 from the float taps
         const unsigned grid = (unsigned)std::min<int64_t>((int64_t)runs.size(), ctx->n_cu);
         HIPCHK(ctx, ctx->sf_prt.ensure(prt.size()));
@@ -1116,7 +1116,7 @@ int msg_fir(msg_ctx* ctx, const float* x_dev, float* y_dev, int64_t n, int32_t n
         HIPCHK(ctx, ctx->sf_jobs.ensure(fj.size()));
         HIPCHK(ctx, ctx->sf_hf.ensure((size_t)M));
         HIPCHK(ctx, ctx->sf_irjobs.ensure(4));
-        HIPCHK(ctx, ctx->sf_hspec.ensure((size_t)(N / 2 + 1)));
+        HIPCHK(ctx, ctx->sf_hspec.ensure((size_t)FIR8_HSTRIDE));
         HIPCHK(ctx, hipMemcpyAsync(ctx->sf_prt.p, prt.data(), sizeof(PresetRt) * prt.size(), hipMemcpyHostToDevice, s));
         HIPCHK(ctx, hipMemcpyAsync(ctx->sf_jobs.p, fj.data(), sizeof(int2) * fj.size(), hipMemcpyHostToDevice, s));
         HIPCHK(ctx, hipMemcpyAsync(ctx->sf_hf.p, hf.data(), sizeof(float) * (size_t)M, hipMemcpyHostToDevice, s));
@@ -1788,6 +1788,8 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
             // each preset's spectra start on a 128-byte boundary (N / 2 + 1 float2 per
             // partition is odd: unpadded, every other preset's He straddled one more
             // cache line per wave-wide load)
+            // (N = 65536: one spectrum of FIR8_HSTRIDE float2, Ho 128-byte aligned inside it)
+            static_assert(((FIR8_N / 2 + 1 + 15) & ~15) == FIR8_HSTRIDE, "fir8 spectrum stride");
             if (!((N == FIR8_N || r.h_fir4 == 3) && r.ir_len > 0 && !(pr.flags & MSG_F_ER_CLOUD)))
                 hsum += ((int64_t)Q * (N / 2 + 1) + 15) & ~int64_t(15);
         } else {
