@@ -288,7 +288,8 @@ struct msg_ctx {
     Slice<int2> fir_jobs;
     Slice<int32_t> spec_ct_list;
     Slice<double> irbank;
-    DevBuf<unsigned> maxbits;
+    Slice<unsigned> maxbits;            // per preset: k_stereo_max's peak bits, zeroed by the batch's upload
+    std::vector<unsigned> maxbits_zero;
     // float64 space FIR of saturated renders (kernels_fir64.h)
     Slice<Fir64Rt> f64rt;
     Slice<int32_t> st_count, odd_list, odd_cnt;
@@ -853,7 +854,7 @@ void msg_destroy(msg_ctx* ctx) {
     ctx->tap_base.release(); ctx->dp_events.release(); ctx->dp_er_off.release(); ctx->dp_er_gain.release();
     ctx->micro.release(); ctx->grain.release();
     ctx->mono_a.release(); ctx->mono_y.release(); ctx->hspec.release();
-    ctx->hscratch.release(); ctx->maxbits.release();
+    ctx->hscratch.release();
     ctx->f64_stats.release(); ctx->f64_flag.release(); ctx->st_done.release(); ctx->st_ctr.release();
     ctx->fir8_ctr.release(); ctx->spec3_ctr.release();
     ctx->st_ready.release(); ctx->st_part.release(); ctx->f64_slot_preset.release(); ctx->f64_nslots.release();
@@ -2083,7 +2084,6 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
     for (size_t j = 0; j < ir4_jobs.size(); j += 4) ir4_jobs[j + 2] += hsum + ir8_sum;
     HIPCHK(ctx, ctx->hspec.ensure(hsum + ir8_sum + ir4_sum));
     HIPCHK(ctx, ctx->hscratch.ensure(hs_sum));
-    HIPCHK(ctx, ctx->maxbits.ensure(P));
     auto h2d = [&](auto** dst, const auto* src, size_t bytes) -> hipError_t {
         ctx->staging.add(dst, src, bytes);    // copied at the flush below, one copy for all
         return hipSuccess;
@@ -2117,7 +2117,8 @@ int msg_render_batch(msg_ctx* ctx, const msg_preset* presets, int32_t P,
     HIPCHK(ctx, h2d(&ctx->fir4c_list.p, fir4c_list.data(), sizeof(int32_t) * fir4c_list.size()));
     HIPCHK(ctx, h2d(&ctx->ir4_jobs.p, ir4_jobs.data(), sizeof(int64_t) * ir4_jobs.size()));
     HIPCHK(ctx, h2d(&ctx->hpart_jobs.p, hpart_jobs.data(), sizeof(int2) * hpart_jobs.size()));
-    HIPCHK(ctx, hipMemsetAsync(ctx->maxbits.p, 0, sizeof(unsigned) * P, s));
+    if (ctx->maxbits_zero.size() < (size_t)P) ctx->maxbits_zero.assign((size_t)P, 0u);
+    HIPCHK(ctx, h2d(&ctx->maxbits.p, ctx->maxbits_zero.data(), sizeof(unsigned) * P));   // zeros in the one upload, no fill launch
     // the float64 FIR chain: slots for up to FIR64_CAP flagged presets of the batch
     const bool f64_on = ctx->fir64 > 0 && f64_cand > 0;
     const int64_t f64_hstride = (f64_hmax + 3) & ~int64_t(3);
