@@ -2,7 +2,7 @@
 # GPU box: the round-6 A/B and diagnostic sessions, one function each (their
 # records are under profiles/r06*; DESIGN section 9 cites them).
 #   usage (on the box): bash tools/round6_ab.sh NAME [args]
-# NAME: c3_streams c3_streams32 h48_host_diag h48_numa_diag h48_sched gate_points_ab gate_c3_ab h48_streams_ab prof_every_ab prof_every_ab2 h48_warmup_ab sub_sweep s3p_check fir8_cus_stamps
+# NAME: c3_streams c3_streams32 h48_host_diag h48_numa_diag h48_sched gate_points_ab gate_c3_ab h48_streams_ab prof_every_ab prof_every_ab2 h48_warmup_ab sub_sweep s3p_check fir8_cus_stamps ho_check q2nt_ab mb_check
 set -o pipefail
 mkdir -p gpurun_out
 
@@ -251,6 +251,44 @@ import json; d=json.load(open('gpurun_out/r06c32_$1_$i.json'))
 print('C3 streams $1 sub $2', $i, d['ms_per_step'], d['checked']['all_ok'])"
   done
 done
+}
+
+# FIR8 spectra with Ho at a 128-byte-aligned offset vs the HEAD library (libmsgpu_head.so): bits, FIR tests, C3 and FIR-point A/B
+ho_check() {
+timeout -k 10 300 python tools/bits_ab.py audio-suite_amd/msgpu/libmsgpu_head.so > gpurun_out/r06ho_bits.json 2>/dev/null; echo "bits rc=$?"; cat gpurun_out/r06ho_bits.json
+timeout -k 10 400 python -u -m pytest tests/test_gpu_fir.py tests/test_gpu_long_filters.py -m gpu -x -q --timeout 200 --timeout-method thread > gpurun_out/r06ho_tests.txt 2>&1; rc=$?; echo "tests rc=$rc"; tail -2 gpurun_out/r06ho_tests.txt
+[ $rc -gt 1 ] && exit $rc
+bash tools/ab_env.sh r06ho "new|MSGPU_X=1|base" "old|MSGPU_X=1|head" "new2|MSGPU_X=1|base" "old2|MSGPU_X=1|head"
+for lib in base head; do
+  if [ $lib = base ]; then le=""; else le="MSGPU_LIB=$PWD/audio-suite_amd/msgpu/libmsgpu_head.so"; fi
+  env $le timeout -k 10 300 python bench.py --no-cpu --points= --steps 5 --from-dicts-steps 0 --iso-steps 0 > gpurun_out/r06ho_fir_$lib.json 2>/dev/null || exit $?
+  python3 -c "
+import json; d=json.load(open('gpurun_out/r06ho_fir_$lib.json')); print('$lib', {k: (v['ms_per_step'], v['roofline']['frac'], v['check']['all_ok']) for k, v in d['points'].items()})"
+done
+}
+
+# k_fir8q carry slot: nontemporal stores (nt1) / stores + loads (nt3) vs product, FIR points, alternating
+q2nt_ab() {
+L=$PWD/audio-suite_amd/msgpu
+for rep in 1 2 3; do
+  for lib in base nt1 nt3; do
+    if [ $lib = base ]; then le=""; else le="MSGPU_LIB=$L/libmsgpu_$lib.so"; fi
+    env $le timeout -k 10 300 python bench.py --no-cpu --points= --steps 5 --from-dicts-steps 0 --iso-steps 0 > gpurun_out/r06nt_$lib$rep.json 2>/dev/null || exit $?
+    python3 -c "
+import json; d=json.load(open('gpurun_out/r06nt_$lib$rep.json')); print('$lib$rep', {k: (v['ms_per_step'], v['roofline']['frac'], v['check']['all_ok']) for k, v in d['points'].items() if k.startswith('FIR')})"
+  done
+done
+}
+
+# maxbits zeroed through the batch upload (no fill launch): bits, stereo / peak tests, H48 and C3 A/B vs HEAD lib
+mb_check() {
+timeout -k 10 300 python tools/bits_ab.py audio-suite_amd/msgpu/libmsgpu_head.so > gpurun_out/r06mb_bits.json 2>/dev/null || exit $?
+python3 -c "import json; d=json.load(open('gpurun_out/r06mb_bits.json')); print('identical', d['identical'], d['differing_presets'])"
+timeout -k 10 500 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > gpurun_out/r06mb_tests.txt 2>&1; rc=$?
+echo "tests rc=$rc"; tail -2 gpurun_out/r06mb_tests.txt
+[ $rc -ne 0 ] && exit $rc
+bash tools/h48_ab.sh r06mb libmsgpu.so libmsgpu_head.so || exit $?
+bash tools/ab_env.sh r06mb "new|MSGPU_X=1|base" "old|MSGPU_X=1|head" "new2|MSGPU_X=1|base" "old2|MSGPU_X=1|head"
 }
 
 name=${1:?usage: tools/round6_ab.sh NAME [args]}; shift
