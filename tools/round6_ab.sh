@@ -2,7 +2,7 @@
 # GPU box: the round-6 A/B and diagnostic sessions, one function each (their
 # records are under profiles/r06*; DESIGN section 9 cites them).
 #   usage (on the box): bash tools/round6_ab.sh NAME [args]
-# NAME: c3_streams c3_streams32 h48_host_diag h48_numa_diag h48_sched gate_points_ab gate_c3_ab h48_streams_ab prof_every_ab prof_every_ab2 h48_warmup_ab sub_sweep s3p_check fir8_cus_stamps ho_check q2nt_ab mb_check
+# NAME: c3_streams c3_streams32 h48_host_diag h48_numa_diag h48_sched gate_points_ab gate_c3_ab h48_streams_ab prof_every_ab prof_every_ab2 h48_warmup_ab sub_sweep s3p_check fir8_cus_stamps ho_check q2nt_ab mb_check c5_sub_ab
 set -o pipefail
 mkdir -p gpurun_out
 
@@ -289,6 +289,19 @@ echo "tests rc=$rc"; tail -2 gpurun_out/r06mb_tests.txt
 [ $rc -ne 0 ] && exit $rc
 bash tools/h48_ab.sh r06mb libmsgpu.so libmsgpu_head.so || exit $?
 bash tools/ab_env.sh r06mb "new|MSGPU_X=1|base" "old|MSGPU_X=1|head" "new2|MSGPU_X=1|base" "old2|MSGPU_X=1|head"
+}
+
+# C5 sub-batch size: 171 (6 = 2 per stream, the default) vs 114 (9 = 3 per stream), alternating
+c5_sub_ab() {
+for i in ${C5_REPS:-1 2}; do
+  for sub in ${C5_SUBS:-171 114}; do
+    timeout -k 10 300 python bench.py --config C5 --no-cpu --points= --fir-points= --steps 3 --warmup 1 --iso-steps 0 \
+      --from-dicts-steps 0 --sub $sub > gpurun_out/r06c5s_${sub}_$i.json 2> gpurun_out/r06c5s_${sub}_$i.log || exit $?
+    python3 -c "
+import json; d=json.load(open('gpurun_out/r06c5s_${sub}_$i.json'))
+print('C5 sub $sub', $i, d['ms_per_step'], d['checked']['all_ok'], d['config'].get('sub_batches_per_gpu'), d['config'].get('stream_gate'))"
+  done
+done
 }
 
 name=${1:?usage: tools/round6_ab.sh NAME [args]}; shift
