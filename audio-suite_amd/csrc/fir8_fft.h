@@ -597,7 +597,8 @@ MSG_DEV void q2_pair(float2 xk, float2 xm, float2 h0k, float2 h0m, float2 h1k, f
 // (sixteen carries beside v, b and the accumulators: scratch spills).  Measured
 // at 64 k taps per 1024 x 384 000 (profiles/r06h_fir8q_prefetch_ab.txt): 0 pairs
 // ahead 2.89 / 2.90 ms, 2 ahead 2.96 / 2.94, 4 ahead 3.14 / 3.10 (each pair
-// ahead costs 16 B of scratch spills per lane)
+// ahead costs 16 B of scratch spills per lane); 1 ahead 2.92 vs 2.88 – 2.90
+// (profiles/r06a1_fir8q_ahead1_ab.txt)
 #ifndef MSG_Q2_AHEAD
 #define MSG_Q2_AHEAD 0
 #endif

@@ -2,7 +2,7 @@
 # GPU box: the round-6 A/B and diagnostic sessions, one function each (their
 # records are under profiles/r06*; DESIGN section 9 cites them).
 #   usage (on the box): bash tools/round6_ab.sh NAME [args]
-# NAME: c3_streams c3_streams32 h48_host_diag h48_numa_diag h48_sched gate_points_ab gate_c3_ab h48_streams_ab prof_every_ab prof_every_ab2 h48_warmup_ab sub_sweep s3p_check fir8_cus_stamps ho_check q2nt_ab mb_check c5_sub_ab
+# NAME: c3_streams c3_streams32 h48_host_diag h48_numa_diag h48_sched gate_points_ab gate_c3_ab h48_streams_ab prof_every_ab prof_every_ab2 h48_warmup_ab sub_sweep s3p_check fir8_cus_stamps ho_check q2nt_ab mb_check c5_sub_ab q2_ahead1_ab
 set -o pipefail
 mkdir -p gpurun_out
 
@@ -300,6 +300,19 @@ for i in ${C5_REPS:-1 2}; do
     python3 -c "
 import json; d=json.load(open('gpurun_out/r06c5s_${sub}_$i.json'))
 print('C5 sub $sub', $i, d['ms_per_step'], d['checked']['all_ok'], d['config'].get('sub_batches_per_gpu'), d['config'].get('stream_gate'))"
+  done
+done
+}
+
+# k_fir8q with the carry loaded one pair ahead (libmsgpu_a1.so, MSG_Q2_AHEAD=1) vs product, FIR points, alternating
+q2_ahead1_ab() {
+L=$PWD/audio-suite_amd/msgpu
+for rep in 1 2 3; do
+  for lib in base a1; do
+    if [ $lib = base ]; then le=""; else le="MSGPU_LIB=$L/libmsgpu_$lib.so"; fi
+    env $le timeout -k 10 300 python bench.py --no-cpu --points= --steps 5 --from-dicts-steps 0 --iso-steps 0 > gpurun_out/r06a1_$lib$rep.json 2>/dev/null || exit $?
+    python3 -c "
+import json; d=json.load(open('gpurun_out/r06a1_$lib$rep.json')); print('$lib$rep', {k: (v['ms_per_step'], v['roofline']['frac'], v['check']['all_ok']) for k, v in d['points'].items() if k.startswith('FIR')})"
   done
 done
 }
